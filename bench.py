@@ -1,0 +1,132 @@
+#!/usr/bin/env python
+"""Headline benchmark: ProteinBERT pretraining throughput (sequences/s, whole job).
+
+Metric/config from BASELINE.json: "sequences/sec (whole node) ProteinBERT
+pretrain L=512 at 1/2/4/8 MI355X" on the 6-block paper config (C=128, G=512,
+K=64, H=4, A=8943), random-init weights, synthetic UniRef90-shaped sequences +
+GO multi-hot annotations generated and corrupted on the device every step.
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
+
+A timed step = synthetic batch generation + corruption, forward, loss,
+backward, bucketed RCCL all-reduce (N>1) and the fused Adam update.
+Rank 0 prints ONE JSON line; the time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from proteinbert_pytorch_replication_amd.config import get_preset  # noqa: E402
+from proteinbert_pytorch_replication_amd.models import ProteinBERT  # noqa: E402
+from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO  # noqa: E402
+from proteinbert_pytorch_replication_amd.parallel import dist as pdist  # noqa: E402
+from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce  # noqa: E402
+from proteinbert_pytorch_replication_amd.train.optim import FusedAdam  # noqa: E402
+from proteinbert_pytorch_replication_amd.train.step import PretrainStep  # noqa: E402
+
+METRIC = "sequences/sec (whole node) ProteinBERT pretrain L=512 at 1/2/4/8 MI355X"
+PAPER_IMPLIED_SEQ_PER_S = 277.0  # 670M sequences / 28 days on one RTX 5000
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: preset)")
+    ap.add_argument("--seq-len", type=int, default=None)
+    ap.add_argument("--preset", default="cfg2_paper_l512")
+    ap.add_argument("--impl", default="hip", choices=["hip", "torch", "faithful"],
+                    help="hip: fused CDNA4 kernels; torch: eager bf16 oracle; faithful: reference math, eager fp32")
+    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--seed", type=int, default=0)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    info = pdist.init_distributed()
+    if info.world_size != a.gpus and not (a.gpus == 1 and info.world_size == 1):
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
+    dev = info.device
+    cfg = get_preset(a.preset)
+    mcfg = cfg.model
+    L = a.seq_len or mcfg.sequences_length
+    B = a.batch or cfg.train.batch_size
+    torch.manual_seed(a.seed)
+    backend = "hip" if a.impl == "hip" else "torch"
+    model = ProteinBERT(sequences_length=L, num_annotations=mcfg.num_annotations, local_dim=mcfg.local_dim,
+                        global_dim=mcfg.global_dim, key_dim=mcfg.key_dim, num_heads=mcfg.num_heads,
+                        num_blocks=mcfg.num_blocks, device=dev, backend=backend)
+    opt = FusedAdam(model.parameters(), lr=2e-4)
+    ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb) if info.distributed else None
+    if ddp is not None:
+        ddp.broadcast_parameters(model)
+    dtype = torch.float32 if a.impl == "faithful" else torch.bfloat16
+    step = PretrainStep(model, opt, ddp, compute_dtype=dtype)
+    if a.impl == "faithful":
+        # reference computation as written: literal Q/K/softmax attention, fp32, eager
+        orig = step.loss
+
+        def faithful_loss(X, Y, W, return_parts=False):
+            from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
+            h, g = model.encode_torch(X["local"], X["global"], torch.float32, faithful_attention=True)
+            pl, pg = model.heads_torch(h, g)
+            return pretrain_loss_torch(pl, pg, Y, W)
+        step.loss = faithful_loss
+        _ = orig
+    gen = SyntheticUniRefGO(L, mcfg.num_annotations, B, dev, seed=a.seed + 1000 * info.rank)
+
+    def one():
+        X, Y, W = gen.next_batch()
+        return step(X, Y, W)
+
+    for _ in range(a.warmup):
+        loss = one()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = one()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    dt = pdist.all_reduce_max(dt, dev)
+    final_loss = float(loss.item())
+    n = info.world_size
+    value = n * B * a.steps / dt
+    if info.is_main:
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "sequences/s", "n_gpus": n,
+               "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3),
+               "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": round(value / PAPER_IMPLIED_SEQ_PER_S, 2),
+               "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+               "data": "synthetic (on-device UniRef90-shaped sequences + 8943-dim GO multi-hot, random-init weights)",
+               "config": {"model": f"ProteinBERT paper config: {mcfg.num_blocks} blocks, d_local={mcfg.local_dim}, "
+                                   f"d_global={mcfg.global_dim}, key_dim={mcfg.key_dim}, heads={mcfg.num_heads}, "
+                                   f"annotations={mcfg.num_annotations}, semantics=reference",
+                          "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
+                          "impl": a.impl},
+               "final_loss": round(final_loss, 5)}
+        print(json.dumps(out), flush=True)
+    pdist.destroy()
+
+
+if __name__ == "__main__":
+    main()

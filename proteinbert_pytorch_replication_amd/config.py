@@ -1,0 +1,191 @@
+"""Typed configuration for models, data, optimisation, distribution and kernels.
+
+The reference has no central config: model knobs are constructor kwargs
+(reference ``ProteinBERT/modules.py:235-246``), trainer knobs are ``pretrain``
+kwargs (``ProteinBERT/utils.py:220-231``) and driver constants live in
+``ProteinBERT/dummy_tests.py:16-19``.  Here they are dataclasses with named
+presets for the five BASELINE configurations, loadable from YAML and
+overridable from the command line with ``section.key=value`` strings.
+"""
+from __future__ import annotations
+
+import dataclasses
+from dataclasses import dataclass, field, asdict
+from typing import Any, Dict, List, Optional
+
+NUM_GO_ANNOTATIONS = 8943  # reference dummy_tests.py:17 / paper
+
+
+@dataclass
+class ModelConfig:
+    sequences_length: int = 512
+    num_annotations: int = NUM_GO_ANNOTATIONS
+    local_dim: int = 128
+    global_dim: int = 512
+    key_dim: int = 64
+    num_heads: int = 4
+    num_blocks: int = 6
+    conv_kernel_size: int = 9
+    wide_conv_dilation: int = 5
+    vocab_size: int = 26
+    # "reference": bit-for-bit the reference's math (batch-axis local softmax,
+    # degenerate attention softmax, CE applied to probabilities, LN over (L, C)).
+    # "paper": the published ProteinBERT intent (softmax over L in attention,
+    # softmax over the vocabulary, CE on logits, per-position LN over C).
+    semantics: str = "reference"
+
+    def kwargs(self) -> Dict[str, Any]:
+        d = asdict(self)
+        return d
+
+
+@dataclass
+class DataConfig:
+    source: str = "synthetic"          # synthetic | dataframe | hdf5
+    path: Optional[str] = None
+    token_corruption_p: float = 0.05    # data_processing.py:156
+    annotation_positive_p: float = 0.25  # data_processing.py:157
+    annotation_negative_p: float = 1e-4
+    blank_annotation_p: float = 0.5     # data_processing.py:127
+    min_length: int = 0                 # dummy_tests.py:27 lengths U[0, 250]
+    max_length: Optional[int] = None    # None -> sequences_length + 64 (forces crops)
+    annotation_density: float = 0.005   # dummy_tests.py:34
+    num_workers: int = 0
+    seed: int = 0
+
+
+@dataclass
+class OptimConfig:
+    lr: float = 2e-4                    # dummy_tests.py:127-130
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    weight_decay: float = 0.0
+    warmup_duration: int = 10000        # utils.py:229
+    plateau_patience: int = 25          # utils.py:228
+    plateau_factor: float = 0.1
+    grad_clip: Optional[float] = None   # pretrain has none (utils.py:220-345)
+
+
+@dataclass
+class DistConfig:
+    backend: str = "auto"               # auto -> nccl (RCCL) on GPU, gloo on CPU
+    bucket_mb: float = 8.0              # sized for 7 xGMI links (see parallel/ddp.py)
+    comm_dtype: str = "fp32"            # fp32 | bf16 gradient all-reduce
+    timeout_s: int = 600
+
+
+@dataclass
+class KernelConfig:
+    backend: str = "auto"               # auto | hip | torch
+    dtype: str = "bf16"                 # compute dtype on GPU
+    hip_graph: bool = False             # capture the whole train step
+
+
+@dataclass
+class TrainConfig:
+    batch_size: int = 32                # per rank
+    max_batch_iterations: int = 250
+    nb_iterations_checkpoint: int = 1000
+    log_every: int = 1
+    save_path: str = "."
+    seed: int = 0
+
+
+@dataclass
+class RunConfig:
+    model: ModelConfig = field(default_factory=ModelConfig)
+    data: DataConfig = field(default_factory=DataConfig)
+    optim: OptimConfig = field(default_factory=OptimConfig)
+    dist: DistConfig = field(default_factory=DistConfig)
+    kernel: KernelConfig = field(default_factory=KernelConfig)
+    train: TrainConfig = field(default_factory=TrainConfig)
+    name: str = "custom"
+
+    def to_dict(self) -> Dict[str, Any]:
+        return asdict(self)
+
+
+def _paper_model(L: int) -> ModelConfig:
+    return ModelConfig(sequences_length=L, local_dim=128, global_dim=512, key_dim=64,
+                       num_heads=4, num_blocks=6)
+
+
+# The five configurations named in BASELINE.json.
+PRESETS: Dict[str, RunConfig] = {
+    "cfg1_cpu_smoke": RunConfig(
+        name="cfg1_cpu_smoke",
+        model=ModelConfig(sequences_length=128, local_dim=64, global_dim=256, key_dim=64,
+                          num_heads=4, num_blocks=2),
+        kernel=KernelConfig(backend="torch", dtype="fp32"),
+        train=TrainConfig(batch_size=4)),
+    "cfg2_paper_l512": RunConfig(
+        name="cfg2_paper_l512", model=_paper_model(512),
+        train=TrainConfig(batch_size=256)),
+    "cfg3_paper_l1024_dp8": RunConfig(
+        name="cfg3_paper_l1024_dp8", model=_paper_model(1024),
+        train=TrainConfig(batch_size=128)),
+    "cfg4_long_l4096_dp8": RunConfig(
+        name="cfg4_long_l4096_dp8", model=_paper_model(4096),
+        train=TrainConfig(batch_size=32)),
+    "cfg5_finetune_ss_l512_dp8": RunConfig(
+        name="cfg5_finetune_ss_l512_dp8", model=_paper_model(512),
+        train=TrainConfig(batch_size=256)),
+    # the reference's own smoke driver (dummy_tests.py:102-118)
+    "dummy_tests": RunConfig(
+        name="dummy_tests", model=_paper_model(256),
+        train=TrainConfig(batch_size=32, max_batch_iterations=250)),
+}
+
+
+def get_preset(name: str) -> RunConfig:
+    if name not in PRESETS:
+        raise KeyError(f"unknown preset {name!r}; known: {sorted(PRESETS)}")
+    return dataclasses.replace(PRESETS[name])  # shallow copy; sections replaced on override
+
+
+def _coerce(old: Any, text: str) -> Any:
+    if isinstance(old, bool):
+        return text.lower() in ("1", "true", "yes", "on")
+    if isinstance(old, int) and not isinstance(old, bool):
+        return int(text)
+    if isinstance(old, float):
+        return float(text)
+    if isinstance(old, tuple):
+        return tuple(float(x) for x in text.strip("()").split(","))
+    if old is None:
+        for cast in (int, float):
+            try:
+                return cast(text)
+            except ValueError:
+                pass
+        return None if text.lower() == "none" else text
+    return text
+
+
+def apply_overrides(cfg: RunConfig, overrides: List[str]) -> RunConfig:
+    """Apply ``section.key=value`` overrides (e.g. ``model.num_blocks=2``)."""
+    for ov in overrides:
+        if "=" not in ov:
+            raise ValueError(f"override {ov!r} is not section.key=value")
+        key, value = ov.split("=", 1)
+        section, _, attr = key.partition(".")
+        sub = getattr(cfg, section)
+        if not hasattr(sub, attr):
+            raise KeyError(f"{section} has no field {attr!r}")
+        new_sub = dataclasses.replace(sub, **{attr: _coerce(getattr(sub, attr), value)})
+        setattr(cfg, section, new_sub)
+    return cfg
+
+
+def load_yaml(path: str) -> RunConfig:
+    import yaml
+    with open(path) as f:
+        raw = yaml.safe_load(f) or {}
+    cfg = get_preset(raw.pop("preset")) if "preset" in raw else RunConfig()
+    for section, values in raw.items():
+        if section == "name":
+            cfg.name = values
+            continue
+        sub = getattr(cfg, section)
+        setattr(cfg, section, dataclasses.replace(sub, **values))
+    return cfg

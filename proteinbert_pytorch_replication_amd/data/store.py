@@ -1,0 +1,182 @@
+"""On-disk pretraining dataset store (the E3 layout).
+
+The reference writes HDF5 with root-level datasets
+(``ProteinBERT/uniref_dataset.py:236-245``)::
+
+    included_annotations[n_ann] str, uniprot_ids[n] str, seqs[n] str,
+    seq_lengths[n] int32, annotation_masks[n, n_ann] bool
+
+h5py is not importable in this image, so two interchangeable backends exist:
+
+* ``.h5``     - the exact reference layout, used when h5py is importable;
+* ``.pbxds``  - a directory of memory-mappable ``.npy`` arrays with the same
+  fields (sequence bytes + offsets, bit-packed annotation masks).  It is what
+  the native batch builder (``ops/csrc/pbx_loader.cpp``) reads without
+  Python in the loop.
+
+Both expose the same :class:`ProteinStore` reader API.
+"""
+from __future__ import annotations
+
+import json
+import os
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+try:  # pragma: no cover - h5py is absent in the build image
+    import h5py  # type: ignore
+except Exception:  # noqa: BLE001
+    h5py = None
+
+PBXDS_VERSION = 1
+
+
+def has_h5py() -> bool:
+    return h5py is not None
+
+
+class ProteinStore:
+    """Random-access reader. Use :meth:`open`."""
+
+    @staticmethod
+    def open(path: str) -> "ProteinStore":
+        if os.path.isdir(path) and os.path.exists(os.path.join(path, "meta.json")):
+            return PbxdsStore(path)
+        if path.endswith((".h5", ".hdf5")):
+            if h5py is None:
+                raise RuntimeError(f"{path} is HDF5 but h5py is not importable; convert it to .pbxds")
+            return H5Store(path)
+        raise FileNotFoundError(f"no dataset store at {path}")
+
+    # interface
+    def __len__(self) -> int: ...
+    def seq(self, i: int) -> str: ...
+    def annotation_mask(self, i: int) -> np.ndarray: ...
+    def uniprot_id(self, i: int) -> str: ...
+    included_annotations: List[str]
+
+
+class PbxdsStore(ProteinStore):
+    def __init__(self, path: str):
+        self.path = path
+        with open(os.path.join(path, "meta.json")) as f:
+            self.meta = json.load(f)
+        if self.meta.get("version") != PBXDS_VERSION:
+            raise ValueError(f"unsupported .pbxds version {self.meta.get('version')}")
+        ld = lambda name: np.load(os.path.join(path, name), mmap_mode="r", allow_pickle=False)  # noqa: E731
+        self.seq_offsets = ld("seq_offsets.npy")
+        self.seq_bytes = ld("seq_bytes.npy")
+        self.seq_lengths = ld("seq_lengths.npy")
+        self.annotation_bits = ld("annotation_bits.npy")
+        self.id_offsets = ld("id_offsets.npy")
+        self.id_bytes = ld("id_bytes.npy")
+        self.n_annotations = int(self.meta["n_annotations"])
+        self.included_annotations = list(self.meta["included_annotations"])
+
+    def __len__(self) -> int:
+        return int(self.meta["n"])
+
+    def seq(self, i: int) -> str:
+        a, b = int(self.seq_offsets[i]), int(self.seq_offsets[i + 1])
+        return bytes(self.seq_bytes[a:b]).decode("ascii")
+
+    def annotation_mask(self, i: int) -> np.ndarray:
+        bits = np.unpackbits(np.asarray(self.annotation_bits[i]), bitorder="little")
+        return bits[:self.n_annotations].astype(bool)
+
+    def uniprot_id(self, i: int) -> str:
+        a, b = int(self.id_offsets[i]), int(self.id_offsets[i + 1])
+        return bytes(self.id_bytes[a:b]).decode("utf-8")
+
+
+class H5Store(ProteinStore):  # pragma: no cover - needs h5py
+    def __init__(self, path: str):
+        self.f = h5py.File(path, "r")
+        self.included_annotations = [x.decode() if isinstance(x, bytes) else str(x)
+                                     for x in self.f["included_annotations"][:]]
+        self.n_annotations = len(self.included_annotations)
+
+    def __len__(self) -> int:
+        return int(self.f["seqs"].shape[0])
+
+    def seq(self, i: int) -> str:
+        s = self.f["seqs"][i]
+        return s.decode() if isinstance(s, bytes) else str(s)
+
+    def annotation_mask(self, i: int) -> np.ndarray:
+        return np.asarray(self.f["annotation_masks"][i], dtype=bool)
+
+    def uniprot_id(self, i: int) -> str:
+        s = self.f["uniprot_ids"][i]
+        return s.decode() if isinstance(s, bytes) else str(s)
+
+
+class ProteinStoreWriter:
+    """Chunked writer for the E3 layout (reference ``create_h5_dataset`` pass 2,
+    ``uniref_dataset.py:249-268``).  ``fmt`` = ``pbxds`` | ``h5``."""
+
+    def __init__(self, path: str, included_annotations: Sequence[str], fmt: str = "auto"):
+        if fmt == "auto":
+            fmt = "h5" if path.endswith((".h5", ".hdf5")) else "pbxds"
+        if fmt == "h5" and h5py is None:
+            raise RuntimeError("h5py is not importable; write the .pbxds format instead")
+        self.path, self.fmt = path, fmt
+        self.included_annotations = list(included_annotations)
+        self.n_ann = len(self.included_annotations)
+        self._seqs: List[bytes] = []
+        self._ids: List[bytes] = []
+        self._bits: List[np.ndarray] = []
+
+    def append(self, uniprot_id: str, seq: str, annotation_indices: Iterable[int]) -> None:
+        mask = np.zeros(self.n_ann, dtype=bool)
+        idx = np.fromiter((int(i) for i in annotation_indices), dtype=np.int64)
+        if idx.size:
+            mask[idx] = True
+        self._ids.append(uniprot_id.encode("utf-8"))
+        self._seqs.append(seq.encode("ascii"))
+        self._bits.append(np.packbits(mask, bitorder="little"))
+
+    def __len__(self) -> int:
+        return len(self._seqs)
+
+    def close(self) -> None:
+        if self.fmt == "pbxds":
+            self._write_pbxds()
+        else:  # pragma: no cover
+            self._write_h5()
+
+    def _write_pbxds(self) -> None:
+        os.makedirs(self.path, exist_ok=True)
+        n = len(self._seqs)
+        lens = np.array([len(s) for s in self._seqs], dtype=np.int64)
+        offs = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        id_lens = np.array([len(s) for s in self._ids], dtype=np.int64)
+        id_offs = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(id_lens, out=id_offs[1:])
+        nbytes = (self.n_ann + 7) // 8
+        bits = np.stack(self._bits) if n else np.zeros((0, nbytes), dtype=np.uint8)
+        sv = lambda name, arr: np.save(os.path.join(self.path, name), arr, allow_pickle=False)  # noqa: E731
+        sv("seq_offsets.npy", offs)
+        sv("seq_bytes.npy", np.frombuffer(b"".join(self._seqs), dtype=np.uint8))
+        sv("seq_lengths.npy", lens.astype(np.int32))
+        sv("annotation_bits.npy", bits)
+        sv("id_offsets.npy", id_offs)
+        sv("id_bytes.npy", np.frombuffer(b"".join(self._ids), dtype=np.uint8))
+        with open(os.path.join(self.path, "meta.json"), "w") as f:
+            json.dump({"version": PBXDS_VERSION, "n": n, "n_annotations": self.n_ann,
+                       "included_annotations": self.included_annotations}, f)
+
+    def _write_h5(self) -> None:  # pragma: no cover - needs h5py
+        n = len(self._seqs)
+        with h5py.File(self.path, "w") as f:
+            f.create_dataset("included_annotations", data=[a.encode() for a in self.included_annotations],
+                             dtype=h5py.string_dtype())
+            f.create_dataset("uniprot_ids", data=self._ids, dtype=h5py.string_dtype())
+            f.create_dataset("seqs", data=self._seqs, dtype=h5py.string_dtype())
+            f.create_dataset("seq_lengths", data=np.array([len(s) for s in self._seqs], dtype=np.int32))
+            masks = np.zeros((n, self.n_ann), dtype=bool)
+            for i, b in enumerate(self._bits):
+                masks[i] = np.unpackbits(b, bitorder="little")[:self.n_ann].astype(bool)
+            f.create_dataset("annotation_masks", data=masks, dtype=bool)

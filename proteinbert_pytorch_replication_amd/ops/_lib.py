@@ -1,0 +1,84 @@
+"""ctypes binding of the in-tree HIP library (``libpbx_hip.so``).
+
+The library must be loaded *after* ``import torch`` so that it binds to the
+HIP runtime torch already loaded (same ``libamdhip64.so.7`` soname).  Every
+launcher returns a ``hipError_t``; a non-zero code raises.  On a GPU box a
+missing library is an error, never a silent fallback to eager ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch
+
+from .build import HIP_LIB, HOST_LIB
+
+_P = ctypes.c_void_p
+_I64 = ctypes.c_int64
+_I32 = ctypes.c_int
+_F32 = ctypes.c_float
+
+# name -> argtypes (all return int hipError_t)
+_SIGS = {
+    "pbx_adam_flat": [_P, _P, _P, _P, _P, _I64, _P, _P, _P],
+    "pbx_sumsq_flat": [_P, _I64, _P, _P, _P],
+    "pbx_clip_scale_flat": [_P, _I64, _P, _F32, _P],
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_host: Optional[ctypes.CDLL] = None
+
+
+class HipError(RuntimeError):
+    pass
+
+
+def available() -> bool:
+    return os.path.exists(HIP_LIB)
+
+
+def register(name: str, argtypes) -> None:
+    """Kernel modules declare their launchers here (before first use)."""
+    _SIGS[name] = argtypes
+    if _lib is not None:
+        fn = getattr(_lib, name)
+        fn.argtypes, fn.restype = argtypes, ctypes.c_int
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(HIP_LIB):
+            raise HipError(f"HIP kernel library not built: {HIP_LIB}. "
+                           f"Run `python -m proteinbert_pytorch_replication_amd.ops.build`.")
+        _ = torch.cuda.is_available()  # make sure torch's HIP runtime is loaded first
+        _lib = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_LOCAL)
+        for name, args in _SIGS.items():
+            fn = getattr(_lib, name)
+            fn.argtypes, fn.restype = args, ctypes.c_int
+    return _lib
+
+
+def host_lib() -> ctypes.CDLL:
+    global _host
+    if _host is None:
+        if not os.path.exists(HOST_LIB):
+            raise HipError(f"host library not built: {HOST_LIB}")
+        _host = ctypes.CDLL(HOST_LIB, mode=ctypes.RTLD_LOCAL)
+    return _host
+
+
+def stream_ptr(device: Optional[torch.device] = None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise HipError(f"{name} failed with hipError {rc}")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()

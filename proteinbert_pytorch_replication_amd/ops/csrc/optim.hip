@@ -1,0 +1,131 @@
+// Flat-arena optimizer kernels.
+//
+// The reference runs torch.optim.Adam over 133 tensors (~1,066 foreach kernel
+// launches per step).  Here every parameter lives in ONE fp32
+// arena, so the whole update is one memory-bound launch (16 B/lane vector
+// loads), hyper-parameters are read from device memory (the step is
+// hipGraph-capturable), and a device-side "skip" flag drops the update when
+// the loss was non-finite without a host sync.  Math is exactly torch Adam
+// (non-decoupled weight decay, denom = sqrt(v)/sqrt(bc2) + eps).
+#include "common.h"
+
+struct AdamHParams {  // device-resident, float32
+  float lr, beta1, beta2, eps, weight_decay, bias_correction1, bias_correction2_sqrt, grad_scale;
+};
+
+__device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, const AdamHParams& h) {
+  g = g * h.grad_scale + h.weight_decay * p;
+  m = h.beta1 * m + (1.0f - h.beta1) * g;
+  v = h.beta2 * v + (1.0f - h.beta2) * g * g;
+  const float denom = sqrtf(v) / h.bias_correction2_sqrt + h.eps;
+  p -= (h.lr / h.bias_correction1) * (m / denom);
+}
+
+// Optional bf16 shadow (nullptr to skip): written from the updated fp32 master.
+__global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                        float* __restrict__ m, float* __restrict__ v,
+                                                        unsigned short* __restrict__ shadow, int64_t n,
+                                                        const AdamHParams* __restrict__ hp,
+                                                        const int* __restrict__ skip) {
+  if (skip != nullptr && *skip != 0) return;
+  const AdamHParams h = *hp;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    adam_one(pp.x, gg.x, mm.x, vv.x, h);
+    adam_one(pp.y, gg.y, mm.y, vv.y, h);
+    adam_one(pp.z, gg.z, mm.z, vv.z, h);
+    adam_one(pp.w, gg.w, mm.w, vv.w, h);
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (shadow != nullptr) {
+      ushort4 s;
+      s.x = f2bf(pp.x); s.y = f2bf(pp.y); s.z = f2bf(pp.z); s.w = f2bf(pp.w);
+      reinterpret_cast<ushort4*>(shadow)[i] = s;
+    }
+  }
+  // tail
+  const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && blockIdx.x * blockDim.x + threadIdx.x < 4) {
+    float pp = p[t], mm = m[t], vv = v[t];
+    adam_one(pp, g[t], mm, vv, h);
+    p[t] = pp; m[t] = mm; v[t] = vv;
+    if (shadow != nullptr) shadow[t] = f2bf(pp);
+  }
+}
+
+PBX_EXPORT int pbx_adam_flat(float* p, const float* g, float* m, float* v, void* shadow_bf16, int64_t n,
+                             const void* hparams, const int* skip, hipStream_t stream) {
+  if (n <= 0) return 0;
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v,
+                     (unsigned short*)shadow_bf16, n, (const AdamHParams*)hparams, skip);
+  return pbx_launch_status();
+}
+
+// ---- global L2 norm of a flat buffer (clip_grad_norm_) --------------------------
+// Two passes in one launch sequence: per-block partial sums of squares -> out[blocks],
+// then a single-block reduce into out_total[0].  Deterministic (fixed tree).
+__global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restrict__ x, int64_t n,
+                                                            float* __restrict__ partial) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const float4 a = reinterpret_cast<const float4*>(x)[i];
+    acc += a.x * a.x + a.y * a.y + a.z * a.z + a.w * a.w;
+  }
+  const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && blockIdx.x * blockDim.x + threadIdx.x < 4) acc += x[t] * x[t];
+  acc = wave_reduce_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void __launch_bounds__(256) sumsq_final_kernel(const float* __restrict__ partial, int nb,
+                                                          float* __restrict__ out) {
+  __shared__ float red[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) acc += partial[i];
+  acc = wave_reduce_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = red[0] + red[1] + red[2] + red[3];
+}
+
+// workspace must hold 1024 floats
+PBX_EXPORT int pbx_sumsq_flat(const float* x, int64_t n, float* workspace, float* out, hipStream_t stream) {
+  int64_t blocks = ((n >> 2) + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, workspace);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, stream, workspace, (int)blocks, out);
+  return pbx_launch_status();
+}
+
+// x *= min(1, max_norm / (sqrt(sumsq) + 1e-6))   (torch.nn.utils.clip_grad_norm_ semantics)
+__global__ void __launch_bounds__(256) clip_scale_kernel(float* __restrict__ x, int64_t n,
+                                                         const float* __restrict__ sumsq, float max_norm) {
+  const float norm = sqrtf(*sumsq);
+  const float c = max_norm / (norm + 1e-6f);
+  if (c >= 1.0f) return;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= c;
+}
+
+PBX_EXPORT int pbx_clip_scale_flat(float* x, int64_t n, const float* sumsq, float max_norm, hipStream_t stream) {
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(clip_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, sumsq, max_norm);
+  return pbx_launch_status();
+}

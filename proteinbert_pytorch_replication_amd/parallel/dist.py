@@ -1,0 +1,119 @@
+"""Process-group bootstrap: one process per GPU, RCCL over xGMI.
+
+The reference has no distributed code at all.  This module
+reads the ``torchrun`` environment (``RANK``, ``WORLD_SIZE``,
+``LOCAL_RANK``, ``MASTER_ADDR``/``MASTER_PORT``), pins the process to
+``cuda:LOCAL_RANK`` and opens a ``"nccl"`` process group — which *is* RCCL on
+ROCm.  ``gloo`` is used only when no GPU is present (CPU unit tests).
+``HSA_ENABLE_IPC_MODE_LEGACY=0`` is kept (dmabuf IPC is the only mode the
+host driver supports).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistInfo:
+    rank: int = 0
+    world_size: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str = "none"
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+_INFO: Optional[DistInfo] = None
+
+
+def env_world() -> DistInfo:
+    return DistInfo(rank=int(os.environ.get("RANK", 0)), world_size=int(os.environ.get("WORLD_SIZE", 1)),
+                    local_rank=int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Optional[str] = None) -> DistInfo:
+    """Idempotent.  With WORLD_SIZE==1 no process group is created."""
+    global _INFO
+    if _INFO is not None:
+        return _INFO
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    info = env_world()
+    use_gpu = torch.cuda.is_available() and device != "cpu"
+    if use_gpu:
+        torch.cuda.set_device(info.local_rank)
+        info.device = torch.device("cuda", info.local_rank)
+    else:
+        info.device = torch.device("cpu")
+    if info.world_size > 1:
+        if backend == "auto":
+            backend = "nccl" if use_gpu else "gloo"
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = info.device
+        if not dist.is_initialized():
+            dist.init_process_group(**kw)
+        info.backend = backend
+    _INFO = info
+    return info
+
+
+def get_info() -> DistInfo:
+    return _INFO if _INFO is not None else env_world()
+
+
+def is_main() -> bool:
+    return get_info().rank == 0
+
+
+def barrier() -> None:
+    if dist.is_available() and dist.is_initialized():
+        if dist.get_backend() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_reduce_max(x: float, device: Optional[torch.device] = None) -> float:
+    if not (dist.is_available() and dist.is_initialized()):
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or get_info().device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def all_reduce_mean_(t: torch.Tensor) -> torch.Tensor:
+    if dist.is_available() and dist.is_initialized():
+        dist.all_reduce(t)
+        t /= dist.get_world_size()
+    return t
+
+
+def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
+    """Make every rank start from rank 0's parameters and buffers (incl. attention heads)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            dist.broadcast(t.data, src)
+
+
+def destroy() -> None:
+    global _INFO
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+    _INFO = None

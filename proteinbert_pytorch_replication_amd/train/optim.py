@@ -1,0 +1,173 @@
+"""Fused Adam over the flat arena.
+
+A drop-in ``torch.optim.Optimizer`` (so ``LambdaLR`` / ``ReduceLROnPlateau``
+drive it through ``param_groups[0]["lr"]``) whose ``step()`` is ONE HIP launch
+over every parameter (``pbx_adam_flat``).  Its ``state_dict()`` has exactly
+the format of ``torch.optim.Adam`` so reference-style checkpoints
+(``optimizer_state_dict``, ``ProteinBERT/utils.py:327-335``) load either way.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, Optional
+
+import torch
+
+from .arena import FlatArena
+
+
+def _hip_ok(t: torch.Tensor) -> bool:
+    if t.device.type != "cuda":
+        return False
+    from ..ops import _lib
+    if not _lib.available():
+        raise _lib.HipError("GPU run but the HIP kernel library is not built; run ops.build")
+    return True
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
+                 weight_decay: float = 0.0, arena: Optional[FlatArena] = None, bf16_shadow: bool = False):
+        if isinstance(params, FlatArena):
+            arena, params = params, params.params
+        params = [p for p in params if p.requires_grad]
+        defaults = dict(lr=lr, betas=tuple(betas), eps=eps, weight_decay=weight_decay, amsgrad=False,
+                        maximize=False, foreach=None, capturable=False, differentiable=False, fused=None,
+                        decoupled_weight_decay=False)
+        super().__init__(params, defaults)
+        if len(self.param_groups) != 1:
+            raise ValueError("FusedAdam supports one param group (the flat arena)")
+        self.arena = arena if arena is not None else FlatArena(self.param_groups[0]["params"])
+        a = self.arena
+        self.exp_avg = torch.zeros_like(a.data)
+        self.exp_avg_sq = torch.zeros_like(a.data)
+        self.shadow = torch.zeros(a.numel, dtype=torch.bfloat16, device=a.data.device) if bf16_shadow else None
+        self.step_count = 0
+        self.grad_scale = 1.0   # set to 1/world by the DP wrapper (SUM all-reduce -> mean)
+        self.skip_flag: Optional[torch.Tensor] = None  # device int32; non-zero -> skip update
+        dev = a.data.device
+        self._hp_dev = torch.zeros(8, dtype=torch.float32, device=dev)
+        # ring of pinned staging buffers: the host never rewrites a buffer whose async H2D copy
+        # may still be queued behind GPU work
+        self._hp_ring = [torch.zeros(8, dtype=torch.float32, pin_memory=dev.type == "cuda") for _ in range(4)]
+        self._hp_events = [None] * 4
+        self._index = {id(p): a.param_index()[id(p)] for p in self.param_groups[0]["params"]}
+
+    # ---------------------------------------------------------------------------------
+    def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002 - arena grads are views
+        self.arena.zero_grad()
+
+    def _hparams(self) -> torch.Tensor:
+        g = self.param_groups[0]
+        b1, b2 = g["betas"]
+        t = self.step_count
+        k = t % len(self._hp_ring)
+        if self._hp_events[k] is not None:
+            self._hp_events[k].synchronize()
+        h = self._hp_ring[k]
+        h[0] = g["lr"]
+        h[1] = b1
+        h[2] = b2
+        h[3] = g["eps"]
+        h[4] = g["weight_decay"]
+        h[5] = 1.0 - b1 ** t
+        h[6] = math.sqrt(1.0 - b2 ** t)
+        h[7] = self.grad_scale
+        return h
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = closure() if closure is not None else None
+        self.step_count += 1
+        a = self.arena
+        if not a.grads_attached():
+            a.attach_grads()
+        h = self._hparams()
+        if _hip_ok(a.data):
+            from ..ops import _lib
+            self._hp_dev.copy_(h, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._hp_events[self.step_count % len(self._hp_ring)] = ev
+            _lib.call("pbx_adam_flat", a.data.data_ptr(), a.grad.data_ptr(), self.exp_avg.data_ptr(),
+                      self.exp_avg_sq.data_ptr(), _lib.ptr(self.shadow), a.numel, self._hp_dev.data_ptr(),
+                      _lib.ptr(self.skip_flag), _lib.stream_ptr(a.data.device))
+        else:
+            lr, b1, b2, eps, wd, bc1, bc2s, gs = [float(x) for x in h.tolist()]
+            g = a.grad * gs
+            if wd != 0:
+                g = g + wd * a.data
+            m_new = self.exp_avg * b1 + (1 - b1) * g
+            v_new = self.exp_avg_sq * b2 + (1 - b2) * g * g
+            p_new = a.data - (lr / bc1) * m_new / (v_new.sqrt() / bc2s + eps)
+            if self.skip_flag is not None:
+                keep = self.skip_flag == 0
+                m_new = torch.where(keep, m_new, self.exp_avg)
+                v_new = torch.where(keep, v_new, self.exp_avg_sq)
+                p_new = torch.where(keep, p_new, a.data)
+            self.exp_avg.copy_(m_new)
+            self.exp_avg_sq.copy_(v_new)
+            a.data.copy_(p_new)
+            if self.shadow is not None:
+                self.shadow.copy_(a.data)
+        return loss
+
+    @torch.no_grad()
+    def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
+        """Global L2 grad-norm clip over the arena (after DP reduction); returns the pre-clip norm."""
+        a = self.arena
+        if _hip_ok(a.grad):
+            from ..ops import _lib
+            ws = torch.empty(1025, dtype=torch.float32, device=a.grad.device)
+            _lib.call("pbx_sumsq_flat", a.grad.data_ptr(), a.numel, ws.data_ptr(), ws[1024:].data_ptr(),
+                      _lib.stream_ptr(a.grad.device))
+            sumsq = ws[1024:] * (self.grad_scale ** 2)
+            _lib.call("pbx_clip_scale_flat", a.grad.data_ptr(), a.numel, sumsq.data_ptr(),
+                      float(max_norm / self.grad_scale), _lib.stream_ptr(a.grad.device))
+            return sumsq.sqrt()[0]
+        norm = (a.grad * self.grad_scale).norm()
+        c = max_norm / (norm + 1e-6)
+        if c < 1:
+            a.grad.mul_(c)
+        return norm
+
+    # ---------------------------------------------------------------------------------
+    def state_dict(self) -> Dict[str, Any]:
+        g = self.param_groups[0]
+        state = {}
+        if self.step_count > 0:
+            for i, p in enumerate(g["params"]):
+                o, n = self.arena.segment(self._index[id(p)])
+                state[i] = {"step": torch.tensor(float(self.step_count)),
+                            "exp_avg": self.exp_avg[o:o + n].view(p.shape).clone(),
+                            "exp_avg_sq": self.exp_avg_sq[o:o + n].view(p.shape).clone()}
+        group = {k: v for k, v in g.items() if k != "params"}
+        group["params"] = list(range(len(g["params"])))
+        return {"state": state, "param_groups": [group]}
+
+    @torch.no_grad()
+    def load_state_dict(self, state_dict: Dict[str, Any]) -> None:
+        g = self.param_groups[0]
+        groups = state_dict["param_groups"]
+        if len(groups) != 1 or len(groups[0]["params"]) != len(g["params"]):
+            raise ValueError("optimizer state does not match the parameter list")
+        for k, v in groups[0].items():
+            if k != "params":
+                g[k] = tuple(v) if k == "betas" else v
+        st = state_dict["state"]
+        steps = 0
+        for i, p in enumerate(g["params"]):
+            if i not in st and str(i) not in st:
+                continue
+            s = st[i] if i in st else st[str(i)]
+            o, n = self.arena.segment(self._index[id(p)])
+            self.exp_avg[o:o + n].copy_(s["exp_avg"].reshape(-1))
+            self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
+            steps = int(float(s["step"]))
+        self.step_count = steps
+
+
+def make_optimizer(model: torch.nn.Module, lr: float = 2e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                   weight_decay: float = 0.0, arena: Optional[FlatArena] = None) -> FusedAdam:
+    return FusedAdam(model.parameters() if arena is None else arena.params, lr=lr, betas=betas, eps=eps,
+                     weight_decay=weight_decay, arena=arena)

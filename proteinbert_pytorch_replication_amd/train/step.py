@@ -1,0 +1,74 @@
+"""One pretraining step: loss -> backward (+ overlapped DP all-reduce) -> fused Adam.
+
+Reference step body: ``ProteinBERT/utils.py:287-301`` (H2D copies, forward,
+weighted CE + BCE, ``.item()`` sync, zero_grad / backward / step).  Here the
+step never synchronises with the host: the loss stays on the device, the
+non-finite check is a device flag consumed by the fused Adam kernel, and on
+a GPU the forward/backward run through the fused HIP kernels
+(:mod:`..ops.fused_model`) with bf16 activations.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from .losses import pretrain_loss_torch, is_standard_loss_pair
+from .optim import FusedAdam
+
+
+def resolve_compute_dtype(spec, device: torch.device) -> torch.dtype:
+    if isinstance(spec, torch.dtype):
+        return spec
+    if spec in (None, "auto"):
+        return torch.bfloat16 if device.type == "cuda" else torch.float32
+    return {"bf16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32,
+            "bfloat16": torch.bfloat16}[spec]
+
+
+class PretrainStep:
+    def __init__(self, model, optimizer, ddp=None, local_loss_fn=None, global_loss_fn=None,
+                 compute_dtype="auto", grad_clip: Optional[float] = None, skip_nonfinite: bool = True):
+        self.model = model
+        self.optimizer = optimizer
+        self.ddp = ddp
+        self.local_loss_fn = local_loss_fn
+        self.global_loss_fn = global_loss_fn
+        self.standard_loss = is_standard_loss_pair(local_loss_fn, global_loss_fn)
+        self.device = next(model.parameters()).device
+        self.compute_dtype = resolve_compute_dtype(compute_dtype, self.device)
+        self.grad_clip = grad_clip
+        self.skip_nonfinite = skip_nonfinite
+        self.fused = isinstance(optimizer, FusedAdam)
+        if self.fused and ddp is not None and ddp.enabled:
+            optimizer.grad_scale = 1.0 / ddp.world
+
+    def loss(self, X: Dict[str, torch.Tensor], Y: Dict[str, torch.Tensor], W: Dict[str, torch.Tensor],
+             return_parts: bool = False):
+        m = self.model
+        if m.resolved_backend(self.device) == "hip" and self.standard_loss:
+            from ..ops.fused_model import fused_pretrain_loss
+            return fused_pretrain_loss(m, X, Y, W, return_parts=return_parts)
+        h, g = m.encode_torch(X["local"], X["global"], compute_dtype=self.compute_dtype)
+        pl, pg = m.heads_torch(h, g)
+        return pretrain_loss_torch(pl, pg, Y, {k: v.float() for k, v in W.items()}, m.semantics,
+                                   None if self.standard_loss else self.local_loss_fn,
+                                   None if self.standard_loss else self.global_loss_fn, return_parts)
+
+    def __call__(self, X, Y, W) -> torch.Tensor:
+        opt = self.optimizer
+        opt.zero_grad()
+        loss = self.loss(X, Y, W)
+        loss.backward()
+        if self.ddp is not None:
+            self.ddp.finish(average=not self.fused)
+        if self.grad_clip is not None:
+            if self.fused:
+                opt.clip_grad_norm_(self.grad_clip)
+            else:
+                torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip)
+        if self.fused and self.skip_nonfinite:
+            # all-reduced grads: every rank takes the same decision, no host sync
+            opt.skip_flag = (~torch.isfinite(opt.arena.grad.sum())).to(torch.int32).reshape(1)
+        opt.step()
+        return loss.detach()
