@@ -262,7 +262,10 @@ class ProteinBERT(nn.Module):
     # ------------------------------------------------------------------------
     def resolved_backend(self, device: torch.device) -> str:
         if self.backend == "auto":
-            return "hip" if device.type == "cuda" else "torch"
+            if device.type != "cuda":
+                return "torch"
+            from ..ops.fused_model import hip_supported
+            return "hip" if hip_supported(self)[0] else "torch"
         return self.backend
 
     def attention_heads_state(self) -> Dict[str, Dict[str, torch.Tensor]]:

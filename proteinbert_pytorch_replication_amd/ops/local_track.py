@@ -1,0 +1,208 @@
+"""Autograd wrappers of the fused CDNA4 local-track kernels (``csrc/conv.hip``, ``csrc/ln.hip``).
+
+One :class:`LocalBlockFn` call is the whole local track of one ``ProteinBERTBlock`` in reference
+semantics (reference ``ProteinBERT/modules.py:201-219``)::
+
+    s1 = x + GELU(conv_d1(x)) + GELU(conv_d5(x)) + gb       (conv_fwd: 1 launch)
+    h1 = LN_(L,C)(s1); s2 = h1 + GELU(h1 Wl^T + bl)           (ln_linear_fwd: 1 launch)
+    h2 = LN_(L,C)(s2); vpart = sum_tile GELU(h2 Wv_cat^T)     (ln_attn_fwd: 1 launch)
+
+and its backward is 9 launches (attention/LN2, LN2 affine, LN2+MLP, MLP wgrad, LN1 affine+finalize,
+conv dgrad, conv wgrad).  Activations are bf16 ``[B, L, 128]`` channels-last; parameters stay fp32
+masters and are packed to bf16 kernel layouts once per forward.  The global track (``[B, 512]``
+vectors) stays in PyTorch: it is ~0.1 % of the FLOPs.
+
+Every op raises if the HIP library is missing — there is no silent eager fallback on a GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, Optional, Tuple
+
+import torch
+
+from . import _lib
+
+_P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
+
+_lib.register("pbx_conv_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_dgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_pack_conv", [_P, _P, _P, _I, _P])
+_lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+_lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_attn_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I,
+                                     _F, _P])
+_lib.register("pbx_ln_affine_bwd", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
+_lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
+
+CH = 128          # kernels are specialised for local_dim = 128
+BML = 128         # LN-kernel tile (positions)
+LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
+
+
+def conv_tile(L: int) -> int:
+    return 256 if L >= 256 else 128
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _num_cus(dev: torch.device) -> int:
+    return torch.cuda.get_device_properties(dev).multi_processor_count
+
+
+def pack_conv(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 ``[co, ci, KS]`` -> bf16 ``WP[KS][co][ci]`` (forward) and ``WT[KS][ci][co]`` (dgrad)."""
+    KS = w.shape[2]
+    wp = torch.empty((KS, CH, CH), dtype=torch.bfloat16, device=w.device)
+    wt = torch.empty_like(wp)
+    _lib.call("pbx_pack_conv", w.detach().contiguous().data_ptr(), wp.data_ptr(), wt.data_ptr(), KS,
+              _lib.stream_ptr(w.device))
+    return wp, wt
+
+
+def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
+           B: int, L: int):
+    dev = x.device
+    ntiles = B * ((L + 127) // 128)
+    R = max(1, min(ntiles, (2 * _num_cus(dev)) // (4 * nconv)))
+    slab = torch.empty((R, nconv, KS, CH, CH), dtype=torch.float32, device=dev)
+    bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
+    shape = (CH, CH, KS) if KS > 1 else (CH, CH)
+    dw0 = torch.empty(shape, dtype=torch.float32, device=dev)
+    db0 = torch.empty(CH, dtype=torch.float32, device=dev)
+    dw1 = torch.empty(shape, dtype=torch.float32, device=dev) if nconv > 1 else None
+    db1 = torch.empty(CH, dtype=torch.float32, device=dev) if nconv > 1 else None
+    _lib.call("pbx_wgrad", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
+              dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, KS, dil, nconv, R, _lib.stream_ptr(dev))
+    return dw0, db0, dw1, db1
+
+
+class LocalBlockFn(torch.autograd.Function):
+    """Fused local track of one block (reference semantics)."""
+
+    @staticmethod
+    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int):
+        B, L, C = x.shape
+        assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
+        KS = wn.shape[2]
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        BM1 = conv_tile(L)
+        T1 = (L + BM1 - 1) // BM1
+        T2 = (L + BML - 1) // BML
+        wpn, wtn = pack_conv(wn)
+        wpw, wtw = pack_conv(ww)
+        wl_b = wl.detach().to(torch.bfloat16).contiguous()
+        gb = gb.detach().float().contiguous()
+        pre_n = torch.empty_like(x)
+        pre_w = torch.empty_like(x)
+        s1 = torch.empty_like(x)
+        st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
+        _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                  gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), st1.data_ptr(), B, L, KS, dil,
+                  BM1, stream)
+        pre_l = torch.empty_like(x)
+        s2 = torch.empty_like(x)
+        st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
+        _lib.call("pbx_ln_linear_fwd", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
+                  wl_b.data_ptr(), bl.data_ptr(), pre_l.data_ptr(), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS,
+                  stream)
+        NJ = wv_bf16.shape[0]
+        h2 = torch.empty_like(x)
+        vpart = torch.empty((B, T2, NJ), dtype=torch.float32, device=dev)
+        _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
+                  wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, LN_EPS, stream)
+        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
+        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ)
+        return h2, vpart
+
+    @staticmethod
+    def backward(ctx, dh2, dvpart):
+        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        B, L, KS, dil, BM1, T1, T2, NJ = ctx.meta
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        dh2 = None if dh2 is None else dh2.to(torch.bfloat16).contiguous()
+        if dvpart is None:
+            dvpart = torch.zeros((B, T2, NJ), dtype=torch.float32, device=dev)
+        dvpart = dvpart.float().contiguous()
+        nbg = max(1, min(B, (2 * _num_cus(dev)) // max(1, (L + 15) // 16)))
+        # attention pool + LN2 partials
+        dh2t = torch.empty_like(x)
+        sums2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
+        _lib.call("pbx_attn_bwd", h2.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                  dvpart.data_ptr(), wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
+                  stream)
+        dg2 = torch.zeros((L, CH), dtype=torch.float32, device=dev)
+        dbe2 = torch.zeros_like(dg2)
+        _lib.call("pbx_ln_affine_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), T2, BML, sums2.data_ptr(),
+                  T2, g2.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), None, None, B, L, nbg, LN_EPS, stream)
+        # LN2 finalize + local MLP backward + LN1 partials
+        dh1 = torch.empty_like(x)
+        dprel = torch.empty_like(x)
+        h1 = torch.empty_like(x)
+        sums1 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
+        _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(),
+                  g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
+                  be1.data_ptr(), wl_b.data_ptr(), dh1.data_ptr(), dprel.data_ptr(), h1.data_ptr(),
+                  sums1.data_ptr(), B, L, LN_EPS, stream)
+        dwl, dbl, _, _ = _wgrad(dprel, None, h1, 1, 1, 1, B, L)
+        # LN1 affine + finalize (ds1) + gradient of the broadcast global->local vector
+        dg1 = torch.zeros((L, CH), dtype=torch.float32, device=dev)
+        dbe1 = torch.zeros_like(dg1)
+        ds1 = torch.empty_like(x)
+        dgb = torch.zeros((B, CH), dtype=torch.float32, device=dev)
+        _lib.call("pbx_ln_affine_bwd", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+                  T2, g1.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, nbg,
+                  LN_EPS, stream)
+        # convolutions
+        dx = torch.empty_like(x)
+        dpn = torch.empty_like(x)
+        dpw = torch.empty_like(x)
+        _lib.call("pbx_conv_dgrad", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, BM1, stream)
+        dwn, dbn, dww, dbw = _wgrad(dpn, dpw, x, KS, dil, 2, B, L)
+        return dx, dgb, dwn, dbn, dww, dbw, dg1, dbe1, dwl, dbl, dg2, dbe2, None, None
+
+
+class EmbedFn(torch.autograd.Function):
+    """Token embedding gather to bf16 (reference ``modules.py:249-253,300``); backward is a 26-row
+    segmented sum instead of torch's sort-based ``embedding_dense_backward``."""
+
+    @staticmethod
+    def forward(ctx, tokens, weight):
+        B, L = tokens.shape
+        V, C = weight.shape
+        assert C == CH and V <= 32
+        tok = tokens.contiguous()
+        out = torch.empty((B, L, C), dtype=torch.bfloat16, device=tokens.device)
+        _lib.call("pbx_embed_fwd", tok.data_ptr(), weight.detach().contiguous().data_ptr(), out.data_ptr(), B * L,
+                  _lib.stream_ptr(tokens.device))
+        ctx.save_for_backward(tok)
+        ctx.V = V
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        (tok,) = ctx.saved_tensors
+        dE = torch.zeros((ctx.V, CH), dtype=torch.float32, device=tok.device)
+        d = dout.to(torch.bfloat16).contiguous()
+        _lib.call("pbx_embed_bwd", tok.data_ptr(), d.data_ptr(), dE.data_ptr(), tok.numel(), ctx.V,
+                  _lib.stream_ptr(tok.device))
+        return None, dE
+
+
+def local_block(x: torch.Tensor, gb: torch.Tensor, blk) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``)."""
+    att = blk.global_attention_layer
+    wv = att.value_weight_cat().t().to(torch.bfloat16).contiguous()          # [H*vd, C]
+    nc = blk.local_narrow_conv_layer[0]
+    wc = blk.local_wide_conv_layer[0]
+    return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
+                              blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
+                              blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation)
