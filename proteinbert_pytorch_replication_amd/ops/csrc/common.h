@@ -21,14 +21,28 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 
-// exact erf GELU (nn.GELU default) and its derivative
+// GELU (nn.GELU default, erf form) and its derivative, branch-free: erf via Abramowitz-Stegun
+// 7.1.26 (|err| <= 1.5e-7) sharing exp(-x^2/2) with the Gaussian pdf.  The libm erff inlines a
+// piecewise polynomial with divergent branches, which dominated the epilogues of the fused kernels.
+__device__ __forceinline__ void gelu_parts(float x, float& cdf, float& pdf) {
+  const float z = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float e = __expf(-z * z);
+  const float poly =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float erfz = fmaf(-poly, e, 1.0f);
+  cdf = fmaf(0.5f, copysignf(erfz, x), 0.5f);
+  pdf = 0.3989422804014327f * e;
+}
 __device__ __forceinline__ float gelu_f(float x) {
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f));
+  float c, p;
+  gelu_parts(x, c, p);
+  return x * c;
 }
 __device__ __forceinline__ float gelu_grad_f(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.39894228040143268f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float c, p;
+  gelu_parts(x, c, p);
+  return fmaf(x, p, c);
 }
 
 __device__ __forceinline__ float wave_reduce_sum(float v) {

@@ -61,26 +61,6 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
     *reinterpret_cast<uint4*>(xs + swz256(j, ch)) = v;
   }
 
-  uint4 wreg[4];
-  auto wload = [&](int s) {
-    const int k = s >> 1, hh = s & 1;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 512 * i;
-      const int cv = id >> 10, row = (id >> 3) & 127, ch = id & 7;
-      const bf16_t* src = (cv ? wpw : wpn) + ((size_t)(k * CH + row) * CH + hh * 64 + ch * 8);
-      wreg[i] = *reinterpret_cast<const uint4*>(src);
-    }
-  };
-  auto wstore = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int id = tid + 512 * i;
-      const int cv = id >> 10, row = (id >> 3) & 127, ch = id & 7;
-      *reinterpret_cast<uint4*>(wb + buf * 32768 + cv * 16384 + swz128(row, ch)) = wreg[i];
-    }
-  };
-
   f32x16_t an[CT][2], aw[CT][2];
 #pragma unroll
   for (int i = 0; i < CT; ++i)
@@ -88,11 +68,30 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
     for (int j = 0; j < 2; ++j) { an[i][j] = zero16(); aw[i][j] = zero16(); }
 
   const int NS = 2 * KS;
-  wload(0);
-  wstore(0);
+  // weight staging for step s = (tap s>>1, input-channel half s&1): 2 convs x 128 rows x 128 B.
+  // thread -> 4 chunks; register staging written after the step's MFMAs (one barrier per step).
+  int wsrc[4], wdst[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int id = tid + 512 * i;
+    const int cv = id >> 10, row = (id >> 3) & 127, ch = id & 7;
+    wsrc[i] = cv * (1 << 30) + row * CH + ch * 8;
+    wdst[i] = cv * 16384 + swz128(row, ch);
+  }
+  auto wptr = [&](int i, int s) -> const uint4* {
+    const bf16_t* base = (wsrc[i] >= (1 << 30)) ? wpw : wpn;
+    const int off = wsrc[i] & ((1 << 30) - 1);
+    return reinterpret_cast<const uint4*>(base + (size_t)(s >> 1) * CH * CH + (s & 1) * 64 + off);
+  };
+  uint4 w0 = *wptr(0, 0), w1 = *wptr(1, 0), w2 = *wptr(2, 0), w3 = *wptr(3, 0);
+  *reinterpret_cast<uint4*>(wb + wdst[0]) = w0;
+  *reinterpret_cast<uint4*>(wb + wdst[1]) = w1;
+  *reinterpret_cast<uint4*>(wb + wdst[2]) = w2;
+  *reinterpret_cast<uint4*>(wb + wdst[3]) = w3;
   __syncthreads();
   for (int s = 0; s < NS; ++s) {
-    if (s + 1 < NS) wload(s + 1);
+    const int sn = s + 1 < NS ? s + 1 : s;
+    w0 = *wptr(0, sn); w1 = *wptr(1, sn); w2 = *wptr(2, sn); w3 = *wptr(3, sn);
     const int k = s >> 1, hh = s & 1;
     const int shn = k - half, shw = (k - half) * dil;
     const unsigned char* wbn = wb + (s & 1) * 32768;
@@ -121,7 +120,13 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
           aw[ct][pt] = mfma32(faw[ct], fbw[pt], aw[ct][pt]);
         }
     }
-    if (s + 1 < NS) wstore((s + 1) & 1);
+    if (s + 1 < NS) {
+      unsigned char* dst = wb + ((s + 1) & 1) * 32768;
+      *reinterpret_cast<uint4*>(dst + wdst[0]) = w0;
+      *reinterpret_cast<uint4*>(dst + wdst[1]) = w1;
+      *reinterpret_cast<uint4*>(dst + wdst[2]) = w2;
+      *reinterpret_cast<uint4*>(dst + wdst[3]) = w3;
+    }
     __syncthreads();
   }
 
@@ -207,7 +212,6 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
   const int wm = w / WN, wn = w % WN;
   const size_t sbase = (size_t)b * L * CH;
 
-  uint4 wreg[4];
   f32x16_t acc[CT][2];
 #pragma unroll
   for (int i = 0; i < CT; ++i)
@@ -220,23 +224,16 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
     const bf16_t* pre = phase ? pre_w : pre_n;
     bf16_t* dpo = phase ? dpre_w : dpre_n;
     const bf16_t* wt = phase ? wtw : wtn;
-    auto wload = [&](int k) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int id = tid + 512 * i;
-        const int row = id >> 4, ch = id & 15;
-        wreg[i] = *reinterpret_cast<const uint4*>(wt + ((size_t)(k * CH + row) * CH + ch * 8));
-      }
+    // weight staging for tap k: 128 rows (ci) x 256 B (co); thread -> 4 chunks
+    auto wptr = [&](int i, int k) -> const uint4* {
+      const int id = tid + 512 * i;
+      return reinterpret_cast<const uint4*>(wt + ((size_t)(k * CH + (id >> 4)) * CH + (id & 15) * 8));
     };
-    auto wstore = [&](int buf) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int id = tid + 512 * i;
-        const int row = id >> 4, ch = id & 15;
-        *reinterpret_cast<uint4*>(wb + buf * 32768 + swz256(row, ch)) = wreg[i];
-      }
+    auto wdst = [&](int i) -> int {
+      const int id = tid + 512 * i;
+      return swz256(id >> 4, id & 15);
     };
-    wload(0);
+    uint4 w0 = *wptr(0, 0), w1 = *wptr(1, 0), w2 = *wptr(2, 0), w3 = *wptr(3, 0);
     // stage dpre = dS1 * GELU'(pre) with halo; central rows also go to global for the wgrad
     const int AR = BM + 2 * halo;
     for (int idx = tid; idx < AR * 16; idx += 512) {
@@ -255,10 +252,14 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
       }
       *reinterpret_cast<uint4*>(as + swz256(j, ch)) = v;
     }
-    wstore(0);
+    *reinterpret_cast<uint4*>(wb + wdst(0)) = w0;
+    *reinterpret_cast<uint4*>(wb + wdst(1)) = w1;
+    *reinterpret_cast<uint4*>(wb + wdst(2)) = w2;
+    *reinterpret_cast<uint4*>(wb + wdst(3)) = w3;
     __syncthreads();
     for (int k = 0; k < KS; ++k) {
-      if (k + 1 < KS) wload(k + 1);
+      const int kn = k + 1 < KS ? k + 1 : k;
+      w0 = *wptr(0, kn); w1 = *wptr(1, kn); w2 = *wptr(2, kn); w3 = *wptr(3, kn);
       const int sh = (k - half) * d;
       const unsigned char* wk = wb + (k & 1) * 32768;
       const int rbase = halo + wm * 64 + r - sh;
@@ -274,7 +275,13 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
 #pragma unroll
           for (int pt = 0; pt < 2; ++pt) acc[ct][pt] = mfma32(fa[ct], fb[pt], acc[ct][pt]);
       }
-      if (k + 1 < KS) wstore((k + 1) & 1);
+      if (k + 1 < KS) {
+        unsigned char* dst = wb + ((k + 1) & 1) * 32768;
+        *reinterpret_cast<uint4*>(dst + wdst(0)) = w0;
+        *reinterpret_cast<uint4*>(dst + wdst(1)) = w1;
+        *reinterpret_cast<uint4*>(dst + wdst(2)) = w2;
+        *reinterpret_cast<uint4*>(dst + wdst(3)) = w3;
+      }
       __syncthreads();
     }
   }
@@ -385,27 +392,45 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
   }
 }
 
-// sum the R slabs; write torch layouts: weight [co][ci][KS] (KS == 1: [co][ci]), bias [co]
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab,
+// sum the R slabs (fixed order: deterministic); write torch layouts: weight [co][ci][KS] (KS == 1:
+// [co][ci]), bias [co].  accumulate != 0 adds into the destination (the flat-arena .grad views).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float4* __restrict__ slab,
                                                            const float* __restrict__ bslab, float* __restrict__ dw0,
                                                            float* __restrict__ dw1, float* __restrict__ db0,
-                                                           float* __restrict__ db1, int R, int nconv, int KS) {
+                                                           float* __restrict__ db1, int R, int nconv, int KS,
+                                                           int accumulate) {
   const int per = KS * CH * CH;
-  const int total = nconv * per;
+  const int total4 = nconv * per / 4;
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < total) {
-    float s = 0.f;
-    for (int rr = 0; rr < R; ++rr) s += slab[(size_t)rr * total + idx];
-    const int cv = idx / per, rem = idx - cv * per;
+  if (idx < total4) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int rr = 0;
+    for (; rr + 4 <= R; rr += 4) {
+      const float4 a = slab[(size_t)rr * total4 + idx], b = slab[(size_t)(rr + 1) * total4 + idx];
+      const float4 c = slab[(size_t)(rr + 2) * total4 + idx], d = slab[(size_t)(rr + 3) * total4 + idx];
+      s.x += (a.x + b.x) + (c.x + d.x); s.y += (a.y + b.y) + (c.y + d.y);
+      s.z += (a.z + b.z) + (c.z + d.z); s.w += (a.w + b.w) + (c.w + d.w);
+    }
+    for (; rr < R; ++rr) {
+      const float4 a = slab[(size_t)rr * total4 + idx];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    const int e = idx * 4;
+    const int cv = e / per, rem = e - cv * per;
     const int k = rem / (CH * CH), co = (rem / CH) % CH, ci = rem % CH;
     float* dw = cv ? dw1 : dw0;
-    dw[((size_t)co * CH + ci) * KS + k] = s;
+    const float sv[4] = {s.x, s.y, s.z, s.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const size_t a = ((size_t)co * CH + ci + j) * KS + k;
+      dw[a] = (accumulate ? dw[a] : 0.f) + sv[j];
+    }
   }
   if (idx < nconv * CH) {
     float s = 0.f;
     for (int rr = 0; rr < R; ++rr) s += bslab[(size_t)rr * nconv * CH + idx];
     float* db = idx >= CH ? db1 : db0;
-    if (db != nullptr) db[idx % CH] = s;
+    if (db != nullptr) db[idx % CH] = (accumulate ? db[idx % CH] : 0.f) + s;
   }
 }
 
@@ -478,7 +503,7 @@ PBX_EXPORT int pbx_conv_dgrad(const void* ds1, const void* pre_n, const void* pr
 // slab: R * nconv * KS * 128 * 128 floats; bslab: R * nconv * 128 floats
 PBX_EXPORT int pbx_wgrad(const void* dy0, const void* dy1, const void* x, float* slab, float* bslab, float* dw0,
                          float* dw1, float* db0, float* db1, int B, int L, int KS, int dil1, int nconv, int R,
-                         hipStream_t st) {
+                         int accumulate, hipStream_t st) {
   set_conv_attrs();
   constexpr int BM = 128;
   const int halo = (KS / 2) * (nconv > 1 ? dil1 : 1);
@@ -493,9 +518,9 @@ PBX_EXPORT int pbx_wgrad(const void* dy0, const void* dy1, const void* x, float*
                        (const bf16_t*)x, slab, bslab, B, L, dil1, nconv);
   else
     return (int)hipErrorInvalidValue;
-  const int total = nconv * KS * CH * CH;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, slab, bslab, dw0, dw1, db0,
-                     db1, R, nconv, KS);
+  const int total4 = nconv * KS * CH * CH / 4;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, (const float4*)slab, bslab,
+                     dw0, dw1, db0, db1, R, nconv, KS, accumulate);
   return pbx_launch_status();
 }
 

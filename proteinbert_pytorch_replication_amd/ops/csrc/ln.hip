@@ -18,7 +18,7 @@ typedef unsigned short bf16_t;
 
 namespace {
 constexpr int CH = 128;
-constexpr int BML = 128;   // LN-kernel tile (positions)
+constexpr int BML = 32;    // tile of the s2 (mean, M2) partials written by ln_linear_fwd
 
 __device__ __forceinline__ void load_f8(const float* p, float* v) {
   const float4 a = *reinterpret_cast<const float4*>(p);
@@ -30,109 +30,160 @@ __device__ __forceinline__ void load_f4(const float* p, float* v) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 
-// stage a [rows x 128] bf16 weight matrix into a swz256 LDS image (256 threads)
+// stage a [rows x 128] bf16 weight matrix into a swz256 LDS image (whole workgroup)
 __device__ __forceinline__ void stage_weight(unsigned char* dst, const bf16_t* __restrict__ w, int rows) {
-  for (int idx = threadIdx.x; idx < rows * 16; idx += 256) {
+  for (int idx = threadIdx.x; idx < rows * 16; idx += blockDim.x) {
     const int row = idx >> 4, ch = idx & 15;
     *reinterpret_cast<uint4*>(dst + swz256(row, ch)) =
         *reinterpret_cast<const uint4*>(w + (size_t)row * CH + ch * 8);
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// h1 = LN(s1) ; pre = h1 Wl^T + bl ; s2 = h1 + GELU(pre)  (+ s2 tile (mean, M2) partials)
-__global__ void __launch_bounds__(256) ln_linear_fwd_kernel(
-    const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
-    const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ bl,
-    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, int B, int L, float eps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;                                     // 32 KB
-  float* scratch = reinterpret_cast<float*>(smem + 32768);      // 16 floats
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int T2 = (L + BML - 1) / BML;
-  stage_weight(ws, wl, CH);
-  __syncthreads();
-  for (int tile = blockIdx.x; tile < B * T2; tile += gridDim.x) {
-    const int b = tile / T2, t = tile - (tile / T2) * T2;
-    const int pos0 = t * BML;
-    float mean, rstd;
-    ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
-    const int p = w * 32 + r;
-    const int pos = pos0 + p;
-    const bool okb = pos < L;
-    const size_t rowoff = ((size_t)b * L + pos) * CH;
-    bf16x8 hf[8];
+// LN-normalised B/A fragment of one position row: 8 x (8 channels kk*16 + 8h .. +8)
+__device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict__ src, const float* __restrict__ gam,
+                                             const float* __restrict__ bet, float mean, float rstd, bool ok,
+                                             int h, bf16_t* __restrict__ out) {
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int ci = kk * 16 + 8 * h;
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (okb) {
-        float s[8], g[8], be[8];
-        unpack8(*reinterpret_cast<const uint4*>(s1 + rowoff + ci), s);
-        load_f8(g1 + (size_t)pos * CH + ci, g);
-        load_f8(be1 + (size_t)pos * CH + ci, be);
+  for (int kk = 0; kk < 8; ++kk) {
+    const int ci = kk * 16 + 8 * h;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (ok) {
+      float sv[8], g[8], be[8];
+      unpack8(*reinterpret_cast<const uint4*>(src + ci), sv);
+      load_f8(gam + ci, g);
+      load_f8(bet + ci, be);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (s[e] - mean) * rstd * g[e] + be[e];
-      }
-      hf[kk] = pack8(v);
+      for (int e = 0; e < 8; ++e) v[e] = (sv[e] - mean) * rstd * g[e] + be[e];
     }
-    f32x16_t acc[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-        acc[ct] = mfma32(lds_frag(ws, swz256(ct * 32 + r, kk * 2 + h)), hf[kk], acc[ct]);
-    // D[co][pos]: lane -> position p, registers -> output channels
-    float lsum = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int co0 = ct * 32 + 8 * g + 4 * h;
-        float s[4] = {0, 0, 0, 0}, gg[4] = {0, 0, 0, 0}, be[4] = {0, 0, 0, 0}, bb[4], pre[4], o[4];
-        if (okb) {
-          unpack4(*reinterpret_cast<const uint2*>(s1 + rowoff + co0), s);
-          load_f4(g1 + (size_t)pos * CH + co0, gg);
-          load_f4(be1 + (size_t)pos * CH + co0, be);
-        }
-        load_f4(bl + co0, bb);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float h1 = (s[e] - mean) * rstd * gg[e] + be[e];
-          pre[e] = acc[ct][4 * g + e] + bb[e];
-          o[e] = okb ? bfround(h1 + gelu_f(pre[e])) : 0.f;
-          acc[ct][4 * g + e] = o[e];
-          lsum += o[e];
-        }
-        if (okb) {
-          *reinterpret_cast<uint2*>(pre_l + rowoff + co0) = packq4(pre);
-          *reinterpret_cast<uint2*>(s2 + rowoff + co0) = packq4(o);
-        }
-      }
-    const int vrows = min(BML, L - pos0);
-    const float tmean = block_sum(lsum, scratch, 4) / (float)(vrows * CH);
-    float m2 = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float d = acc[ct][i] - tmean;
-        m2 += okb ? d * d : 0.f;
-      }
-    m2 = block_sum(m2, scratch + 4, 4);
-    if (tid == 0) {
-      st2[((size_t)b * T2 + t) * 2] = tmean;
-      st2[((size_t)b * T2 + t) * 2 + 1] = m2;
-    }
+    const uint4 q = packq8(v);
+    if (ok && out != nullptr) *reinterpret_cast<uint4*>(out + ci) = q;
+    f[kk] = __builtin_bit_cast(bf16x8, q);
   }
 }
 
 // ------------------------------------------------------------------------------------------------
+// Position-major LayerNorm kernels.  A workgroup owns PB = 32 positions of the [L, C] LayerNorm
+// affine and walks a group of samples, so every thread keeps the affine parameters (and, in the
+// backward, the affine-gradient accumulators) of its fixed (position, 8-channel chunk) in registers
+// and the next sample's rows are prefetched while the current one is in the MFMA.
+// Thread t (of 512) owns row j = t >> 4 (position l0 + j) and channel chunk ch = t & 15.
+constexpr int PB = 32;
+
+__device__ __forceinline__ uint4 ldq(const bf16_t* p, bool ok) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+
+// per-sample statistics through LDS (computed by one wave, broadcast)
+__device__ __forceinline__ void sample_stats(float* sh, const float* __restrict__ st, int T, int BM, int L, float eps,
+                                             const float* __restrict__ sums, int Ts, float inv_n) {
+  if (threadIdx.x == 0) {
+    float mean, rstd;
+    ln_stats(st, T, BM, L, CH, eps, mean, rstd);
+    sh[0] = mean;
+    sh[1] = rstd;
+    if (sums != nullptr) {
+      float m1, m2;
+      ln_bwd_consts(sums, Ts, inv_n, m1, m2);
+      sh[2] = m1;
+      sh[3] = m2;
+    }
+  }
+}
+
+// h1 = LN(s1) ; pre = h1 Wl^T + bl ; s2 = h1 + GELU(pre)  (+ s2 (mean, M2) partial per 32 positions)
+// grid (ceil(L/PB), nbg), 512 threads; waves 0-3 run the 32x32 MFMA tiles of D[co][pos].
+__global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
+    const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
+    const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ bl,
+    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, int B, int L, float eps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ws = smem;                                          // Wl, 32 KB
+  unsigned char* ht = smem + 32768;                                  // h1 tile bf16, PB x 256 B
+  float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // D^T tile fp32 [PB][128]
+  float* sh = yt + PB * CH;                                          // stats + reduction scratch
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int j = tid >> 4, ch = tid & 15;
+  const int l0 = blockIdx.x * PB, l = l0 + j;
+  const bool okl = l < L;
+  const int TP = (L + PB - 1) / PB;
+  const int nbg = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
+  stage_weight(ws, wl, CH);
+  float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bb[8];
+  if (okl) {
+    load_f8(g1 + (size_t)l * CH + ch * 8, gam);
+    load_f8(be1 + (size_t)l * CH + ch * 8, bet);
+  }
+  load_f8(bl + ch * 8, bb);
+  const int vrows = min(PB, L - l0);
+  uint4 nxt = ldq(s1 + ((size_t)b0 * L + l) * CH + ch * 8, okl && b0 < b1);
+  for (int b = b0; b < b1; ++b) {
+    sample_stats(sh, st1 + (size_t)b * T1 * 2, T1, BM1, L, eps, nullptr, 0, 0.f);
+    __syncthreads();
+    const float mean = sh[0], rstd = sh[1];
+    float sv[8], h1[8];
+    unpack8(nxt, sv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) h1[e] = okl ? (sv[e] - mean) * rstd * gam[e] + bet[e] : 0.f;
+    *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(h1);
+    __syncthreads();
+    nxt = ldq(s1 + ((size_t)(b + 1) * L + l) * CH + ch * 8, okl && b + 1 < b1);
+    if (w < 4) {
+      f32x16_t acc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk)
+        acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(yt + r * CH + w * 32 + 8 * g + 4 * h) =
+            make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+    }
+    __syncthreads();
+    float pre[8], o[8], lsum = 0.f;
+    const float4 ya = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8);
+    const float4 yb = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8 + 4);
+    const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pre[e] = yv[e] + bb[e];
+      o[e] = okl ? bfround(h1[e] + gelu_f(pre[e])) : 0.f;
+      lsum += o[e];
+    }
+    if (okl) {
+      const size_t off = ((size_t)b * L + l) * CH + ch * 8;
+      *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);
+      *reinterpret_cast<uint4*>(s2 + off) = packq8(o);
+    }
+    const float tmean = block_sum(lsum, sh + 8, 8) / (float)(vrows * CH);
+    float m2 = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) m2 += okl ? (o[e] - tmean) * (o[e] - tmean) : 0.f;
+    m2 = block_sum(m2, sh + 16, 8);
+    if (tid == 0) {
+      st2[((size_t)b * TP + blockIdx.x) * 2] = tmean;
+      st2[((size_t)b * TP + blockIdx.x) * 2 + 1] = m2;
+    }
+  }
+}
+
+// 8 chained MFMAs: D[j][pos] (A = Wv rows jt*32.., B = h2 fragments) or D[pos][j] (swapped)
+template <bool POS_ROWS>
+__device__ __forceinline__ f32x16_t wv_chain(const unsigned char* ws, const bf16x8* hf, int jt, int r, int h) {
+  f32x16_t acc = zero16();
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const bf16x8 wf = lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h));
+    acc = POS_ROWS ? mfma32(hf[kk], wf, acc) : mfma32(wf, hf[kk], acc);
+  }
+  return acc;
+}
+
+// ------------------------------------------------------------------------------------------------
 // h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in tile} GELU(h2[pos] . Wv[j])
-__global__ void __launch_bounds__(256) ln_attn_fwd_kernel(
+// NW waves (blockDim = 64 NW), tile = 32 NW positions; the MFMA chain of column block jt+1 is
+// issued before the GELU/column-sum VALU work of block jt so the two pipes overlap.
+__global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
     float* __restrict__ vpart, int B, int L, int NJ, float eps) {
@@ -141,55 +192,44 @@ __global__ void __launch_bounds__(256) ln_attn_fwd_kernel(
   float* red = reinterpret_cast<float*>(smem + NJ * 256);            // NJ floats
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
+  const int NW = blockDim.x >> 6, BMA = NW * 32;
   const int T2 = (L + BML - 1) / BML;
+  const int TA = (L + BMA - 1) / BMA;
+  const int NJT = NJ / 32;
   stage_weight(ws, wv, NJ);
   __syncthreads();
-  for (int tile = blockIdx.x; tile < B * T2; tile += gridDim.x) {
-    const int b = tile / T2, t = tile - (tile / T2) * T2;
-    const int pos0 = t * BML;
+  for (int tile = blockIdx.x; tile < B * TA; tile += gridDim.x) {
+    const int b = tile / TA, t = tile - (tile / TA) * TA;
+    const int pos0 = t * BMA;
     float mean, rstd;
     ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    for (int j = tid; j < NJ; j += 256) red[j] = 0.f;
+    for (int j = tid; j < NJ; j += blockDim.x) red[j] = 0.f;
     const int pos = pos0 + w * 32 + r;
     const bool okb = pos < L;
     const size_t rowoff = ((size_t)b * L + pos) * CH;
     bf16x8 hf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int ci = kk * 16 + 8 * h;
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (okb) {
-        float s[8], g[8], be[8];
-        unpack8(*reinterpret_cast<const uint4*>(s2 + rowoff + ci), s);
-        load_f8(g2 + (size_t)pos * CH + ci, g);
-        load_f8(be2 + (size_t)pos * CH + ci, be);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = (s[e] - mean) * rstd * g[e] + be[e];
-        const uint4 q = packq8(v);
-        *reinterpret_cast<uint4*>(h2 + rowoff + ci) = q;
-        hf[kk] = __builtin_bit_cast(bf16x8, q);
-      } else {
-        hf[kk] = pack8(v);
-      }
-    }
+    ln_row_frags(hf, s2 + rowoff, g2 + (size_t)pos * CH, be2 + (size_t)pos * CH, mean, rstd, okb, h, h2 + rowoff);
     __syncthreads();   // red zeroed
-    // D[pos][j]: lane -> column j, registers -> positions; GELU then sum over positions
     const int rowbase = pos0 + w * 32 + 4 * h;
-    for (int jt = 0; jt < NJ / 32; ++jt) {
-      f32x16_t acc = zero16();
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) acc = mfma32(hf[kk], lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h)), acc);
-      float s = 0.f;
+    auto colsum = [&](const f32x16_t& acc, int jt) {
+      float sacc = 0.f;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int prow = rowbase + (i & 3) + 8 * (i >> 2);
-        s += prow < L ? gelu_f(acc[i]) : 0.f;
+        sacc += prow < L ? gelu_f(acc[i]) : 0.f;
       }
-      s += __shfl_xor(s, 32, 64);
-      if (h == 0) atomicAdd(&red[jt * 32 + r], s);
+      sacc += __shfl_xor(sacc, 32, 64);
+      if (h == 0) atomicAdd(&red[jt * 32 + r], sacc);
+    };
+    f32x16_t a0 = wv_chain<true>(ws, hf, 0, r, h);
+    for (int jt = 0; jt < NJT; jt += 2) {
+      const f32x16_t a1 = wv_chain<true>(ws, hf, jt + 1, r, h);
+      colsum(a0, jt);
+      if (jt + 2 < NJT) a0 = wv_chain<true>(ws, hf, jt + 2, r, h);
+      colsum(a1, jt + 1);
     }
     __syncthreads();
-    for (int j = tid; j < NJ; j += 256) vpart[((size_t)b * T2 + t) * NJ + j] = red[j];
+    for (int j = tid; j < NJ; j += blockDim.x) vpart[((size_t)b * TA + t) * NJ + j] = red[j];
     __syncthreads();
   }
 }
@@ -197,10 +237,11 @@ __global__ void __launch_bounds__(256) ln_attn_fwd_kernel(
 // ------------------------------------------------------------------------------------------------
 // attention pool backward + LayerNorm-2 backward partials.
 // dP[j][pos] = dv[b][t][j] * GELU'(Wv[j] . h2[pos]) ; dh2 = dh2_in + Wv^T dP  (dP never leaves
-// registers: the 32x32 accumulator of the recompute is the B operand of the second MFMA)
-__global__ void __launch_bounds__(256) attn_bwd_kernel(
+// registers: the 32x32 accumulator of the recompute is the B operand of the second MFMA).
+// NW waves, tile = 32 NW positions (sums2 partials per tile); dv rows are per ln_attn_fwd tile.
+__global__ void __launch_bounds__(512) attn_bwd_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart,
+    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
     const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, int NJ,
     float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -209,12 +250,16 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
+  const int NW = blockDim.x >> 6, BMA = NW * 32;
   const int T2 = (L + BML - 1) / BML;
+  const int TA = (L + BMA - 1) / BMA;
+  const int TV = (L + BMV - 1) / BMV;
+  const int NJT = NJ / 32;
   stage_weight(ws, wv, NJ);
   __syncthreads();
-  for (int tile = blockIdx.x; tile < B * T2; tile += gridDim.x) {
-    const int b = tile / T2, t = tile - (tile / T2) * T2;
-    const int pos0 = t * BML;
+  for (int tile = blockIdx.x; tile < B * TA; tile += gridDim.x) {
+    const int b = tile / TA, t = tile - (tile / TA) * TA;
+    const int pos0 = t * BMA;
     const int pos = pos0 + w * 32 + r;
     const bool okb = pos < L;
     const size_t rowoff = ((size_t)b * L + pos) * CH;
@@ -228,11 +273,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
     f32x16_t y[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    const float* dv = dvpart + ((size_t)b * T2 + t) * NJ;
-    for (int jt = 0; jt < NJ / 32; ++jt) {
-      f32x16_t d1 = zero16();
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) d1 = mfma32(lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h)), hf[kk], d1);
+    const float* dv = dvpart + ((size_t)b * TV + (okb ? pos / BMV : 0)) * NJ;
+    auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -252,6 +294,13 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
           y[ct] = mfma32(fa, fb, y[ct]);
         }
       }
+    };
+    f32x16_t d0 = wv_chain<false>(ws, hf, 0, r, h);
+    for (int jt = 0; jt < NJT; jt += 2) {
+      const f32x16_t d1 = wv_chain<false>(ws, hf, jt + 1, r, h);
+      proc(d0, jt);
+      if (jt + 2 < NJT) d0 = wv_chain<false>(ws, hf, jt + 2, r, h);
+      proc(d1, jt + 1);
     }
     // Y[ci][pos]; LN2 backward partials
     float mean, rstd;
@@ -263,14 +312,14 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int ci0 = ct * 32 + 8 * g + 4 * h;
-          float din[4] = {0, 0, 0, 0}, s[4], gg[4], o[4];
+          float din[4] = {0, 0, 0, 0}, sv[4], gg[4], o[4];
           if (dh2_in != nullptr) unpack4(*reinterpret_cast<const uint2*>(dh2_in + rowoff + ci0), din);
-          unpack4(*reinterpret_cast<const uint2*>(s2 + rowoff + ci0), s);
+          unpack4(*reinterpret_cast<const uint2*>(s2 + rowoff + ci0), sv);
           load_f4(g2 + (size_t)pos * CH + ci0, gg);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             o[e] = bfround(din[e] + y[ct][4 * g + e]);
-            const float xh = (s[e] - mean) * rstd;
+            const float xh = (sv[e] - mean) * rstd;
             const float dxh = o[e] * gg[e];
             sa += dxh;
             sc += dxh * xh;
@@ -278,194 +327,199 @@ __global__ void __launch_bounds__(256) attn_bwd_kernel(
           *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
         }
     }
-    sa = block_sum(sa, scratch, 4);
-    sc = block_sum(sc, scratch + 4, 4);
+    sa = block_sum(sa, scratch, NW);
+    sc = block_sum(sc, scratch + 16, NW);
     if (tid == 0) {
-      sums2[((size_t)b * T2 + t) * 2] = sa;
-      sums2[((size_t)b * T2 + t) * 2 + 1] = sc;
+      sums2[((size_t)b * TA + t) * 2] = sa;
+      sums2[((size_t)b * TA + t) * 2 + 1] = sc;
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// LayerNorm-2 backward finalize + local MLP backward + LayerNorm-1 backward partials.
-// ds2 = rstd2 (dh2 g2 - m1 - xhat2 m2) ; dpre = ds2 GELU'(pre) ; dh1 = ds2 + Wl^T dpre
-// writes dh1, dpre (and the recomputed h1) for the Linear weight gradient.
-__global__ void __launch_bounds__(256) ln2_linear_bwd_kernel(
+// LayerNorm-2 backward + local MLP backward + LayerNorm-1 backward partials + both [L, C] affine
+// gradients, position-major (grid (ceil(L/PB), nbg), 512 threads):
+//   ds2 = rstd2 (dh2 g2 - m1 - xhat2 m2) ; dpre = ds2 GELU'(pre) ; dh1 = ds2 + Wl^T dpre
+//   dg2 += dh2 xhat2 ; db2 += dh2 ; dg1 += dh1 xhat1 ; db1 += dh1   (registers, one atomic pass at the end)
+// writes dh1, dpre and the recomputed h1 (inputs of the Linear weight gradient) and the per-sample
+// LN1 partials (sum dxhat1, sum dxhat1*xhat1) per 32 positions.
+__global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ sums2, const float* __restrict__ g2, const bf16_t* __restrict__ pre_l,
+    const float* __restrict__ sums2, int TS2, const float* __restrict__ g2, const bf16_t* __restrict__ pre_l,
     const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
     const float* __restrict__ be1, const bf16_t* __restrict__ wl, bf16_t* __restrict__ dh1,
-    bf16_t* __restrict__ dpre_out, bf16_t* __restrict__ h1_out, float* __restrict__ sums1, int B, int L,
+    bf16_t* __restrict__ dpre_out, bf16_t* __restrict__ h1_out, float* __restrict__ sums1,
+    float* __restrict__ dg2, float* __restrict__ db2, float* __restrict__ dg1, float* __restrict__ db1, int B, int L,
     float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;
-  float* scratch = reinterpret_cast<float*>(smem + 32768);
+  unsigned char* ws = smem;                                          // Wl, 32 KB
+  unsigned char* dt = smem + 32768;                                  // dpre tile bf16
+  float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // [PB][128] fp32
+  float* sh = yt + PB * CH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
-  const int T2 = (L + BML - 1) / BML;
+  const int j = tid >> 4, ch = tid & 15;
+  const int l0 = blockIdx.x * PB, l = l0 + j;
+  const bool okl = l < L;
+  const int TP = (L + PB - 1) / PB;
+  const int T2 = TP;
+  const int nbg = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
   const float inv_n = 1.0f / (float)(L * CH);
   stage_weight(ws, wl, CH);
-  __syncthreads();
-  for (int tile = blockIdx.x; tile < B * T2; tile += gridDim.x) {
-    const int b = tile / T2, t = tile - (tile / T2) * T2;
-    const int pos0 = t * BML;
-    const int pos = pos0 + w * 32 + r;
-    const bool okb = pos < L;
-    const size_t rowoff = ((size_t)b * L + pos) * CH;
-    float mean2, rstd2, m1, m2, mean1, rstd1;
-    ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean2, rstd2);
-    ln_bwd_consts(sums2 + (size_t)b * T2 * 2, T2, inv_n, m1, m2);
-    ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
-    bf16x8 df[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int co = kk * 16 + 8 * h;
-      float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (okb) {
-        float dh[8], s[8], g[8], pr[8];
-        unpack8(*reinterpret_cast<const uint4*>(dh2 + rowoff + co), dh);
-        unpack8(*reinterpret_cast<const uint4*>(s2 + rowoff + co), s);
-        unpack8(*reinterpret_cast<const uint4*>(pre_l + rowoff + co), pr);
-        load_f8(g2 + (size_t)pos * CH + co, g);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (s[e] - mean2) * rstd2;
-          const float ds = rstd2 * (dh[e] * g[e] - m1 - xh * m2);
-          v[e] = ds * gelu_grad_f(pr[e]);
-        }
-        const uint4 qv = packq8(v);
-        *reinterpret_cast<uint4*>(dpre_out + rowoff + co) = qv;
-        df[kk] = __builtin_bit_cast(bf16x8, qv);
-      } else {
-        df[kk] = pack8(v);
-      }
+  float ga2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (okl) {
+    load_f8(g2 + (size_t)l * CH + ch * 8, ga2);
+    load_f8(g1 + (size_t)l * CH + ch * 8, ga1);
+    load_f8(be1 + (size_t)l * CH + ch * 8, bt1);
+  }
+  float adg2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float adg1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const size_t coff = (size_t)l * CH + ch * 8;
+  uint4 n_dh = ldq(dh2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  uint4 n_s2 = ldq(s2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  uint4 n_pr = ldq(pre_l + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  uint4 n_s1 = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  for (int b = b0; b < b1; ++b) {
+    if (threadIdx.x == 0) {
+      float mean, rstd, m1, m2;
+      ln_stats(st2 + (size_t)b * T2 * 2, T2, PB, L, CH, eps, mean, rstd);
+      ln_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, inv_n, m1, m2);
+      sh[0] = mean; sh[1] = rstd; sh[2] = m1; sh[3] = m2;
+      ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+      sh[4] = mean; sh[5] = rstd;
     }
-    f32x16_t y[4];
+    __syncthreads();
+    const float mean2 = sh[0], rstd2 = sh[1], m1 = sh[2], m2 = sh[3], mean1 = sh[4], rstd1 = sh[5];
+    float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
+    unpack8(n_dh, dh);
+    unpack8(n_s2, sv2);
+    unpack8(n_pr, pr);
+    unpack8(n_s1, sv1);
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
+    for (int e = 0; e < 8; ++e) {
+      const float xh2 = (sv2[e] - mean2) * rstd2;
+      adg2[e] += okl ? dh[e] * xh2 : 0.f;
+      adb2[e] += okl ? dh[e] : 0.f;
+      ds2[e] = okl ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
+      dp[e] = ds2[e] * gelu_grad_f(pr[e]);
+      xh1[e] = (sv1[e] - mean1) * rstd1;
+      hv[e] = xh1[e] * ga1[e] + bt1[e];
+    }
+    const uint4 dq = packq8(dp);
+    *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
+    const size_t off = (size_t)b * L * CH + coff;
+    if (okl) {
+      *reinterpret_cast<uint4*>(dpre_out + off) = dq;
+      *reinterpret_cast<uint4*>(h1_out + off) = packq8(hv);
+    }
+    __syncthreads();
+    const size_t noff = (size_t)(b + 1) * L * CH + coff;
+    const bool nok = okl && b + 1 < b1;
+    n_dh = ldq(dh2 + noff, nok);
+    n_s2 = ldq(s2 + noff, nok);
+    n_pr = ldq(pre_l + noff, nok);
+    n_s1 = ldq(s1 + noff, nok);
+    if (w < 4) {
+      // D[ci][pos] = sum_co Wl[co][ci] dpre[pos][co]: A = Wl^T (transposed LDS read), B = dpre rows
+      f32x16_t acc = zero16();
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const int rlo = kk * 16 + 8 * h + q;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int col = ct * 32 + tc;
+      for (int kk = 0; kk < 8; ++kk) {
+        const int rlo = kk * 16 + 8 * h + q;
+        const int col = w * 32 + tc;
         const bf16x8 fa = cat_tr(lds_tr(ws, swz256e(rlo, col)), lds_tr(ws, swz256e(rlo + 4, col)));
-        y[ct] = mfma32(fa, df[kk], y[ct]);
+        acc = mfma32(fa, lds_frag(dt, swz256(r, kk * 2 + h)), acc);
       }
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(yt + r * CH + w * 32 + 8 * g + 4 * h) =
+            make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
-    float sa = 0.f, sc = 0.f;
-    if (okb) {
+    __syncthreads();
+    const float4 ya = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8);
+    const float4 yb = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8 + 4);
+    const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
+    float o[8], sa = 0.f, sc = 0.f;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int ci0 = ct * 32 + 8 * g + 4 * h;
-          float dh[4], s[4], gg[4], sv1[4], ga[4], bb[4], o[4], hv[4];
-          unpack4(*reinterpret_cast<const uint2*>(dh2 + rowoff + ci0), dh);
-          unpack4(*reinterpret_cast<const uint2*>(s2 + rowoff + ci0), s);
-          load_f4(g2 + (size_t)pos * CH + ci0, gg);
-          unpack4(*reinterpret_cast<const uint2*>(s1 + rowoff + ci0), sv1);
-          load_f4(g1 + (size_t)pos * CH + ci0, ga);
-          load_f4(be1 + (size_t)pos * CH + ci0, bb);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float xh2 = (s[e] - mean2) * rstd2;
-            const float ds = rstd2 * (dh[e] * gg[e] - m1 - xh2 * m2);
-            o[e] = bfround(ds + y[ct][4 * g + e]);
-            const float xh1 = (sv1[e] - mean1) * rstd1;
-            hv[e] = xh1 * ga[e] + bb[e];
-            const float dxh = o[e] * ga[e];
-            sa += dxh;
-            sc += dxh * xh1;
-          }
-          *reinterpret_cast<uint2*>(dh1 + rowoff + ci0) = packq4(o);
-          *reinterpret_cast<uint2*>(h1_out + rowoff + ci0) = packq4(hv);
-        }
+    for (int e = 0; e < 8; ++e) {
+      o[e] = okl ? bfround(ds2[e] + yv[e]) : 0.f;
+      const float dxh = o[e] * ga1[e];
+      sa += dxh;
+      sc += dxh * xh1[e];
+      adg1[e] += o[e] * xh1[e];
+      adb1[e] += o[e];
     }
-    sa = block_sum(sa, scratch, 4);
-    sc = block_sum(sc, scratch + 4, 4);
+    if (okl) *reinterpret_cast<uint4*>(dh1 + off) = packq8(o);
+    sa = block_sum(sa, sh + 8, 8);
+    sc = block_sum(sc, sh + 16, 8);
     if (tid == 0) {
-      sums1[((size_t)b * T2 + t) * 2] = sa;
-      sums1[((size_t)b * T2 + t) * 2 + 1] = sc;
+      sums1[((size_t)b * TP + blockIdx.x) * 2] = sa;
+      sums1[((size_t)b * TP + blockIdx.x) * 2 + 1] = sc;
+    }
+  }
+  // affine gradients: transpose through LDS so each wave-instruction adds 256 contiguous bytes
+  float* accs[4] = {adg2, adb2, adg1, adb1};
+  float* dsts[4] = {dg2, db2, dg1, db1};
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = accs[a][e];
+    __syncthreads();
+    for (int i = tid; i < PB * CH; i += 512) {
+      if (l0 + (i >> 7) < L) atomicAdd(dsts[a] + (size_t)l0 * CH + i, yt[i]);
     }
   }
 }
 
 // ------------------------------------------------------------------------------------------------
-// [L, C]-affine gradients of a whole-sequence LayerNorm (sum over the batch) and, optionally, the
-// input gradient ds = rstd (dh g - m1 - xhat m2) plus its per-sample column sum (gradient of the
-// broadcast global->local vector, reference modules.py:208-211).
-// grid (ceil(L/16), nbg); thread = (position pl = tid>>4, channel chunk c8 = tid&15)
-__global__ void __launch_bounds__(256) ln_affine_bwd_kernel(
-    const bf16_t* __restrict__ dh, const bf16_t* __restrict__ s, const float* __restrict__ st, int Tst, int BMst,
-    const float* __restrict__ sums, int Tsm, const float* __restrict__ gamma, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, bf16_t* __restrict__ ds, float* __restrict__ dgb, int B, int L, float eps) {
-  __shared__ float consts[4 * 64];
-  __shared__ float red[16 * CH];
-  const int tid = threadIdx.x, pl = tid >> 4, c8 = tid & 15;
-  const int l = blockIdx.x * 16 + pl;
-  const int nbg = gridDim.y, bg = blockIdx.y;
-  const int b0 = (int)((long)B * bg / nbg), b1 = (int)((long)B * (bg + 1) / nbg);
-  const float inv_n = 1.0f / (float)(L * CH);
+// LayerNorm-1 backward finalize: ds1 = rstd1 (dh1 g1 - m1 - xhat1 m2) and dgb[b][c] = sum_l ds1
+// (gradient of the broadcast global->local vector, reference modules.py:208-211).
+// grid (ceil(L/PB), nbg), 512 threads, same (position, chunk) ownership.
+__global__ void __launch_bounds__(512) ln1_finalize_kernel(
+    const bf16_t* __restrict__ dh1, const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1,
+    const float* __restrict__ sums1, int TS1, const float* __restrict__ g1, bf16_t* __restrict__ ds1,
+    float* __restrict__ dgb, int B, int L, float eps) {
+  __shared__ float red[PB * CH];
+  __shared__ float sh[8];
+  const int tid = threadIdx.x;
+  const int j = tid >> 4, ch = tid & 15;
+  const int l0 = blockIdx.x * PB, l = l0 + j;
   const bool okl = l < L;
-  float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (okl) load_f8(gamma + (size_t)l * CH + c8 * 8, gam);
-  float dg[8] = {0, 0, 0, 0, 0, 0, 0, 0}, db[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int bc = b0; bc < b1; bc += 64) {
-    const int nb = min(64, b1 - bc);
+  const int nbg = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
+  const float inv_n = 1.0f / (float)(L * CH);
+  float ga[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (okl) load_f8(g1 + (size_t)l * CH + ch * 8, ga);
+  const size_t coff = (size_t)l * CH + ch * 8;
+  uint4 n_dh = ldq(dh1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  uint4 n_s = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  for (int b = b0; b < b1; ++b) {
+    sample_stats(sh, st1 + (size_t)b * T1 * 2, T1, BM1, L, eps, sums1 + (size_t)b * TS1 * 2, TS1, inv_n);
     __syncthreads();
-    if (tid < nb) {
-      const int bb = bc + tid;
-      float mean, rstd, m1, m2;
-      ln_stats(st + (size_t)bb * Tst * 2, Tst, BMst, L, CH, eps, mean, rstd);
-      ln_bwd_consts(sums + (size_t)bb * Tsm * 2, Tsm, inv_n, m1, m2);
-      consts[4 * tid] = mean; consts[4 * tid + 1] = rstd; consts[4 * tid + 2] = m1; consts[4 * tid + 3] = m2;
+    const float mean = sh[0], rstd = sh[1], m1 = sh[2], m2 = sh[3];
+    float dv[8], sv[8], o[8];
+    unpack8(n_dh, dv);
+    unpack8(n_s, sv);
+    const size_t noff = (size_t)(b + 1) * L * CH + coff;
+    n_dh = ldq(dh1 + noff, okl && b + 1 < b1);
+    n_s = ldq(s1 + noff, okl && b + 1 < b1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = okl ? rstd * (dv[e] * ga[e] - m1 - (sv[e] - mean) * rstd * m2) : 0.f;
+    const uint4 qv = packq8(o);
+    if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + coff) = qv;
+    unpack8(qv, o);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[j * CH + ch * 8 + e] = o[e];
+    __syncthreads();
+    if (tid < CH) {
+      float a = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < PB; ++k) a += red[k * CH + tid];
+      atomicAdd(dgb + (size_t)b * CH + tid, a);
     }
     __syncthreads();
-    for (int i = 0; i < nb; ++i) {
-      const int bb = bc + i;
-      const float mean = consts[4 * i], rstd = consts[4 * i + 1], m1 = consts[4 * i + 2], m2 = consts[4 * i + 3];
-      float dsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-      if (okl) {
-        const size_t off = ((size_t)bb * L + l) * CH + c8 * 8;
-        float dv[8], sv[8];
-        unpack8(*reinterpret_cast<const uint4*>(dh + off), dv);
-        unpack8(*reinterpret_cast<const uint4*>(s + off), sv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float xh = (sv[e] - mean) * rstd;
-          dg[e] += dv[e] * xh;
-          db[e] += dv[e];
-          dsv[e] = rstd * (dv[e] * gam[e] - m1 - xh * m2);
-        }
-        if (ds != nullptr) {
-          const uint4 qv = packq8(dsv);
-          *reinterpret_cast<uint4*>(ds + off) = qv;
-          unpack8(qv, dsv);
-        }
-      }
-      if (dgb != nullptr) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) red[pl * CH + c8 * 8 + e] = dsv[e];
-        __syncthreads();
-        if (tid < CH) {
-          float a = 0.f;
-#pragma unroll
-          for (int k = 0; k < 16; ++k) a += red[k * CH + tid];
-          atomicAdd(dgb + (size_t)bb * CH + tid, a);
-        }
-        __syncthreads();
-      }
-    }
-  }
-  if (okl) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      atomicAdd(dgamma + (size_t)l * CH + c8 * 8 + e, dg[e]);
-      atomicAdd(dbeta + (size_t)l * CH + c8 * 8 + e, db[e]);
-    }
   }
 }
 
@@ -501,18 +555,22 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restr
   for (int i = threadIdx.x; i < V * CH; i += 256) atomicAdd(dE + i, acc[i]);
 }
 
-int grid_for(int tiles) {
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) {
-    hipDeviceProp_t p;
-    if (hipGetDeviceProperties(&p, dev) == hipSuccess) cus = p.multiProcessorCount;
-  }
-  return tiles < cus ? tiles : cus;
-}
 int g_cus = -1;
-int persistent_grid(int tiles) {
-  if (g_cus < 0) g_cus = grid_for(1 << 30);
-  return tiles < g_cus ? (tiles > 0 ? tiles : 1) : g_cus;
+int num_cus() {
+  if (g_cus < 0) {
+    int dev = 0;
+    g_cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t p;
+      if (hipGetDeviceProperties(&p, dev) == hipSuccess) g_cus = p.multiProcessorCount;
+    }
+  }
+  return g_cus;
+}
+// persistent grid: at most `per_cu` workgroups per CU, never more than the tile count
+int persistent_grid(int tiles, int per_cu) {
+  const int cap = num_cus() * per_cu;
+  return tiles < cap ? (tiles > 0 ? tiles : 1) : cap;
 }
 }  // namespace
 
@@ -524,56 +582,68 @@ static void set_ln_attrs() {
   ln_attrs_set = true;
 }
 
+static int ln_groups(int B, int L) {
+  const int tp = (L + PB - 1) / PB;
+  int g = (2 * num_cus() + tp - 1) / tp;          // ~2 workgroups of 8 waves per CU
+  return g < 1 ? 1 : (g > B ? B : g);
+}
+
 PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int BM1, const float* g1,
                                  const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
                                  float* st2, int B, int L, float eps, hipStream_t st) {
-  const int T2 = (L + BML - 1) / BML;
-  hipLaunchKernelGGL(ln_linear_fwd_kernel, dim3(persistent_grid(B * T2)), dim3(256), 32768 + 64, st,
-                     (const bf16_t*)s1, st1, T1, BM1, g1, be1, (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2,
-                     st2, B, L, eps);
+  dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
+  const int lds = 32768 + PB * 256 + PB * CH * 4 + 128;
+  hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
+                     (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
   return pbx_launch_status();
 }
 
+// nw: waves per workgroup (tile = 32 nw positions); vpart is [B][ceil(L / (32 nw))][NJ]
 PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
-                               void* h2, float* vpart, int B, int L, int NJ, float eps, hipStream_t st) {
+                               void* h2, float* vpart, int B, int L, int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 32 != 0 || NJ * 256 + NJ * 4 > 163840) return (int)hipErrorInvalidValue;
-  const int T2 = (L + BML - 1) / BML;
-  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3(persistent_grid(B * T2)), dim3(256), NJ * 256 + NJ * 4, st,
+  if (NJ % 64 != 0 || NJ * 256 + NJ * 4 > 163840 || nw < 1 || nw > 16) return (int)hipErrorInvalidValue;
+  const int TA = (L + 32 * nw - 1) / (32 * nw);
+  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + NJ * 4, st,
                      (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, B, L, NJ, eps);
   return pbx_launch_status();
 }
 
+// dvpart rows follow the forward tiling (bmv positions); sums2 is [B][ceil(L / (32 nw))][2]
 PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
-                            const float* dvpart, const void* wv, void* dh2, float* sums2, int B, int L, int NJ,
-                            float eps, hipStream_t st) {
+                            const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
+                            int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 32 != 0 || NJ * 256 + 64 > 163840) return (int)hipErrorInvalidValue;
-  const int T2 = (L + BML - 1) / BML;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(persistent_grid(B * T2)), dim3(256), NJ * 256 + 64, st,
-                     (const bf16_t*)h2, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart,
+  if (NJ % 64 != 0 || NJ * 256 + 128 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  const int TA = (L + 32 * nw - 1) / (32 * nw);
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + 128, st,
+                     (const bf16_t*)h2, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
                      (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ, eps);
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2,
+// dg2/db2/dg1/db1 ([L, C] fp32) are accumulated into (atomics)
+PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
                                   int BM1, const float* g1, const float* be1, const void* wl, void* dh1,
-                                  void* dpre, void* h1, float* sums1, int B, int L, float eps, hipStream_t st) {
-  const int T2 = (L + BML - 1) / BML;
-  hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(persistent_grid(B * T2)), dim3(256), 32768 + 64, st,
-                     (const bf16_t*)dh2, (const bf16_t*)s2, st2, sums2, g2, (const bf16_t*)pre_l,
-                     (const bf16_t*)s1, st1, T1, BM1, g1, be1, (const bf16_t*)wl, (bf16_t*)dh1, (bf16_t*)dpre,
-                     (bf16_t*)h1, sums1, B, L, eps);
+                                  void* dpre, void* h1, float* sums1, float* dg2, float* db2, float* dg1,
+                                  float* db1, int B, int L, float eps, hipStream_t st) {
+  dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
+  const int lds = 32768 + PB * 256 + PB * CH * 4 + 128;
+  hipLaunchKernelGGL(ln2_linear_bwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh2, (const bf16_t*)s2, st2,
+                     sums2, TS2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
+                     (const bf16_t*)wl, (bf16_t*)dh1, (bf16_t*)dpre, (bf16_t*)h1, sums1, dg2, db2, dg1, db1, B, L,
+                     eps);
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_ln_affine_bwd(const void* dh, const void* s, const float* stp, int Tst, int BMst,
-                                 const float* sums, int Tsm, const float* gamma, float* dgamma, float* dbeta,
-                                 void* ds, float* dgb, int B, int L, int nbg, float eps, hipStream_t st) {
-  dim3 grid((L + 15) / 16, nbg);
-  hipLaunchKernelGGL(ln_affine_bwd_kernel, grid, dim3(256), 0, st, (const bf16_t*)dh, (const bf16_t*)s, stp, Tst,
-                     BMst, sums, Tsm, gamma, dgamma, dbeta, (bf16_t*)ds, dgb, B, L, eps);
+// dgb ([B, 128] fp32) is accumulated into
+PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
+                                const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
+                                float eps, hipStream_t st) {
+  dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
+  hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), 0, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
+                     BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, B, L, eps);
   return pbx_launch_status();
 }
 

@@ -22,29 +22,39 @@ from typing import Dict, Optional, Tuple
 import torch
 
 from . import _lib
+from ..train.arena import notify_grads_ready
 
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
-_lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv", [_P, _P, _P, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
-_lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
-_lib.register("pbx_attn_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
-_lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I,
-                                     _F, _P])
-_lib.register("pbx_ln_affine_bwd", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_attn_bwd", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
+                                     _P, _P, _P, _I, _I, _F, _P])
+_lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
 
 CH = 128          # kernels are specialised for local_dim = 128
-BML = 128         # LN-kernel tile (positions)
+PB = 32           # positions per workgroup of the position-major LayerNorm kernels
 LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 
 
 def conv_tile(L: int) -> int:
     return 256 if L >= 256 else 128
+
+
+def attn_fwd_waves(L: int) -> int:
+    """ln_attn_fwd workgroup: 16 waves (4 per SIMD) when the sequence fills them."""
+    return max(4, min(16, (L + 31) // 32))
+
+
+def attn_bwd_waves(L: int) -> int:
+    return max(4, min(8, (L + 31) // 32))
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -65,21 +75,26 @@ def pack_conv(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     return wp, wt
 
 
+def _grad_dst(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
+    """Accumulate straight into the parameter's (arena) .grad when it exists, else a new tensor."""
+    g = getattr(p, "grad", None) if getattr(p, "_pbx_arena", False) else None
+    if g is not None and g.is_contiguous() and g.dtype == torch.float32 and tuple(g.shape) == tuple(shape):
+        return g, True
+    return torch.zeros(shape, dtype=torch.float32, device=p.device), False
+
+
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
-           B: int, L: int):
+           B: int, L: int, outs):
+    """outs: [(dw, db)] destinations (accumulated into)."""
     dev = x.device
     ntiles = B * ((L + 127) // 128)
     R = max(1, min(ntiles, (2 * _num_cus(dev)) // (4 * nconv)))
     slab = torch.empty((R, nconv, KS, CH, CH), dtype=torch.float32, device=dev)
     bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
-    shape = (CH, CH, KS) if KS > 1 else (CH, CH)
-    dw0 = torch.empty(shape, dtype=torch.float32, device=dev)
-    db0 = torch.empty(CH, dtype=torch.float32, device=dev)
-    dw1 = torch.empty(shape, dtype=torch.float32, device=dev) if nconv > 1 else None
-    db1 = torch.empty(CH, dtype=torch.float32, device=dev) if nconv > 1 else None
+    (dw0, db0) = outs[0]
+    (dw1, db1) = outs[1] if nconv > 1 else (None, None)
     _lib.call("pbx_wgrad", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
-              dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, KS, dil, nconv, R, _lib.stream_ptr(dev))
-    return dw0, db0, dw1, db1
+              dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, KS, dil, nconv, R, 1, _lib.stream_ptr(dev))
 
 
 class LocalBlockFn(torch.autograd.Function):
@@ -87,6 +102,7 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int):
+        params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
         B, L, C = x.shape
         assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
         KS = wn.shape[2]
@@ -94,7 +110,7 @@ class LocalBlockFn(torch.autograd.Function):
         stream = _lib.stream_ptr(dev)
         BM1 = conv_tile(L)
         T1 = (L + BM1 - 1) // BM1
-        T2 = (L + BML - 1) // BML
+        T2 = (L + PB - 1) // PB
         wpn, wtn = pack_conv(wn)
         wpw, wtw = pack_conv(ww)
         wl_b = wl.detach().to(torch.bfloat16).contiguous()
@@ -113,61 +129,67 @@ class LocalBlockFn(torch.autograd.Function):
                   wl_b.data_ptr(), bl.data_ptr(), pre_l.data_ptr(), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS,
                   stream)
         NJ = wv_bf16.shape[0]
+        nwf = attn_fwd_waves(L)
+        TV = (L + 32 * nwf - 1) // (32 * nwf)
         h2 = torch.empty_like(x)
-        vpart = torch.empty((B, T2, NJ), dtype=torch.float32, device=dev)
+        vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                  wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, LN_EPS, stream)
+                  wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
-        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ)
+        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 32 * nwf)
+        ctx.params = params
         return h2, vpart
 
     @staticmethod
     def backward(ctx, dh2, dvpart):
         (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
-        B, L, KS, dil, BM1, T1, T2, NJ = ctx.meta
+        B, L, KS, dil, BM1, T1, T2, NJ, BMV = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
+        params = ctx.params
+        dsts = [_grad_dst(p, p.shape) for p in params]
+        (dwn, _), (dbn, _), (dww, _), (dbw, _), (dg1, _), (dbe1, _), (dwl, _), (dbl, _), (dg2, _), (dbe2, _) = dsts
         dh2 = None if dh2 is None else dh2.to(torch.bfloat16).contiguous()
+        TV = (L + BMV - 1) // BMV
         if dvpart is None:
-            dvpart = torch.zeros((B, T2, NJ), dtype=torch.float32, device=dev)
+            dvpart = torch.zeros((B, TV, NJ), dtype=torch.float32, device=dev)
         dvpart = dvpart.float().contiguous()
-        nbg = max(1, min(B, (2 * _num_cus(dev)) // max(1, (L + 15) // 16)))
         # attention pool + LN2 partials
+        nwb = attn_bwd_waves(L)
+        TA = (L + 32 * nwb - 1) // (32 * nwb)
         dh2t = torch.empty_like(x)
-        sums2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
+        sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_attn_bwd", h2.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                  dvpart.data_ptr(), wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                  stream)
-        dg2 = torch.zeros((L, CH), dtype=torch.float32, device=dev)
-        dbe2 = torch.zeros_like(dg2)
-        _lib.call("pbx_ln_affine_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), T2, BML, sums2.data_ptr(),
-                  T2, g2.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), None, None, B, L, nbg, LN_EPS, stream)
-        # LN2 finalize + local MLP backward + LN1 partials
+                  dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, nwb,
+                  LN_EPS, stream)
+        # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
         dh1 = torch.empty_like(x)
         dprel = torch.empty_like(x)
         h1 = torch.empty_like(x)
         sums1 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(),
+        _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(), TA,
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), dh1.data_ptr(), dprel.data_ptr(), h1.data_ptr(),
-                  sums1.data_ptr(), B, L, LN_EPS, stream)
-        dwl, dbl, _, _ = _wgrad(dprel, None, h1, 1, 1, 1, B, L)
-        # LN1 affine + finalize (ds1) + gradient of the broadcast global->local vector
-        dg1 = torch.zeros((L, CH), dtype=torch.float32, device=dev)
-        dbe1 = torch.zeros_like(dg1)
+                  sums1.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), B, L, LN_EPS,
+                  stream)
+        _wgrad(dprel, None, h1, 1, 1, 1, B, L, [(dwl, dbl)])
+        # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
         dgb = torch.zeros((B, CH), dtype=torch.float32, device=dev)
-        _lib.call("pbx_ln_affine_bwd", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
-                  T2, g1.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, nbg,
-                  LN_EPS, stream)
+        _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(), T2,
+                  g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, stream)
         # convolutions
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
         _lib.call("pbx_conv_dgrad", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
                   wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, BM1, stream)
-        dwn, dbn, dww, dbw = _wgrad(dpn, dpw, x, KS, dil, 2, B, L)
-        return dx, dgb, dwn, dbn, dww, dbw, dg1, dbe1, dwl, dbl, dg2, dbe2, None, None
+        _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
+        direct = [p for p, (_, d) in zip(params, dsts) if d]
+        if direct:
+            notify_grads_ready(direct)
+        pgrads = [None if d else g for (g, d) in dsts]
+        return (dx, dgb, *pgrads, None, None)
 
 
 class EmbedFn(torch.autograd.Function):

@@ -28,7 +28,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
-from ..train.arena import FlatArena
+from ..train.arena import FlatArena, add_grad_ready_listener, remove_grad_ready_listener
 
 
 class BucketedAllReduce:
@@ -64,9 +64,11 @@ class BucketedAllReduce:
         self._next = 0
         self._hooks = []
         self.enabled = self.world > 1
+        self._index = {id(p): i for i, p in enumerate(arena.params)}
         if self.enabled:
             for i, p in enumerate(arena.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+            add_grad_ready_listener(self._on_direct_grads)
 
     # --------------------------------------------------------------------------------
     def _make_hook(self, idx: int):
@@ -77,6 +79,16 @@ class BucketedAllReduce:
             if self._pending[b] == 0:
                 self._launch_ready()
         return hook
+
+    def _on_direct_grads(self, params) -> None:
+        """Gradients written in place by a fused backward kernel (no AccumulateGrad hook)."""
+        for p in params:
+            i = self._index.get(id(p))
+            if i is None:
+                continue
+            b = self.param_bucket[i]
+            self._pending[b] -= 1
+        self._launch_ready()
 
     def _dtype_for(self, b: int) -> torch.dtype:
         if self.tail_bf16 and b == len(self.buckets) - 1:
@@ -134,3 +146,4 @@ class BucketedAllReduce:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        remove_grad_ready_listener(self._on_direct_grads)

@@ -49,6 +49,7 @@ class FlatArena:
             for p, (o, n) in zip(self.params, self.offsets):
                 self.data[o:o + n].copy_(p.detach().reshape(-1).float())
                 p.data = self.data[o:o + n].view(p.shape)
+                p._pbx_arena = True  # fused backward kernels may accumulate into p.grad directly
         self.attach_grads()
 
     def attach_grads(self) -> None:
@@ -72,3 +73,25 @@ class FlatArena:
 
     def segment(self, i: int) -> Tuple[int, int]:
         return self.offsets[i]
+
+
+# --- direct gradient writes ---------------------------------------------------------------------
+# Fused backward kernels (ops.local_track) accumulate parameter gradients straight into the arena
+# ``.grad`` views instead of returning them to autograd (which would launch one add kernel per
+# parameter).  AccumulateGrad -- and with it ``post_accumulate_grad`` hooks -- then never runs for
+# those parameters, so consumers that track gradient readiness (the DP bucketer) subscribe here.
+_grad_ready_listeners = []
+
+
+def add_grad_ready_listener(fn) -> None:
+    _grad_ready_listeners.append(fn)
+
+
+def remove_grad_ready_listener(fn) -> None:
+    if fn in _grad_ready_listeners:
+        _grad_ready_listeners.remove(fn)
+
+
+def notify_grads_ready(params) -> None:
+    for fn in list(_grad_ready_listeners):
+        fn(params)

@@ -134,3 +134,29 @@ def test_full_model_loss_and_grads_vs_torch():
         # the local-output bias is a softmax-over-batch invariant: its exact gradient
         # is 0, so it is checked against the gradient scale of the model, not relative to itself
         assert err < 6e-2 * norms[n] + 1e-4 * scale, f"{n}: err {err:.3e} vs |g| {norms[n]:.3e}"
+
+
+def test_arena_direct_grads_match_autograd_path():
+    """Training path: fused backward accumulates straight into the flat-arena .grad views."""
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.train.optim import FusedAdam
+    from proteinbert_pytorch_replication_amd.train.step import PretrainStep
+    torch.manual_seed(0)
+    L, A = 128, 512
+    m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=256, key_dim=64, num_heads=4,
+                    num_blocks=2, device="cuda", backend="hip")
+    opt = FusedAdam(m.parameters(), lr=1e-3)
+    step = PretrainStep(m, opt)
+    X, Y, W = SyntheticUniRefGO(L, A, 8, "cuda", seed=5).next_batch()
+    opt.zero_grad()
+    step.loss(X, Y, W).backward()
+    direct = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    opt.zero_grad()
+    m.backend = "torch"
+    step.loss(X, Y, W).backward()
+    ref = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    torch.cuda.synchronize()
+    scale = sorted(r.norm().item() for r in ref.values())[len(ref) // 2]
+    for n in ref:
+        err = (direct[n] - ref[n]).norm().item()
+        assert err < 6e-2 * ref[n].norm().item() + 1e-4 * scale, f"{n}: err {err:.3e} |g| {ref[n].norm().item():.3e}"
