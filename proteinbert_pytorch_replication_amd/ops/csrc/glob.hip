@@ -1,0 +1,391 @@
+// Global (per-protein) track, pretraining heads and losses.
+//
+// Reference: ProteinBERT/modules.py:175-199,221-229 (two Linear G->G + GELU + residual + LayerNorm(G)
+// per block), :21-92 (attention output scaled by sum(W)/K in reference semantics), :277-293 (local
+// head Linear C->V + nn.Softmax() over the BATCH axis, GO head Linear G->A + Sigmoid) and
+// ProteinBERT/utils.py:293-294 (CE applied to the local probabilities, BCE with log clamp -100,
+// weighted means over B*L and B*A).
+//
+// The [B, G] GEMMs run on hipBLASLt (bf16 in, fp32 out); everything around them is fused here:
+//   row_ln_fwd  : z = res + GELU(u + b) [+ scale * sum_t vpart] -> LayerNorm(G)  (one row / workgroup)
+//   row_ln_bwd  : LayerNorm + GELU backward, affine/bias gradients (accumulated in place), the
+//                 attention-scale gradient and the gradient of the attention partial sums
+//   local_head  : logits, softmax over the batch, CE on the probabilities, and the whole backward
+//                 (the loss is terminal, so gradients are produced in the forward pass)
+//   go_head     : sigmoid + BCE + weighted mean + dlogits in one pass over [B, A]
+#include "common.h"
+
+typedef unsigned short bf16_t;
+
+namespace {
+constexpr int MAXG = 1024;   // global_dim supported by the row kernels (<= 4 values per thread)
+
+__device__ __forceinline__ float block_reduce(float v, float* red) {
+  v = wave_reduce_sum(v);
+  const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  return s;
+}
+
+// grid (B), block 256.  u: [B, G] GEMM output (no bias); out = LN(z)
+__global__ void __launch_bounds__(256) row_ln_fwd_kernel(
+    const float* __restrict__ u, const float* __restrict__ bias, const float* __restrict__ res,
+    const float* __restrict__ vpart, int TV, const float* __restrict__ wp, int K, const float* __restrict__ gamma,
+    const float* __restrict__ beta, float* __restrict__ out, bf16_t* __restrict__ out_bf, float* __restrict__ xhat,
+    float* __restrict__ rstd_out, float* __restrict__ vsum, int G, float eps) {
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  float scale = 0.f;
+  if (vpart != nullptr) {
+    float s = 0.f;
+    for (int i = 0; i < K; ++i) s += wp[i];
+    scale = s / (float)K;
+  }
+  float z[4];
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    z[i] = 0.f;
+    if (c < G) {
+      float v = res[(size_t)b * G + c] + gelu_f(u[(size_t)b * G + c] + bias[c]);
+      if (vpart != nullptr) {
+        float vs = 0.f;
+        for (int t = 0; t < TV; ++t) vs += vpart[((size_t)b * TV + t) * G + c];
+        vsum[(size_t)b * G + c] = vs;
+        v += scale * vs;
+      }
+      z[i] = v;
+      sum += v;
+    }
+  }
+  const float mean = block_reduce(sum, red) / (float)G;
+  float var = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    if (c < G) var += (z[i] - mean) * (z[i] - mean);
+  }
+  var = block_reduce(var, red) / (float)G;
+  const float rstd = rsqrtf(var + eps);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    if (c < G) {
+      const float xh = (z[i] - mean) * rstd;
+      const float o = xh * gamma[c] + beta[c];
+      xhat[(size_t)b * G + c] = xh;
+      out[(size_t)b * G + c] = o;
+      out_bf[(size_t)b * G + c] = f2bf(o);
+    }
+  }
+  if (tid == 0) rstd_out[b] = rstd;
+}
+
+// grid (B), block 256.  dout: [B, G] gradient of the LN output.
+//   dz = rstd (dout g - mean(dout g) - xhat mean(dout g xhat))
+//   dgamma += dout xhat ; dbeta += dout ; du = dz GELU'(u + b) (bf16, GEMM operand) ; dbias += du
+//   dres = dz (fp32) ; with vpart: dvs = scale dz, dWp[i] += sum(dz vsum) / K
+__global__ void __launch_bounds__(256) row_ln_bwd_kernel(
+    const float* __restrict__ dout, const float* __restrict__ xhat, const float* __restrict__ rstd_in,
+    const float* __restrict__ gamma, const float* __restrict__ u, const float* __restrict__ bias,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, float* __restrict__ dbias, bf16_t* __restrict__ du,
+    float* __restrict__ dres, const float* __restrict__ vsum, const float* __restrict__ wp, int K,
+    float* __restrict__ dwp, float* __restrict__ dvs, int G) {
+  __shared__ float red[8];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float rstd = rstd_in[b];
+  float dxh[4], xh[4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    dxh[i] = 0.f;
+    xh[i] = 0.f;
+    if (c < G) {
+      const float d = dout[(size_t)b * G + c];
+      xh[i] = xhat[(size_t)b * G + c];
+      dxh[i] = d * gamma[c];
+      s1 += dxh[i];
+      s2 += dxh[i] * xh[i];
+      atomicAdd(dgamma + c, d * xh[i]);
+      atomicAdd(dbeta + c, d);
+    }
+  }
+  const float m1 = block_reduce(s1, red) / (float)G;
+  const float m2 = block_reduce(s2, red) / (float)G;
+  float scale = 0.f;
+  if (vsum != nullptr) {
+    float s = 0.f;
+    for (int i = 0; i < K; ++i) s += wp[i];
+    scale = s / (float)K;
+  }
+  float ds = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int c = tid + 256 * i;
+    if (c < G) {
+      const float dz = rstd * (dxh[i] - m1 - xh[i] * m2);
+      dres[(size_t)b * G + c] = dz;
+      const float g = dz * gelu_grad_f(u[(size_t)b * G + c] + bias[c]);
+      du[(size_t)b * G + c] = f2bf(g);
+      atomicAdd(dbias + c, g);
+      if (vsum != nullptr) {
+        dvs[(size_t)b * G + c] = scale * dz;
+        ds += dz * vsum[(size_t)b * G + c];
+      }
+    }
+  }
+  if (vsum != nullptr) {
+    ds = block_reduce(ds, red);
+    if (tid < K) atomicAdd(dwp + tid, ds / (float)K);
+  }
+}
+
+// out = GELU(u + b) (fp32 and bf16 copies); used for the global input layer and gb = global->local
+__global__ void __launch_bounds__(256) bias_gelu_kernel(const float* __restrict__ u, const float* __restrict__ bias,
+                                                        float* __restrict__ out, bf16_t* __restrict__ out_bf,
+                                                        int n, int N) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float v = gelu_f(u[i] + bias[i % N]);
+  if (out != nullptr) out[i] = v;
+  if (out_bf != nullptr) out_bf[i] = f2bf(v);
+}
+
+// du = dout * GELU'(u + b) (bf16) ; dbias += column sums
+__global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const float* __restrict__ dout,
+                                                            const float* __restrict__ u,
+                                                            const float* __restrict__ bias, bf16_t* __restrict__ du,
+                                                            float* __restrict__ dbias, int M, int N) {
+  // grid (ceil(N/256), ceil(M/rows_per_block)); each thread owns one column for a run of rows
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= N) return;
+  const int rpb = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rpb, r1 = min(M, r0 + rpb);
+  float acc = 0.f;
+  const float bc = bias[c];
+  for (int r = r0; r < r1; ++r) {
+    const float g = dout[(size_t)r * N + c] * gelu_grad_f(u[(size_t)r * N + c] + bc);
+    du[(size_t)r * N + c] = f2bf(g);
+    acc += g;
+  }
+  atomicAdd(dbias + c, acc);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Local head + loss, reference semantics (modules.py:277-284, utils.py:293):
+//   z[b,l,v] = h[b,l] . Wo[v] + bo[v] ; P = softmax over b of z[., l, v]
+//   loss_bl = logsumexp_v P[b,l,:] - P[b,l,y]          (CrossEntropyLoss applied to probabilities)
+//   L_loc = sum_bl w_bl loss_bl / (B L)
+// backward (in the same pass): G = w/(BL) (softmax_v(P) - onehot(y)); dz = P (G - sum_b G P);
+//   dh = dz Wo (bf16) ; dWo += dz^T h ; dbo += sum dz.
+// grid (L), block 256: one position l per workgroup, all B samples (B <= 1024).
+__global__ void __launch_bounds__(256) local_head_kernel(
+    const bf16_t* __restrict__ h, const float* __restrict__ wo, const float* __restrict__ bo,
+    const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, bf16_t* __restrict__ dzo,
+    float* __restrict__ dbo, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* W = sm;                       // [V][128]
+  float* zs = W + V * 128;             // [B][V]  logits -> probabilities -> dz
+  float* red = zs + B * V;             // [8][V]  per-wave reductions
+  float* colv = red + 8 * V;           // [V]
+  const int tid = threadIdx.x, l = blockIdx.x;
+  const int lane = tid & 63;
+  for (int i = tid; i < V * 128; i += 256) W[i] = wo[i];
+  __syncthreads();
+  // logits: thread per (sample, v) pair
+  for (int i = tid; i < B * V; i += 256) {
+    const int b = i / V, v = i - (i / V) * V;
+    const bf16_t* hr = h + ((size_t)b * L + l) * 128;
+    float acc = bo[v];
+#pragma unroll 4
+    for (int c8 = 0; c8 < 16; ++c8) {
+      const uint4 q = *reinterpret_cast<const uint4*>(hr + c8 * 8);
+      const float hv[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                           __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u),
+                           __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
+                           __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = fmaf(hv[e], W[v * 128 + c8 * 8 + e], acc);
+    }
+    zs[i] = acc;
+  }
+  __syncthreads();
+  // softmax over b for each v: column max and sum (threads v, strided over b by 256/V groups)
+  if (tid < V) {
+    float m = -3.4e38f;
+    for (int b = 0; b < B; ++b) m = fmaxf(m, zs[b * V + tid]);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) s += __expf(zs[b * V + tid] - m);
+    red[tid] = m;
+    red[V + tid] = 1.0f / s;
+  }
+  __syncthreads();
+  for (int i = tid; i < B * V; i += 256) {
+    const int v = i - (i / V) * V;
+    zs[i] = __expf(zs[i] - red[v]) * red[V + v];
+  }
+  __syncthreads();
+  // per (b, l): CE over v on the probabilities; G stored in place of P? keep P, accumulate colv = sum_b G P
+  float lsum = 0.f;
+  if (tid < V) colv[tid] = 0.f;
+  __syncthreads();
+  for (int b = tid; b < B; b += 256) {
+    const float* p = zs + b * V;
+    float mx = -3.4e38f;
+    for (int v = 0; v < V; ++v) mx = fmaxf(mx, p[v]);
+    float se = 0.f;
+    for (int v = 0; v < V; ++v) se += __expf(p[v] - mx);
+    const int yv = (int)y[(size_t)b * L + l];
+    const float wgt = wl[(size_t)b * L + l];
+    lsum += wgt * (mx + __logf(se) - p[yv]);
+    const float coef = wgt * inv_bl;
+    const float inv_se = 1.0f / se;
+    for (int v = 0; v < V; ++v) {
+      const float g = coef * (__expf(p[v] - mx) * inv_se - (v == yv ? 1.f : 0.f));
+      atomicAdd(&colv[v], g * p[v]);
+    }
+  }
+  __syncthreads();
+  // dz = P (G - colv), recomputing G per element
+  for (int b = tid; b < B; b += 256) {
+    float* p = zs + b * V;
+    float mx = -3.4e38f;
+    for (int v = 0; v < V; ++v) mx = fmaxf(mx, p[v]);
+    float se = 0.f;
+    for (int v = 0; v < V; ++v) se += __expf(p[v] - mx);
+    const int yv = (int)y[(size_t)b * L + l];
+    const float coef = wl[(size_t)b * L + l] * inv_bl;
+    const float inv_se = 1.0f / se;
+    for (int v = 0; v < V; ++v) {
+      const float g = coef * (__expf(p[v] - mx) * inv_se - (v == yv ? 1.f : 0.f));
+      p[v] = p[v] * (g - colv[v]);
+    }
+  }
+  __syncthreads();
+  // dh[b,l,:] = sum_v dz[b,v] Wo[v,:]  (thread per (b, 8-channel chunk)); dWo += dz^T h
+  for (int i = tid; i < B * 16; i += 256) {
+    const int b = i >> 4, c8 = i & 15;
+    const float* dz = zs + b * V;
+    float o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int v = 0; v < V; ++v) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(dz[v], W[v * 128 + c8 * 8 + e], o[e]);
+    }
+    uint4 q;
+    q.x = (unsigned)f2bf(o[0]) | ((unsigned)f2bf(o[1]) << 16);
+    q.y = (unsigned)f2bf(o[2]) | ((unsigned)f2bf(o[3]) << 16);
+    q.z = (unsigned)f2bf(o[4]) | ((unsigned)f2bf(o[5]) << 16);
+    q.w = (unsigned)f2bf(o[6]) | ((unsigned)f2bf(o[7]) << 16);
+    *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) = q;
+  }
+  // dz rows (padded to 32 logits) for the dWo = dz^T h GEMM
+  for (int i = tid; i < B * 32; i += 256) {
+    const int b = i >> 5, v = i & 31;
+    dzo[((size_t)b * L + l) * 32 + v] = v < V ? f2bf(zs[b * V + v]) : (bf16_t)0;
+  }
+  if (tid < V) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += zs[b * V + tid];
+    atomicAdd(dbo + tid, a);
+  }
+  lsum = wave_reduce_sum(lsum);
+  if (lane == 0) atomicAdd(loss, lsum * inv_bl);
+}
+
+// GO head: P = sigmoid(z), BCE(P, y) with PyTorch's log clamp (>= -100) and backward
+// dz = w/(BA) (P - y) P(1-P) / max(P(1-P), 1e-12)   (BCELoss backward x sigmoid backward).
+// z: [B, A] fp32 (GEMM output without bias); weights w[r * wsr + c * wsc] (wsc = 0: one per row)
+__global__ void __launch_bounds__(256) go_head_kernel(const float* __restrict__ z, const float* __restrict__ bias,
+                                                      const float* __restrict__ y, const float* __restrict__ wgt_p,
+                                                      long wsr, long wsc, bf16_t* __restrict__ dz,
+                                                      float* __restrict__ dbias, float* __restrict__ loss, int B,
+                                                      int A, float inv_ba) {
+  // thread owns column c for a run of rows (column bias gradient in registers)
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  const int rpb = (B + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rpb, r1 = min(B, r0 + rpb);
+  float lsum = 0.f, dsum = 0.f;
+  if (c < A) {
+    const float bc = bias[c];
+    for (int r = r0; r < r1; ++r) {
+      const size_t i = (size_t)r * A + c;
+      const float zz = z[i] + bc;
+      const float p = 1.0f / (1.0f + __expf(-zz));
+      const float yy = y[i];
+      const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.0f - p), -100.f);
+      const float wgt = wgt_p[r * wsr + c * wsc];
+      lsum += wgt * -(yy * lp + (1.0f - yy) * l1p);
+      const float pq = p * (1.0f - p);
+      const float g = wgt * inv_ba * (p - yy) * pq / fmaxf(pq, 1e-12f);
+      dz[i] = f2bf(g);
+      dsum += g;
+    }
+    atomicAdd(dbias + c, dsum);
+  }
+  lsum = wave_reduce_sum(lsum);
+  if ((threadIdx.x & 63) == 0) atomicAdd(loss, lsum * inv_ba);
+}
+}  // namespace
+
+PBX_EXPORT int pbx_row_ln_fwd(const float* u, const float* bias, const float* res, const float* vpart, int TV,
+                              const float* wp, int K, const float* gamma, const float* beta, float* out, void* out_bf,
+                              float* xhat, float* rstd, float* vsum, int B, int G, float eps, hipStream_t st) {
+  if (G > MAXG) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_ln_fwd_kernel, dim3(B), dim3(256), 0, st, u, bias, res, vpart, TV, wp, K, gamma, beta, out,
+                     (bf16_t*)out_bf, xhat, rstd, vsum, G, eps);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_row_ln_bwd(const float* dout, const float* xhat, const float* rstd, const float* gamma,
+                              const float* u, const float* bias, float* dgamma, float* dbeta, float* dbias, void* du,
+                              float* dres, const float* vsum, const float* wp, int K, float* dwp, float* dvs, int B,
+                              int G, hipStream_t st) {
+  if (G > MAXG || (vsum != nullptr && K > 256)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_ln_bwd_kernel, dim3(B), dim3(256), 0, st, dout, xhat, rstd, gamma, u, bias, dgamma, dbeta,
+                     dbias, (bf16_t*)du, dres, vsum, wp, K, dwp, dvs, G);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_bias_gelu(const float* u, const float* bias, float* out, void* out_bf, int M, int N,
+                             hipStream_t st) {
+  const int n = M * N;
+  hipLaunchKernelGGL(bias_gelu_kernel, dim3((n + 255) / 256), dim3(256), 0, st, u, bias, out, (bf16_t*)out_bf, n, N);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float* bias, void* du, float* dbias, int M,
+                                 int N, hipStream_t st) {
+  const int gy = M < 32 ? M : 32;
+  hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((N + 255) / 256, gy), dim3(256), 0, st, dout, u, bias, (bf16_t*)du,
+                     dbias, M, N);
+  return pbx_launch_status();
+}
+
+// dzo: [B*L][32] bf16 (dz of the V logits, zero padded) for the dWo GEMM
+PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
+                              void* dh, void* dzo, float* dbo, float* loss, int B, int L, int V, hipStream_t st) {
+  const int lds = (V * 128 + B * V + 9 * V) * 4;
+  if (V > 32 || lds > 163840) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)local_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    attr = true;
+  }
+  hipLaunchKernelGGL(local_head_kernel, dim3(L), dim3(256), lds, st, (const bf16_t*)h, wo, bo, (const long long*)y,
+                     wl, (bf16_t*)dh, (bf16_t*)dzo, dbo, loss, B, L, V, 1.0f / ((float)B * (float)L));
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, const float* w, long wsr, long wsc,
+                           void* dz, float* dbias, float* loss, int B, int A, hipStream_t st) {
+  const int gy = B < 16 ? B : 16;
+  hipLaunchKernelGGL(go_head_kernel, dim3((A + 255) / 256, gy), dim3(256), 0, st, z, bias, y, w, wsr, wsc,
+                     (bf16_t*)dz, dbias, loss, B, A, 1.0f / ((float)B * (float)A));
+  return pbx_launch_status();
+}

@@ -12,8 +12,8 @@ from typing import Dict, Tuple
 import torch
 import torch.nn.functional as F
 
+from .global_track import GlobalBlockFn, HeadsLossFn, InputLayerFn
 from .local_track import CH, EmbedFn, local_block
-from ..train.losses import pretrain_loss_torch
 
 
 def hip_supported(model) -> Tuple[bool, str]:
@@ -37,27 +37,28 @@ def _check(model) -> None:
         raise NotImplementedError(f"HIP backend: unsupported configuration: {why}")
 
 
-def _gelu_linear(x: torch.Tensor, seq) -> torch.Tensor:
-    lin = seq[0]
-    return F.gelu(F.linear(x, lin.weight, lin.bias))
-
-
-def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
+                 return_bf16: bool = False):
+    """Encoder on the HIP path: returns ``h [B, L, 128]`` (bf16) and ``g [B, G]`` (fp32)."""
     _check(model)
-    h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
+    blocks = list(model.proteinBERT_blocks)
     lin = model.global_linear_layer[0]
-    g = F.gelu(F.linear(annotations.to(torch.bfloat16), lin.weight.to(torch.bfloat16),
-                        lin.bias.to(torch.bfloat16))).float()                    # [B,G]
-    for blk in model.proteinBERT_blocks:
-        gb = _gelu_linear(g, blk.global_to_local_linear_layer)                   # [B,128]
+    g, g_bf = InputLayerFn.apply(annotations, lin.weight, lin.bias)
+    h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
+    # gb for block 0; every GlobalBlockFn produces the next block's gb
+    gl0 = blocks[0].global_to_local_linear_layer[0]
+    gb = F.gelu(F.linear(g, gl0.weight, gl0.bias))
+    for i, blk in enumerate(blocks):
         h, vpart = local_block(h, gb, blk)
         att = blk.global_attention_layer
-        ga = vpart.sum(dim=1) * (att.W_parameter.sum() / att.key_dim)           # [B,G]
+        nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
+        l1, l2 = blk.global_linear_layer_1[0], blk.global_linear_layer_2[0]
         n1, n2 = blk.global_norm_1, blk.global_norm_2
-        g1 = F.layer_norm(g + _gelu_linear(g, blk.global_linear_layer_1) + ga, n1.normalized_shape, n1.weight,
-                          n1.bias, n1.eps)
-        g = F.layer_norm(g1 + _gelu_linear(g1, blk.global_linear_layer_2), n2.normalized_shape, n2.weight,
-                         n2.bias, n2.eps)
+        g, g_bf, gb = GlobalBlockFn.apply(g, g_bf, vpart, l1.weight, l1.bias, n1.weight, n1.bias, l2.weight, l2.bias,
+                                          n2.weight, n2.bias, att.W_parameter,
+                                          None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
+    if return_bf16:
+        return h, g, g_bf
     return h, g
 
 
@@ -68,6 +69,11 @@ def fused_forward(model, tokens: torch.Tensor, annotations: torch.Tensor):
 
 def fused_pretrain_loss(model, X: Dict[str, torch.Tensor], Y: Dict[str, torch.Tensor], W: Dict[str, torch.Tensor],
                         return_parts: bool = False):
-    probs_l, probs_g = fused_forward(model, X["local"], X["global"])
-    return pretrain_loss_torch(probs_l, probs_g, Y, {k: v.float() for k, v in W.items()}, model.semantics,
-                               return_parts=return_parts)
+    """Reference loss (utils.py:293-294) through the fused heads: one HIP pass per head."""
+    h, g, g_bf = fused_encode(model, X["local"], X["global"], return_bf16=True)
+    lo, go = model.pretraining_local_output[0], model.pretraining_global_output[0]
+    total, parts = HeadsLossFn.apply(h, g, g_bf, lo.weight, lo.bias, go.weight, go.bias, Y["local"], Y["global"],
+                                     W["local"], W["global"])
+    if return_parts:
+        return total, parts[0], parts[1]
+    return total

@@ -1,0 +1,257 @@
+"""Global track, input layer and pretraining heads on MI355X (``csrc/glob.hip`` + hipBLASLt).
+
+Reference: ``ProteinBERT/modules.py:175-199,221-229`` (global MLP + LayerNorm(G)),
+``:255-262`` (GO input layer), ``:277-293`` (heads) and ``ProteinBERT/utils.py:293-294`` (loss).
+
+The ``[B, G]``/``[B, A]`` GEMMs are plain library GEMMs (bf16 operands, fp32 output through
+``torch.mm(..., out_dtype=float32)`` -> hipBLASLt); bias, GELU, residual, LayerNorm, the attention
+scale ``sum(W)/K``, the loss and every elementwise backward step are fused HIP kernels.  Backward
+passes are written by hand: each autograd node is 2-6 launches instead of ~30 eager ops, and
+parameter gradients accumulate straight into the flat-arena ``.grad`` views (weight gradients via
+``addmm(out=grad)``, bias/affine gradients via in-kernel atomics).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Tuple
+
+import torch
+
+from . import _lib
+from ..train.arena import notify_grads_ready
+
+_P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+_lib.register("pbx_row_ln_fwd", [_P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+_lib.register("pbx_row_ln_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _P])
+_lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
+_lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
+_lib.register("pbx_local_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_go_head", [_P, _P, _P, _P, ctypes.c_long, ctypes.c_long, _P, _P, _P, _I, _I, _P])
+
+LN_EPS = 1e-5
+BF16 = torch.bfloat16
+F32 = torch.float32
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else t.data_ptr()
+
+
+def _s(dev) -> int:
+    return _lib.stream_ptr(dev)
+
+
+def bf16_of(p: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of a parameter: the optimizer-maintained shadow view when the arena has one."""
+    v = getattr(p, "_pbx_bf16", None)
+    if v is not None:
+        return v
+    return p.detach().to(BF16)
+
+
+def mm32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 x bf16 -> fp32 (hipBLASLt)."""
+    return torch.mm(a, b, out_dtype=F32)
+
+
+def addmm_into(dst: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
+    """dst += a @ b with bf16 operands and fp32 accumulation/output, in place."""
+    torch.addmm(dst, a, b, out_dtype=F32, out=dst)
+
+
+class _Grads:
+    """Gradient destinations: arena ``.grad`` views (accumulated in place) or fresh zero tensors."""
+
+    def __init__(self, params):
+        self.params = params
+        self.dst: List[torch.Tensor] = []
+        self.direct: List[bool] = []
+        for p in params:
+            g = getattr(p, "grad", None) if getattr(p, "_pbx_arena", False) else None
+            if g is not None and g.is_contiguous() and g.dtype == F32:
+                self.dst.append(g)
+                self.direct.append(True)
+            else:
+                self.dst.append(None if p is None else torch.zeros(p.shape, dtype=F32, device=p.device))
+                self.direct.append(False)
+
+    def finish(self):
+        direct = [p for p, d in zip(self.params, self.direct) if d and p is not None]
+        if direct:
+            notify_grads_ready(direct)
+        return [None if (d or p is None) else g for p, g, d in zip(self.params, self.dst, self.direct)]
+
+
+class InputLayerFn(torch.autograd.Function):
+    """g0 = GELU(ann W_in^T + b_in) (reference modules.py:255-262,301); ann is the corrupted GO
+    multi-hot (values {0, 1, 2}, exact in bf16)."""
+
+    @staticmethod
+    def forward(ctx, ann, w, b):
+        dev = ann.device
+        ann_bf = ann.to(BF16)
+        u = mm32(ann_bf, bf16_of(w).t())
+        B, G = u.shape
+        g = torch.empty_like(u)
+        g_bf = torch.empty((B, G), dtype=BF16, device=dev)
+        _lib.call("pbx_bias_gelu", u.data_ptr(), b.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, G, _s(dev))
+        ctx.save_for_backward(ann_bf, u)
+        ctx.params = (w, b)
+        ctx.mark_non_differentiable(g_bf)
+        return g, g_bf
+
+    @staticmethod
+    def backward(ctx, dg, _dgbf):
+        ann_bf, u = ctx.saved_tensors
+        w, b = ctx.params
+        dev = u.device
+        B, G = u.shape
+        gr = _Grads([w, b])
+        du = torch.empty((B, G), dtype=BF16, device=dev)
+        _lib.call("pbx_bias_gelu_bwd", dg.float().contiguous().data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(),
+                  gr.dst[1].data_ptr(), B, G, _s(dev))
+        addmm_into(gr.dst[0], du.t(), ann_bf)
+        return (None, *gr.finish())
+
+
+class GlobalBlockFn(torch.autograd.Function):
+    """Global track of one block (reference modules.py:175-199,219-229, reference semantics):
+
+        g1 = LN1(g + GELU(g W1^T + b1) + (sum W_att / K) * sum_t vpart)
+        g2 = LN2(g1 + GELU(g1 W2^T + b2))
+        gb_next = GELU(g2 Wgl_next^T + bgl_next)      (the next block's global->local vector)
+    """
+
+    @staticmethod
+    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl):
+        dev = g.device
+        B, G = g.shape
+        TV = vpart.shape[1]
+        K = wp.numel()
+        st = _s(dev)
+        u1 = mm32(g_bf, bf16_of(w1).t())
+        g1 = torch.empty_like(g)
+        g1_bf = torch.empty((B, G), dtype=BF16, device=dev)
+        xh1 = torch.empty_like(g)
+        r1 = torch.empty(B, dtype=F32, device=dev)
+        vsum = torch.empty_like(g)
+        _lib.call("pbx_row_ln_fwd", u1.data_ptr(), b1.data_ptr(), g.data_ptr(), vpart.data_ptr(), TV, wp.data_ptr(),
+                  K, n1w.data_ptr(), n1b.data_ptr(), g1.data_ptr(), g1_bf.data_ptr(), xh1.data_ptr(), r1.data_ptr(),
+                  vsum.data_ptr(), B, G, LN_EPS, st)
+        u2 = mm32(g1_bf, bf16_of(w2).t())
+        g2 = torch.empty_like(g)
+        g2_bf = torch.empty((B, G), dtype=BF16, device=dev)
+        xh2 = torch.empty_like(g)
+        r2 = torch.empty(B, dtype=F32, device=dev)
+        _lib.call("pbx_row_ln_fwd", u2.data_ptr(), b2.data_ptr(), g1.data_ptr(), None, 0, None, 0, n2w.data_ptr(),
+                  n2b.data_ptr(), g2.data_ptr(), g2_bf.data_ptr(), xh2.data_ptr(), r2.data_ptr(), None, B, G, LN_EPS,
+                  st)
+        if wgl is not None:
+            ugl = mm32(g2_bf, bf16_of(wgl).t())
+            N = ugl.shape[1]
+            gb = torch.empty_like(ugl)
+            _lib.call("pbx_bias_gelu", ugl.data_ptr(), bgl.data_ptr(), gb.data_ptr(), None, B, N, st)
+        else:
+            ugl = None
+            gb = torch.zeros((B, 0), dtype=F32, device=dev)
+        ctx.save_for_backward(g_bf, u1, xh1, r1, vsum, g1_bf, u2, xh2, r2, g2_bf, ugl)
+        ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
+        ctx.TV = TV
+        ctx.mark_non_differentiable(g2_bf)
+        return g2, g2_bf, gb
+
+    @staticmethod
+    def backward(ctx, dg2, _dg2bf, dgb):
+        g_bf, u1, xh1, r1, vsum, g1_bf, u2, xh2, r2, g2_bf, ugl = ctx.saved_tensors
+        w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl = ctx.params
+        dev = u1.device
+        st = _s(dev)
+        B, G = u1.shape
+        gr = _Grads([w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl])
+        dw1, db1, dn1w, dn1b, dw2, db2, dn2w, dn2b, dwp, dwgl, dbgl = gr.dst
+        dg2 = torch.zeros((B, G), dtype=F32, device=dev) if dg2 is None else dg2.float().contiguous()
+        if wgl is not None and dgb is not None and dgb.numel() > 0:
+            N = ugl.shape[1]
+            dugl = torch.empty((B, N), dtype=BF16, device=dev)
+            _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
+            addmm_into(dwgl, dugl.t(), g2_bf)
+            dg2 = dg2.clone()   # never modify autograd's incoming buffer in place
+            addmm_into(dg2, dugl, bf16_of(wgl))
+        # LN2 + MLP2
+        du2 = torch.empty((B, G), dtype=BF16, device=dev)
+        dg1 = torch.empty((B, G), dtype=F32, device=dev)
+        _lib.call("pbx_row_ln_bwd", dg2.data_ptr(), xh2.data_ptr(), r2.data_ptr(), n2w.data_ptr(), u2.data_ptr(),
+                  b2.data_ptr(), dn2w.data_ptr(), dn2b.data_ptr(), db2.data_ptr(), du2.data_ptr(), dg1.data_ptr(),
+                  None, None, 0, None, None, B, G, st)
+        addmm_into(dw2, du2.t(), g1_bf)
+        addmm_into(dg1, du2, bf16_of(w2))
+        # LN1 + MLP1 + attention scale
+        du1 = torch.empty((B, G), dtype=BF16, device=dev)
+        dg = torch.empty((B, G), dtype=F32, device=dev)
+        dvs = torch.empty((B, G), dtype=F32, device=dev)
+        _lib.call("pbx_row_ln_bwd", dg1.data_ptr(), xh1.data_ptr(), r1.data_ptr(), n1w.data_ptr(), u1.data_ptr(),
+                  b1.data_ptr(), dn1w.data_ptr(), dn1b.data_ptr(), db1.data_ptr(), du1.data_ptr(), dg.data_ptr(),
+                  vsum.data_ptr(), wp.data_ptr(), wp.numel(), dwp.data_ptr(), dvs.data_ptr(), B, G, st)
+        addmm_into(dw1, du1.t(), g_bf)
+        addmm_into(dg, du1, bf16_of(w1))
+        dvpart = dvs.unsqueeze(1).expand(B, ctx.TV, G)
+        return (dg, None, dvpart, *gr.finish())
+
+
+class HeadsLossFn(torch.autograd.Function):
+    """Both pretraining heads + the reference loss (``utils.py:293-294``), reference semantics.
+
+    The loss is terminal, so the local-head kernel computes the input gradient in the forward pass;
+    the GO head runs its GEMM, then one fused sigmoid/BCE/dlogits pass.
+    """
+
+    @staticmethod
+    def forward(ctx, h, g2, g2_bf, wo, bo, wa, ba, y_l, y_g, w_l, w_g):
+        dev = h.device
+        st = _s(dev)
+        B, L, C = h.shape
+        V = wo.shape[0]
+        A = wa.shape[0]
+        loss = torch.zeros(2, dtype=F32, device=dev)
+        dh = torch.empty_like(h)
+        dzo = torch.empty((B * L, 32), dtype=BF16, device=dev)
+        dbo = torch.zeros(V, dtype=F32, device=dev)
+        _lib.call("pbx_local_head", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
+                  y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dzo.data_ptr(),
+                  dbo.data_ptr(), loss.data_ptr(), B, L, V, st)
+        z = mm32(g2_bf, bf16_of(wa).t())
+        dz = torch.empty((B, A), dtype=BF16, device=dev)
+        dba = torch.zeros(A, dtype=F32, device=dev)
+        # per-row weights (the reference's any(annotation) broadcast) are read without expanding them
+        if w_g.dim() == 2 and w_g.stride(1) == 0:
+            wg, wsr, wsc = w_g[:, 0].float().contiguous(), 1, 0
+        else:
+            wg = w_g.float().expand(B, A).contiguous()
+            wsr, wsc = A, 1
+        _lib.call("pbx_go_head", z.data_ptr(), ba.data_ptr(), y_g.float().contiguous().data_ptr(), wg.data_ptr(),
+                  wsr, wsc, dz.data_ptr(), dba.data_ptr(), loss[1:].data_ptr(), B, A, st)
+        ctx.save_for_backward(h, dh, dzo, dbo, dz, dba, g2_bf)
+        ctx.params = (wo, bo, wa, ba)
+        ctx.V = V
+        total = loss.sum()
+        ctx.mark_non_differentiable(loss)
+        return total, loss
+
+    @staticmethod
+    def backward(ctx, dtotal, _dparts):
+        h, dh, dzo, dbo, dz, dba, g2_bf = ctx.saved_tensors
+        wo, bo, wa, ba = ctx.params
+        B, L, C = h.shape
+        V = ctx.V
+        gr = _Grads([wo, bo, wa, ba])
+        dwo, dbo_dst, dwa, dba_dst = gr.dst
+        s = dtotal.reshape(()).to(F32)          # 1.0 for loss.backward(); kept on device (no sync)
+        dz_s = dz * s
+        dzo_s = dzo * s
+        dg2 = mm32(dz_s, bf16_of(wa))
+        addmm_into(dwa, dz_s.t(), g2_bf)
+        addmm_into(dwo, dzo_s[:, :V].t(), h.reshape(B * L, C))
+        dbo_dst.add_(dbo * s)
+        dba_dst.add_(dba * s)
+        return (dh * s, dg2, None, *gr.finish(), None, None, None, None)

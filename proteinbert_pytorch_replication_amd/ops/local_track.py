@@ -153,6 +153,10 @@ class LocalBlockFn(torch.autograd.Function):
         TV = (L + BMV - 1) // BMV
         if dvpart is None:
             dvpart = torch.zeros((B, TV, NJ), dtype=torch.float32, device=dev)
+        if dvpart.dim() == 3 and dvpart.stride(1) == 0:
+            # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
+            dvpart = dvpart[:, 0, :].float().contiguous()
+            BMV = L
         dvpart = dvpart.float().contiguous()
         # attention pool + LN2 partials
         nwb = attn_bwd_waves(L)
