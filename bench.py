@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--impl", default="hip", choices=["hip", "torch", "faithful"],
                     help="hip: fused CDNA4 kernels; torch: eager bf16 oracle; faithful: reference math, eager fp32")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="capture the whole step in a hipGraph (auto: single GPU, or PBX_GRAPH_DP=1)")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
@@ -91,6 +93,17 @@ def main():
         X, Y, W = gen.next_batch()
         return step(X, Y, W)
 
+    use_graph = a.graph == "on" or (a.graph == "auto" and dev.type == "cuda" and a.impl == "hip" and
+                                     (info.world_size == 1 or os.environ.get("PBX_GRAPH_DP") == "1"))
+    graphed = False
+    if use_graph:
+        from proteinbert_pytorch_replication_amd.train.step import GraphedStep
+        try:
+            one = GraphedStep(step, gen.next_batch, warmup=2)
+            graphed = True
+        except Exception as e:  # capture unsupported here: run eagerly
+            print(f"warning: hipGraph capture failed ({type(e).__name__}: {e}); running eagerly", file=sys.stderr)
+
     for _ in range(a.warmup):
         loss = one()
     if dev.type == "cuda":
@@ -122,7 +135,7 @@ def main():
                                    f"d_global={mcfg.global_dim}, key_dim={mcfg.key_dim}, heads={mcfg.num_heads}, "
                                    f"annotations={mcfg.num_annotations}, semantics=reference",
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
-                          "impl": a.impl},
+                          "impl": a.impl, "hip_graph": graphed},
                "final_loss": round(final_loss, 5)}
         print(json.dumps(out), flush=True)
     pdist.destroy()

@@ -94,14 +94,16 @@ class SyntheticUniRefGO:
         if use_kernel is None:
             use_kernel = self.device.type == "cuda"
         self.use_kernel = use_kernel
+        # device-side step counter: generation launches read it, so a hipGraph-captured step draws a
+        # fresh batch on every replay (the counter is advanced by a captured add)
+        self.step_dev = torch.zeros(1, dtype=torch.int64, device=self.device) if use_kernel else None
 
     def clean_batch(self) -> Tuple[torch.Tensor, torch.Tensor]:
         B, L, dev, g = self.B, self.L, self.device, self.generator
         if self.use_kernel:
             from ..ops.corrupt import synth_batch
-            self.gen_step += 1
             return synth_batch(B, L, self.A, self.min_length, self.max_length, self.density, self.seed,
-                               self.gen_step, dev)
+                               1, dev, step_dev=self.step_dev)
         n = torch.randint(self.min_length, self.max_length + 1, (B, 1), device=dev, generator=g)
         total = n + 2  # <sos> + aa + <eos>
         span = (total - L).clamp(min=1)
@@ -119,8 +121,10 @@ class SyntheticUniRefGO:
     def corrupt(self, tokens: torch.Tensor, ann: torch.Tensor) -> Batch:
         if self.use_kernel:
             from ..ops import corrupt as corrupt_op
-            self.step += 1
-            return corrupt_op.corrupt_batch(tokens, ann, self.corruption, seed=self.seed, step=self.step)
+            out = corrupt_op.corrupt_batch(tokens, ann, self.corruption, seed=self.seed, step=1,
+                                           step_dev=self.step_dev)
+            self.step_dev.add_(1)
+            return out
         return corrupt_batch_torch(tokens, ann, self.corruption, self.generator)
 
     def __iter__(self):

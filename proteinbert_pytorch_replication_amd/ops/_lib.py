@@ -22,7 +22,7 @@ _F32 = ctypes.c_float
 
 # name -> argtypes (all return int hipError_t)
 _SIGS = {
-    "pbx_adam_flat": [_P, _P, _P, _P, _P, _I64, _P, _P, _P],
+    "pbx_adam_flat": [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P],
     "pbx_sumsq_flat": [_P, _I64, _P, _P, _P],
     "pbx_clip_scale_flat": [_P, _I64, _P, _F32, _P],
 }

@@ -16,8 +16,8 @@ from . import _lib
 from ..data.vocab import VOCAB_SIZE
 
 _P, _I, _F, _U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_uint64
-_lib.register("pbx_synth_batch", [_P, _P, _I, _I, _I, _I, _I, _F, _I, _U64, _U64, _P])
-_lib.register("pbx_corrupt_batch", [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _F, _F, _U64, _U64, _P])
+_lib.register("pbx_synth_batch", [_P, _P, _I, _I, _I, _I, _I, _F, _I, _U64, _U64, _P, _P])
+_lib.register("pbx_corrupt_batch", [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _F, _F, _F, _U64, _U64, _P, _P])
 
 
 def _check(t: torch.Tensor, dtype, name: str):
@@ -26,17 +26,18 @@ def _check(t: torch.Tensor, dtype, name: str):
 
 
 def synth_batch(B: int, L: int, A: int, min_len: int, max_len: int, density: float, seed: int, step: int,
-                device) -> Tuple[torch.Tensor, torch.Tensor]:
+                device, step_dev: torch.Tensor = None) -> Tuple[torch.Tensor, torch.Tensor]:
     tokens = torch.empty((B, L), dtype=torch.long, device=device)
     ann = torch.empty((B, A), dtype=torch.float32, device=device)
     if max_len < min_len:
         raise ValueError("max_len < min_len")
     _lib.call("pbx_synth_batch", tokens.data_ptr(), ann.data_ptr(), B, L, A, min_len, max_len, float(density),
-              VOCAB_SIZE, seed & (2**64 - 1), step, _lib.stream_ptr(tokens.device))
+              VOCAB_SIZE, seed & (2**64 - 1), step, _lib.ptr(step_dev), _lib.stream_ptr(tokens.device))
     return tokens, ann
 
 
-def corrupt_batch(tokens: torch.Tensor, ann: torch.Tensor, params, seed: int, step: int):
+def corrupt_batch(tokens: torch.Tensor, ann: torch.Tensor, params, seed: int, step: int,
+                  step_dev: torch.Tensor = None):
     _check(tokens, torch.long, "tokens")
     _check(ann, torch.float32, "ann")
     B, L = tokens.shape
@@ -50,7 +51,7 @@ def corrupt_batch(tokens: torch.Tensor, ann: torch.Tensor, params, seed: int, st
     _lib.call("pbx_corrupt_batch", tokens.data_ptr(), ann.data_ptr(), x_local.data_ptr(), x_global.data_ptr(),
               w_local.data_ptr(), w_sample.data_ptr(), B, L, A, VOCAB_SIZE, float(params.token_p),
               float(params.positive_p), float(params.negative_p), float(params.blank_p),
-              seed & (2**64 - 1), step, _lib.stream_ptr(tokens.device))
+              seed & (2**64 - 1), step, _lib.ptr(step_dev), _lib.stream_ptr(tokens.device))
     return ({"local": x_local, "global": x_global},
             {"local": tokens, "global": ann},
             {"local": w_local, "global": w_sample.unsqueeze(1).expand(B, A)})

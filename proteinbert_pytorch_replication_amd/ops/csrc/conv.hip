@@ -392,13 +392,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
   }
 }
 
-// sum the R slabs (fixed order: deterministic); write torch layouts: weight [co][ci][KS] (KS == 1:
-// [co][ci]), bias [co].  accumulate != 0 adds into the destination (the flat-arena .grad views).
+// sum the R slabs (fixed order: deterministic) and ADD the result into the torch layouts:
+// weight [co][ci][KS] (KS == 1: [co][ci]), bias [co] -- the destinations are the flat-arena .grad
+// views (or zero-initialised tensors); one thread owns each destination element (no atomics).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float4* __restrict__ slab,
                                                            const float* __restrict__ bslab, float* __restrict__ dw0,
                                                            float* __restrict__ dw1, float* __restrict__ db0,
-                                                           float* __restrict__ db1, int R, int nconv, int KS,
-                                                           int accumulate) {
+                                                           float* __restrict__ db1, int R, int nconv, int KS) {
   const int per = KS * CH * CH;
   const int total4 = nconv * per / 4;
   const int idx = blockIdx.x * 256 + threadIdx.x;
@@ -421,16 +421,13 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float4* __restr
     float* dw = cv ? dw1 : dw0;
     const float sv[4] = {s.x, s.y, s.z, s.w};
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const size_t a = ((size_t)co * CH + ci + j) * KS + k;
-      dw[a] = (accumulate ? dw[a] : 0.f) + sv[j];
-    }
+    for (int j = 0; j < 4; ++j) dw[((size_t)co * CH + ci + j) * KS + k] += sv[j];
   }
   if (idx < nconv * CH) {
     float s = 0.f;
     for (int rr = 0; rr < R; ++rr) s += bslab[(size_t)rr * nconv * CH + idx];
     float* db = idx >= CH ? db1 : db0;
-    if (db != nullptr) db[idx % CH] = (accumulate ? db[idx % CH] : 0.f) + s;
+    if (db != nullptr) db[idx % CH] += s;
   }
 }
 
@@ -518,9 +515,10 @@ PBX_EXPORT int pbx_wgrad(const void* dy0, const void* dy1, const void* x, float*
                        (const bf16_t*)x, slab, bslab, B, L, dil1, nconv);
   else
     return (int)hipErrorInvalidValue;
+  (void)accumulate;   // destinations are always accumulated into (zero-initialised when not arena views)
   const int total4 = nconv * KS * CH * CH / 4;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, (const float4*)slab, bslab,
-                     dw0, dw1, db0, db1, R, nconv, KS, accumulate);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, (const float4*)slab,
+                     bslab, dw0, dw1, db0, db1, R, nconv, KS);
   return pbx_launch_status();
 }
 

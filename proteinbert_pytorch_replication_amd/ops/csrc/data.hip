@@ -25,7 +25,9 @@ __device__ __forceinline__ unsigned long long stream_id(unsigned long long step,
 __global__ void __launch_bounds__(256) synth_batch_kernel(long long* __restrict__ tokens, float* __restrict__ ann,
                                                           int L, int A, int min_len, int max_len, float density,
                                                           int vocab, unsigned long long seed,
-                                                          unsigned long long step) {
+                                                          unsigned long long step,
+                                                          const long long* __restrict__ step_dev) {
+  if (step_dev != nullptr) step += (unsigned long long)*step_dev;
   const int b = blockIdx.x;
   const float u_len = pbx_uniform(seed, stream_id(step, S_LEN), b);
   const int n = min_len + min((int)(u_len * (float)(max_len - min_len + 1)), max_len - min_len);
@@ -63,7 +65,9 @@ __global__ void __launch_bounds__(256) corrupt_batch_kernel(const long long* __r
                                                             float* __restrict__ w_sample,
                                                             int L, int A, int vocab, float token_p,
                                                             float positive_p, float negative_p, float blank_p,
-                                                            unsigned long long seed, unsigned long long step) {
+                                                            unsigned long long seed, unsigned long long step,
+                                                            const long long* __restrict__ step_dev) {
+  if (step_dev != nullptr) step += (unsigned long long)*step_dev;
   __shared__ int any_s[4];
   const int b = blockIdx.x;
   for (int j = threadIdx.x; j < L; j += blockDim.x) {
@@ -101,22 +105,24 @@ __global__ void __launch_bounds__(256) corrupt_batch_kernel(const long long* __r
   if (threadIdx.x == 0) w_sample[b] = (any_s[0] | any_s[1] | any_s[2] | any_s[3]) ? 1.0f : 0.0f;
 }
 
+// step_dev (optional, device int64): added to `step`, so a captured launch draws new data per replay
 PBX_EXPORT int pbx_synth_batch(void* tokens, void* ann, int B, int L, int A, int min_len, int max_len,
                                float density, int vocab, unsigned long long seed, unsigned long long step,
-                               hipStream_t stream) {
+                               const void* step_dev, hipStream_t stream) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(synth_batch_kernel, dim3(B), dim3(256), 0, stream, (long long*)tokens, (float*)ann, L, A,
-                     min_len, max_len, density, vocab, seed, step);
+                     min_len, max_len, density, vocab, seed, step, (const long long*)step_dev);
   return pbx_launch_status();
 }
 
 PBX_EXPORT int pbx_corrupt_batch(const void* tokens, const void* ann, void* x_local, void* x_global,
                                  void* w_local, void* w_sample, int B, int L, int A, int vocab, float token_p,
                                  float positive_p, float negative_p, float blank_p, unsigned long long seed,
-                                 unsigned long long step, hipStream_t stream) {
+                                 unsigned long long step, const void* step_dev, hipStream_t stream) {
   if (B <= 0) return 0;
   hipLaunchKernelGGL(corrupt_batch_kernel, dim3(B), dim3(256), 0, stream, (const long long*)tokens,
                      (const float*)ann, (long long*)x_local, (float*)x_global, (float*)w_local,
-                     (float*)w_sample, L, A, vocab, token_p, positive_p, negative_p, blank_p, seed, step);
+                     (float*)w_sample, L, A, vocab, token_p, positive_p, negative_p, blank_p, seed, step,
+                     (const long long*)step_dev);
   return pbx_launch_status();
 }

@@ -187,8 +187,8 @@ __global__ void __launch_bounds__(256) bias_gelu_bwd_kernel(const float* __restr
 // grid (L), block 256: one position l per workgroup, all B samples (B <= 1024).
 __global__ void __launch_bounds__(256) local_head_kernel(
     const bf16_t* __restrict__ h, const float* __restrict__ wo, const float* __restrict__ bo,
-    const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, bf16_t* __restrict__ dzo,
-    float* __restrict__ dbo, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
+    const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, float* __restrict__ dwo_part,
+    float* __restrict__ dbo_part, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* W = sm;                       // [V][128]
   float* zs = W + V * 128;             // [B][V]  logits -> probabilities -> dz
@@ -198,12 +198,12 @@ __global__ void __launch_bounds__(256) local_head_kernel(
   const int lane = tid & 63;
   for (int i = tid; i < V * 128; i += 256) W[i] = wo[i];
   __syncthreads();
-  // logits: thread per (sample, v) pair
-  for (int i = tid; i < B * V; i += 256) {
-    const int b = i / V, v = i - (i / V) * V;
+  // logits: thread per sample row (the h row is read once; Wo reads are LDS broadcasts)
+  for (int b = tid; b < B; b += 256) {
     const bf16_t* hr = h + ((size_t)b * L + l) * 128;
-    float acc = bo[v];
-#pragma unroll 4
+    float acc[32];
+#pragma unroll
+    for (int v = 0; v < 32; ++v) acc[v] = 0.f;
     for (int c8 = 0; c8 < 16; ++c8) {
       const uint4 q = *reinterpret_cast<const uint4*>(hr + c8 * 8);
       const float hv[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
@@ -211,21 +211,47 @@ __global__ void __launch_bounds__(256) local_head_kernel(
                            __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
                            __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc = fmaf(hv[e], W[v * 128 + c8 * 8 + e], acc);
+      for (int v = 0; v < 32; ++v) {
+        if (v < V) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[v] = fmaf(hv[e], W[v * 128 + c8 * 8 + e], acc[v]);
+        }
+      }
     }
-    zs[i] = acc;
+#pragma unroll
+    for (int v = 0; v < 32; ++v)
+      if (v < V) zs[b * V + v] = acc[v] + bo[v];
   }
   __syncthreads();
-  // softmax over b for each v: column max and sum (threads v, strided over b by 256/V groups)
-  if (tid < V) {
+  // softmax over b for each v: 8 partial columns per v (8 threads), then combine
+  {
+    float* pm = colv + V;                // [8][V] partial max, then partial sum (reuses tail space)
+    const int v = tid % 32, part = tid / 32;
     float m = -3.4e38f;
-    for (int b = 0; b < B; ++b) m = fmaxf(m, zs[b * V + tid]);
-    float s = 0.f;
-    for (int b = 0; b < B; ++b) s += __expf(zs[b * V + tid] - m);
-    red[tid] = m;
-    red[V + tid] = 1.0f / s;
+    if (v < V)
+      for (int b = part; b < B; b += 8) m = fmaxf(m, zs[b * V + v]);
+    if (v < V) red[part * V + v] = m;
+    __syncthreads();
+    if (tid < V) {
+      float mm = -3.4e38f;
+      for (int k = 0; k < 8; ++k) mm = fmaxf(mm, red[k * V + tid]);
+      pm[tid] = mm;
+    }
+    __syncthreads();
+    float sacc = 0.f;
+    if (v < V)
+      for (int b = part; b < B; b += 8) sacc += __expf(zs[b * V + v] - pm[v]);
+    if (v < V) red[part * V + v] = sacc;
+    __syncthreads();
+    if (tid < V) {
+      float ss = 0.f;
+      for (int k = 0; k < 8; ++k) ss += red[k * V + tid];
+      pm[V + tid] = 1.0f / ss;
+    }
+    __syncthreads();
+    if (tid < V) { red[tid] = pm[tid]; red[V + tid] = pm[V + tid]; }
+    __syncthreads();
   }
-  __syncthreads();
   for (int i = tid; i < B * V; i += 256) {
     const int v = i - (i / V) * V;
     zs[i] = __expf(zs[i] - red[v]) * red[V + v];
@@ -284,15 +310,38 @@ __global__ void __launch_bounds__(256) local_head_kernel(
     q.w = (unsigned)f2bf(o[6]) | ((unsigned)f2bf(o[7]) << 16);
     *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) = q;
   }
-  // dz rows (padded to 32 logits) for the dWo = dz^T h GEMM
-  for (int i = tid; i < B * 32; i += 256) {
-    const int b = i >> 5, v = i & 31;
-    dzo[((size_t)b * L + l) * 32 + v] = v < V ? f2bf(zs[b * V + v]) : (bf16_t)0;
+  // per-position partials of dWo = sum_b dz[b,:]^T h[b,l,:] and dbo (summed over l by the caller):
+  // thread (v pair vp = tid>>4, channel chunk c8 = tid&15) walks the batch
+  {
+    const int vp = tid >> 4, c8 = tid & 15;
+    const int v0 = 2 * vp, v1 = 2 * vp + 1;
+    float a0[8] = {0, 0, 0, 0, 0, 0, 0, 0}, a1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (v0 < V) {
+      for (int b = 0; b < B; ++b) {
+        const uint4 q = *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + c8 * 8);
+        const float hv[8] = {__uint_as_float(q.x << 16), __uint_as_float(q.x & 0xffff0000u),
+                             __uint_as_float(q.y << 16), __uint_as_float(q.y & 0xffff0000u),
+                             __uint_as_float(q.z << 16), __uint_as_float(q.z & 0xffff0000u),
+                             __uint_as_float(q.w << 16), __uint_as_float(q.w & 0xffff0000u)};
+        const float d0 = zs[b * V + v0], d1 = v1 < V ? zs[b * V + v1] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          a0[e] = fmaf(d0, hv[e], a0[e]);
+          a1[e] = fmaf(d1, hv[e], a1[e]);
+        }
+      }
+      float* dst = dwo_part + (size_t)l * V * 128;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dst[v0 * 128 + c8 * 8 + e] = a0[e];
+        if (v1 < V) dst[v1 * 128 + c8 * 8 + e] = a1[e];
+      }
+    }
   }
   if (tid < V) {
     float a = 0.f;
     for (int b = 0; b < B; ++b) a += zs[b * V + tid];
-    atomicAdd(dbo + tid, a);
+    dbo_part[(size_t)l * V + tid] = a;
   }
   lsum = wave_reduce_sum(lsum);
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
@@ -367,10 +416,11 @@ PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float*
   return pbx_launch_status();
 }
 
-// dzo: [B*L][32] bf16 (dz of the V logits, zero padded) for the dWo GEMM
+// dwo_part: [L][V][128], dbo_part: [L][V] per-position partial gradients (sum over L by the caller)
 PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
-                              void* dh, void* dzo, float* dbo, float* loss, int B, int L, int V, hipStream_t st) {
-  const int lds = (V * 128 + B * V + 9 * V) * 4;
+                              void* dh, float* dwo_part, float* dbo_part, float* loss, int B, int L, int V,
+                              hipStream_t st) {
+  const int lds = (V * 128 + B * V + 12 * V) * 4;
   if (V > 32 || lds > 163840) return (int)hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
@@ -378,13 +428,13 @@ PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, c
     attr = true;
   }
   hipLaunchKernelGGL(local_head_kernel, dim3(L), dim3(256), lds, st, (const bf16_t*)h, wo, bo, (const long long*)y,
-                     wl, (bf16_t*)dh, (bf16_t*)dzo, dbo, loss, B, L, V, 1.0f / ((float)B * (float)L));
+                     wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V, 1.0f / ((float)B * (float)L));
   return pbx_launch_status();
 }
 
 PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, const float* w, long wsr, long wsc,
                            void* dz, float* dbias, float* loss, int B, int A, hipStream_t st) {
-  const int gy = B < 16 ? B : 16;
+  const int gy = B < 64 ? B : 64;
   hipLaunchKernelGGL(go_head_kernel, dim3((A + 255) / 256, gy), dim3(256), 0, st, z, bias, y, w, wsr, wsc,
                      (bf16_t*)dz, dbias, loss, B, A, 1.0f / ((float)B * (float)A));
   return pbx_launch_status();

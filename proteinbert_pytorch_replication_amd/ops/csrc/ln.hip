@@ -337,24 +337,25 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// LayerNorm-2 backward + local MLP backward + LayerNorm-1 backward partials + both [L, C] affine
-// gradients, position-major (grid (ceil(L/PB), nbg), 512 threads):
+// LayerNorm-2 backward + local MLP backward (input AND weight gradient) + LayerNorm-1 backward
+// partials + both [L, C] affine gradients, position-major (grid (ceil(L/PB), nbg), 512 threads):
 //   ds2 = rstd2 (dh2 g2 - m1 - xhat2 m2) ; dpre = ds2 GELU'(pre) ; dh1 = ds2 + Wl^T dpre
-//   dg2 += dh2 xhat2 ; db2 += dh2 ; dg1 += dh1 xhat1 ; db1 += dh1   (registers, one atomic pass at the end)
-// writes dh1, dpre and the recomputed h1 (inputs of the Linear weight gradient) and the per-sample
-// LN1 partials (sum dxhat1, sum dxhat1*xhat1) per 32 positions.
+//   dWl += dpre^T h1 ; dbl += sum dpre                        (MFMA, registers across samples)
+//   dg2 += dh2 xhat2 ; db2 += dh2 ; dg1 += dh1 xhat1 ; db1 += dh1   (registers across samples)
+// and the per-sample LN1 partials (sum dxhat1, sum dxhat1*xhat1) per 32 positions.  All parameter
+// gradients are added into their destinations (flat-arena .grad views) once per workgroup.
 __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ sums2, int TS2, const float* __restrict__ g2, const bf16_t* __restrict__ pre_l,
     const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
     const float* __restrict__ be1, const bf16_t* __restrict__ wl, bf16_t* __restrict__ dh1,
-    bf16_t* __restrict__ dpre_out, bf16_t* __restrict__ h1_out, float* __restrict__ sums1,
-    float* __restrict__ dg2, float* __restrict__ db2, float* __restrict__ dg1, float* __restrict__ db1, int B, int L,
-    float eps) {
+    float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2, float* __restrict__ dg1,
+    float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B, int L, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16
-  float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // [PB][128] fp32
+  unsigned char* ht = dt + PB * 256;                                 // h1 tile bf16
+  float* yt = reinterpret_cast<float*>(ht + PB * 256);               // [PB][128] fp32
   float* sh = yt + PB * CH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -376,6 +377,10 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   }
   float adg2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float adg1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float adbl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // dWl accumulators: wave w owns co tile (w >> 1) and ci tiles 2 (w & 1) + {0, 1}
+  f32x16_t aw0 = zero16(), aw1 = zero16();
+  const int wco = (w >> 1) * 32, wci = (w & 1) * 64;
   const size_t coff = (size_t)l * CH + ch * 8;
   uint4 n_dh = ldq(dh2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
   uint4 n_s2 = ldq(s2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
@@ -405,15 +410,18 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       ds2[e] = okl ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
       dp[e] = ds2[e] * gelu_grad_f(pr[e]);
       xh1[e] = (sv1[e] - mean1) * rstd1;
-      hv[e] = xh1[e] * ga1[e] + bt1[e];
+      hv[e] = okl ? xh1[e] * ga1[e] + bt1[e] : 0.f;
     }
     const uint4 dq = packq8(dp);
     *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
-    const size_t off = (size_t)b * L * CH + coff;
-    if (okl) {
-      *reinterpret_cast<uint4*>(dpre_out + off) = dq;
-      *reinterpret_cast<uint4*>(h1_out + off) = packq8(hv);
+    *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(hv);
+    {
+      float dpr[8];
+      unpack8(dq, dpr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) adbl[e] += dpr[e];
     }
+    const size_t off = (size_t)b * L * CH + coff;
     __syncthreads();
     const size_t noff = (size_t)(b + 1) * L * CH + coff;
     const bool nok = okl && b + 1 < b1;
@@ -435,6 +443,17 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<float4*>(yt + r * CH + w * 32 + 8 * g + 4 * h) =
             make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+    }
+    // dWl[co][ci] += sum_pos dpre[pos][co] h1[pos][ci]   (both operands transposed LDS reads)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int rlo = ks * 16 + 8 * h + q;
+      const bf16x8 fa = cat_tr(lds_tr(dt, swz256e(rlo, wco + tc)), lds_tr(dt, swz256e(rlo + 4, wco + tc)));
+      const bf16x8 fb0 = cat_tr(lds_tr(ht, swz256e(rlo, wci + tc)), lds_tr(ht, swz256e(rlo + 4, wci + tc)));
+      const bf16x8 fb1 =
+          cat_tr(lds_tr(ht, swz256e(rlo, wci + 32 + tc)), lds_tr(ht, swz256e(rlo + 4, wci + 32 + tc)));
+      aw0 = mfma32(fa, fb0, aw0);
+      aw1 = mfma32(fa, fb1, aw1);
     }
     __syncthreads();
     const float4 ya = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8);
@@ -458,7 +477,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       sums1[((size_t)b * TP + blockIdx.x) * 2 + 1] = sc;
     }
   }
-  // affine gradients: transpose through LDS so each wave-instruction adds 256 contiguous bytes
+  // [L, C] affine gradients: transpose through LDS so each wave-instruction adds 256 contiguous bytes
   float* accs[4] = {adg2, adb2, adg1, adb1};
   float* dsts[4] = {dg2, db2, dg1, db1};
 #pragma unroll
@@ -470,6 +489,24 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     for (int i = tid; i < PB * CH; i += 512) {
       if (l0 + (i >> 7) < L) atomicAdd(dsts[a] + (size_t)l0 * CH + i, yt[i]);
     }
+  }
+  // local-MLP bias: column sums over the workgroup's positions
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = adbl[e];
+  __syncthreads();
+  if (tid < CH) {
+    float a = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < PB; ++k) a += yt[k * CH + tid];
+    atomicAdd(dbl + tid, a);
+  }
+  // local-MLP weight: D[co][ci], lane -> ci (128 contiguous bytes per half-wave)
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int co = wco + (i & 3) + 8 * (i >> 2) + 4 * h;
+    atomicAdd(dwl + (size_t)co * CH + wci + r, aw0[i]);
+    atomicAdd(dwl + (size_t)co * CH + wci + 32 + r, aw1[i]);
   }
 }
 
@@ -622,18 +659,17 @@ PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, co
   return pbx_launch_status();
 }
 
-// dg2/db2/dg1/db1 ([L, C] fp32) are accumulated into (atomics)
+// dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics)
 PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
                                   int BM1, const float* g1, const float* be1, const void* wl, void* dh1,
-                                  void* dpre, void* h1, float* sums1, float* dg2, float* db2, float* dg1,
-                                  float* db1, int B, int L, float eps, hipStream_t st) {
+                                  float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
+                                  float* dbl, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int lds = 32768 + PB * 256 + PB * CH * 4 + 128;
+  const int lds = 32768 + 2 * PB * 256 + PB * CH * 4 + 128;
   hipLaunchKernelGGL(ln2_linear_bwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh2, (const bf16_t*)s2, st2,
                      sums2, TS2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
-                     (const bf16_t*)wl, (bf16_t*)dh1, (bf16_t*)dpre, (bf16_t*)h1, sums1, dg2, db2, dg1, db1, B, L,
-                     eps);
+                     (const bf16_t*)wl, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L, eps);
   return pbx_launch_status();
 }
 
@@ -657,7 +693,7 @@ PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long ro
 PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long rows, int V, hipStream_t st) {
   if (V > 32) return (int)hipErrorInvalidValue;
   long g = (rows + 15) / 16;
-  if (g > 1024) g = 1024;
+  if (g > 128) g = 128;    // few adders per address: the 26 x 128 table is tiny and hot
   hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
                      (const bf16_t*)dout, dE, rows, V);
   return pbx_launch_status();

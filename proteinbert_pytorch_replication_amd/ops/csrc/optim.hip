@@ -22,13 +22,21 @@ __device__ __forceinline__ void adam_one(float& p, float g, float& m, float& v, 
 }
 
 // Optional bf16 shadow (nullptr to skip): written from the updated fp32 master.
+// step_dev (optional): device step counter t (already incremented for this step); the bias
+// corrections are then computed on the device, so the launch is replayable from a hipGraph.
 __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                         float* __restrict__ m, float* __restrict__ v,
                                                         unsigned short* __restrict__ shadow, int64_t n,
                                                         const AdamHParams* __restrict__ hp,
-                                                        const int* __restrict__ skip) {
+                                                        const int* __restrict__ skip,
+                                                        const float* __restrict__ step_dev) {
   if (skip != nullptr && *skip != 0) return;
-  const AdamHParams h = *hp;
+  AdamHParams h = *hp;
+  if (step_dev != nullptr) {
+    const float t = *step_dev;
+    h.bias_correction1 = 1.0f - powf(h.beta1, t);
+    h.bias_correction2_sqrt = sqrtf(1.0f - powf(h.beta2, t));
+  }
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -59,14 +67,14 @@ __global__ void __launch_bounds__(256) adam_flat_kernel(float* __restrict__ p, c
   }
 }
 
-PBX_EXPORT int pbx_adam_flat(float* p, const float* g, float* m, float* v, void* shadow_bf16, int64_t n,
-                             const void* hparams, const int* skip, hipStream_t stream) {
+PBX_EXPORT int pbx_adam_flat(float* p, const float* g, float* m, float* v, void* shadow, int64_t n,
+                             const void* hparams, const int* skip, const float* step_dev, hipStream_t stream) {
   if (n <= 0) return 0;
   int64_t blocks = ((n >> 2) + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(adam_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, p, g, m, v,
-                     (unsigned short*)shadow_bf16, n, (const AdamHParams*)hparams, skip);
+                     (unsigned short*)shadow, n, (const AdamHParams*)hparams, skip, step_dev);
   return pbx_launch_status();
 }
 

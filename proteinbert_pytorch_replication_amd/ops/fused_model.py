@@ -43,11 +43,10 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     _check(model)
     blocks = list(model.proteinBERT_blocks)
     lin = model.global_linear_layer[0]
-    g, g_bf = InputLayerFn.apply(annotations, lin.weight, lin.bias)
-    h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
-    # gb for block 0; every GlobalBlockFn produces the next block's gb
     gl0 = blocks[0].global_to_local_linear_layer[0]
-    gb = F.gelu(F.linear(g, gl0.weight, gl0.bias))
+    # g0 and block 0's global->local vector; every GlobalBlockFn then produces the next block's gb
+    g, g_bf, gb = InputLayerFn.apply(annotations, lin.weight, lin.bias, gl0.weight, gl0.bias)
+    h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
     for i, blk in enumerate(blocks):
         h, vpart = local_block(h, gb, blk)
         att = blk.global_attention_layer

@@ -87,30 +87,45 @@ class InputLayerFn(torch.autograd.Function):
     multi-hot (values {0, 1, 2}, exact in bf16)."""
 
     @staticmethod
-    def forward(ctx, ann, w, b):
+    def forward(ctx, ann, w, b, wgl, bgl):
         dev = ann.device
+        st = _s(dev)
         ann_bf = ann.to(BF16)
         u = mm32(ann_bf, bf16_of(w).t())
         B, G = u.shape
         g = torch.empty_like(u)
         g_bf = torch.empty((B, G), dtype=BF16, device=dev)
-        _lib.call("pbx_bias_gelu", u.data_ptr(), b.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, G, _s(dev))
-        ctx.save_for_backward(ann_bf, u)
-        ctx.params = (w, b)
+        _lib.call("pbx_bias_gelu", u.data_ptr(), b.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, G, st)
+        # block 0's global->local vector gb = GELU(g Wgl^T + bgl)
+        ugl = mm32(g_bf, bf16_of(wgl).t())
+        gb = torch.empty_like(ugl)
+        _lib.call("pbx_bias_gelu", ugl.data_ptr(), bgl.data_ptr(), gb.data_ptr(), None, B, ugl.shape[1], st)
+        ctx.save_for_backward(ann_bf, u, g_bf, ugl)
+        ctx.params = (w, b, wgl, bgl)
         ctx.mark_non_differentiable(g_bf)
-        return g, g_bf
+        return g, g_bf, gb
 
     @staticmethod
-    def backward(ctx, dg, _dgbf):
-        ann_bf, u = ctx.saved_tensors
-        w, b = ctx.params
+    def backward(ctx, dg, _dgbf, dgb):
+        ann_bf, u, g_bf, ugl = ctx.saved_tensors
+        w, b, wgl, bgl = ctx.params
         dev = u.device
+        st = _s(dev)
         B, G = u.shape
-        gr = _Grads([w, b])
+        gr = _Grads([w, b, wgl, bgl])
+        dw, db, dwgl, dbgl = gr.dst
+        dg = torch.zeros((B, G), dtype=F32, device=dev) if dg is None else dg.float().contiguous().clone()
+        if dgb is not None:
+            N = ugl.shape[1]
+            dugl = torch.empty((B, N), dtype=BF16, device=dev)
+            _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
+            addmm_into(dwgl, dugl.t(), g_bf)
+            addmm_into(dg, dugl, bf16_of(wgl))
         du = torch.empty((B, G), dtype=BF16, device=dev)
-        _lib.call("pbx_bias_gelu_bwd", dg.float().contiguous().data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(),
-                  gr.dst[1].data_ptr(), B, G, _s(dev))
-        addmm_into(gr.dst[0], du.t(), ann_bf)
+        _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
+                  st)
+        addmm_into(dw, du.t(), ann_bf)
         return (None, *gr.finish())
 
 
@@ -215,11 +230,11 @@ class HeadsLossFn(torch.autograd.Function):
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
         dh = torch.empty_like(h)
-        dzo = torch.empty((B * L, 32), dtype=BF16, device=dev)
-        dbo = torch.zeros(V, dtype=F32, device=dev)
+        dwo_part = torch.empty((L, V, C), dtype=F32, device=dev)
+        dbo_part = torch.empty((L, V), dtype=F32, device=dev)
         _lib.call("pbx_local_head", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
-                  y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dzo.data_ptr(),
-                  dbo.data_ptr(), loss.data_ptr(), B, L, V, st)
+                  y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(),
+                  dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, st)
         z = mm32(g2_bf, bf16_of(wa).t())
         dz = torch.empty((B, A), dtype=BF16, device=dev)
         dba = torch.zeros(A, dtype=F32, device=dev)
@@ -231,7 +246,7 @@ class HeadsLossFn(torch.autograd.Function):
             wsr, wsc = A, 1
         _lib.call("pbx_go_head", z.data_ptr(), ba.data_ptr(), y_g.float().contiguous().data_ptr(), wg.data_ptr(),
                   wsr, wsc, dz.data_ptr(), dba.data_ptr(), loss[1:].data_ptr(), B, A, st)
-        ctx.save_for_backward(h, dh, dzo, dbo, dz, dba, g2_bf)
+        ctx.save_for_backward(dh, dwo_part, dbo_part, dz, dba, g2_bf)
         ctx.params = (wo, bo, wa, ba)
         ctx.V = V
         total = loss.sum()
@@ -240,18 +255,39 @@ class HeadsLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dtotal, _dparts):
-        h, dh, dzo, dbo, dz, dba, g2_bf = ctx.saved_tensors
+        dh, dwo_part, dbo_part, dz, dba, g2_bf = ctx.saved_tensors
         wo, bo, wa, ba = ctx.params
-        B, L, C = h.shape
-        V = ctx.V
         gr = _Grads([wo, bo, wa, ba])
         dwo, dbo_dst, dwa, dba_dst = gr.dst
-        s = dtotal.reshape(()).to(F32)          # 1.0 for loss.backward(); kept on device (no sync)
-        dz_s = dz * s
-        dzo_s = dzo * s
+        if _UNIT_LOSS_GRAD[0]:
+            # loss.backward() from the training step: d(loss) == 1 exactly, skip the rescale passes
+            dz_s, dh_s = dz, dh
+            dwo.add_(dwo_part.sum(0))
+            dbo_dst.add_(dbo_part.sum(0))
+            dba_dst.add_(dba)
+        else:
+            s = dtotal.reshape(()).to(F32)
+            dz_s, dh_s = dz * s, dh * s
+            dwo.add_(dwo_part.sum(0) * s)
+            dbo_dst.add_(dbo_part.sum(0) * s)
+            dba_dst.add_(dba * s)
         dg2 = mm32(dz_s, bf16_of(wa))
         addmm_into(dwa, dz_s.t(), g2_bf)
-        addmm_into(dwo, dzo_s[:, :V].t(), h.reshape(B * L, C))
-        dbo_dst.add_(dbo * s)
-        dba_dst.add_(dba * s)
-        return (dh * s, dg2, None, *gr.finish(), None, None, None, None)
+        return (dh_s, dg2, None, *gr.finish(), None, None, None, None)
+
+
+_UNIT_LOSS_GRAD = [False]
+
+
+class unit_loss_grad:
+    """Context for ``loss.backward()`` with the implicit gradient 1.0 (the training step): lets the
+    fused loss skip scaling its precomputed gradients by d(loss)."""
+
+    def __enter__(self):
+        self._prev = _UNIT_LOSS_GRAD[0]
+        _UNIT_LOSS_GRAD[0] = True
+        return self
+
+    def __exit__(self, *exc):
+        _UNIT_LOSS_GRAD[0] = self._prev
+        return False

@@ -41,39 +41,41 @@ class FusedAdam(torch.optim.Optimizer):
         a = self.arena
         self.exp_avg = torch.zeros_like(a.data)
         self.exp_avg_sq = torch.zeros_like(a.data)
-        self.shadow = torch.zeros(a.numel, dtype=torch.bfloat16, device=a.data.device) if bf16_shadow else None
+        self.shadow = a.data.to(torch.bfloat16) if bf16_shadow else None
         self.step_count = 0
         self.grad_scale = 1.0   # set to 1/world by the DP wrapper (SUM all-reduce -> mean)
         self.skip_flag: Optional[torch.Tensor] = None  # device int32; non-zero -> skip update
         dev = a.data.device
+        # device-resident hyper-parameters + step counter: the update launch reads everything from
+        # device memory, so it can be captured in a hipGraph and replayed; the host only rewrites
+        # the hyper-parameter block when lr/betas/... change (prepare(), never during capture)
         self._hp_dev = torch.zeros(8, dtype=torch.float32, device=dev)
-        # ring of pinned staging buffers: the host never rewrites a buffer whose async H2D copy
-        # may still be queued behind GPU work
-        self._hp_ring = [torch.zeros(8, dtype=torch.float32, pin_memory=dev.type == "cuda") for _ in range(4)]
-        self._hp_events = [None] * 4
+        self._step_dev = torch.zeros(1, dtype=torch.float32, device=dev)
+        self._hp_host = None
         self._index = {id(p): a.param_index()[id(p)] for p in self.param_groups[0]["params"]}
 
     # ---------------------------------------------------------------------------------
     def zero_grad(self, set_to_none: bool = False) -> None:  # noqa: ARG002 - arena grads are views
         self.arena.zero_grad()
 
-    def _hparams(self) -> torch.Tensor:
+    def _hparam_values(self):
         g = self.param_groups[0]
         b1, b2 = g["betas"]
-        t = self.step_count
-        k = t % len(self._hp_ring)
-        if self._hp_events[k] is not None:
-            self._hp_events[k].synchronize()
-        h = self._hp_ring[k]
-        h[0] = g["lr"]
-        h[1] = b1
-        h[2] = b2
-        h[3] = g["eps"]
-        h[4] = g["weight_decay"]
-        h[5] = 1.0 - b1 ** t
-        h[6] = math.sqrt(1.0 - b2 ** t)
-        h[7] = self.grad_scale
-        return h
+        t = max(1, self.step_count)
+        return (float(g["lr"]), float(b1), float(b2), float(g["eps"]), float(g["weight_decay"]),
+                1.0 - b1 ** t, math.sqrt(1.0 - b2 ** t), float(self.grad_scale))
+
+    def prepare(self) -> None:
+        """Push changed hyper-parameters (lr from a scheduler, grad scale) to the device block.
+        Host -> device copy: call outside graph capture (the captured step reads the block)."""
+        vals = self._hparam_values()
+        key = vals[:5] + vals[7:]
+        if key != self._hp_host:
+            self._hp_dev.copy_(torch.tensor(vals, dtype=torch.float32))
+            self._hp_host = key
+
+    def sync_step_counter(self) -> None:
+        self._step_dev.fill_(float(self.step_count))
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -82,18 +84,16 @@ class FusedAdam(torch.optim.Optimizer):
         a = self.arena
         if not a.grads_attached():
             a.attach_grads()
-        h = self._hparams()
         if _hip_ok(a.data):
             from ..ops import _lib
-            self._hp_dev.copy_(h, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self._hp_events[self.step_count % len(self._hp_ring)] = ev
+            if not torch.cuda.is_current_stream_capturing():
+                self.prepare()
+            self._step_dev.add_(1.0)
             _lib.call("pbx_adam_flat", a.data.data_ptr(), a.grad.data_ptr(), self.exp_avg.data_ptr(),
                       self.exp_avg_sq.data_ptr(), _lib.ptr(self.shadow), a.numel, self._hp_dev.data_ptr(),
-                      _lib.ptr(self.skip_flag), _lib.stream_ptr(a.data.device))
+                      _lib.ptr(self.skip_flag), self._step_dev.data_ptr(), _lib.stream_ptr(a.data.device))
         else:
-            lr, b1, b2, eps, wd, bc1, bc2s, gs = [float(x) for x in h.tolist()]
+            lr, b1, b2, eps, wd, bc1, bc2s, gs = self._hparam_values()
             g = a.grad * gs
             if wd != 0:
                 g = g + wd * a.data
@@ -165,6 +165,7 @@ class FusedAdam(torch.optim.Optimizer):
             self.exp_avg_sq[o:o + n].copy_(s["exp_avg_sq"].reshape(-1))
             steps = int(float(s["step"]))
         self.step_count = steps
+        self.sync_step_counter()
 
 
 def make_optimizer(model: torch.nn.Module, lr: float = 2e-4, betas=(0.9, 0.999), eps: float = 1e-8,

@@ -59,7 +59,12 @@ class PretrainStep:
         opt = self.optimizer
         opt.zero_grad()
         loss = self.loss(X, Y, W)
-        loss.backward()
+        if self.model.resolved_backend(self.device) == "hip":
+            from ..ops.global_track import unit_loss_grad
+            with unit_loss_grad():
+                loss.backward()
+        else:
+            loss.backward()
         if self.ddp is not None:
             self.ddp.finish(average=not self.fused)
         if self.grad_clip is not None:
@@ -72,3 +77,45 @@ class PretrainStep:
             opt.skip_flag = (~torch.isfinite(opt.arena.grad.sum())).to(torch.int32).reshape(1)
         opt.step()
         return loss.detach()
+
+
+class GraphedStep:
+    """The whole training step captured once as a hipGraph and replayed.
+
+    Captures data generation (when ``batch_fn`` produces the batch on the device), forward, the fused
+    loss, backward, the (optional) DP all-reduce and the fused Adam update: ~290 kernel launches
+    become one ``hipGraphLaunch``, so the host never throttles the GPU.  Everything the replay reads
+    that changes between steps lives in device memory (synthetic-data and Adam step counters, Adam
+    hyper-parameters refreshed by :meth:`FusedAdam.prepare` before each replay).
+    """
+
+    def __init__(self, step: PretrainStep, batch_fn, warmup: int = 2):
+        if not torch.cuda.is_available():
+            raise RuntimeError("GraphedStep needs a GPU")
+        self.step = step
+        self.batch_fn = batch_fn
+        opt = step.optimizer
+        if not isinstance(opt, FusedAdam):
+            raise TypeError("GraphedStep needs the FusedAdam optimizer (device-side hyper-parameters)")
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(max(1, warmup)):
+                X, Y, W = batch_fn()
+                step(X, Y, W)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        opt.prepare()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            X, Y, W = batch_fn()
+            self.loss = step(X, Y, W)
+        # capture recorded the optimizer step without executing it: undo the host-side increment
+        opt.step_count -= 1
+
+    def __call__(self) -> torch.Tensor:
+        opt = self.step.optimizer
+        opt.step_count += 1
+        opt.prepare()
+        self.graph.replay()
+        return self.loss
