@@ -114,7 +114,13 @@ class H5Store(ProteinStore):  # pragma: no cover - needs h5py
 
 class ProteinStoreWriter:
     """Chunked writer for the E3 layout (reference ``create_h5_dataset`` pass 2,
-    ``uniref_dataset.py:249-268``).  ``fmt`` = ``pbxds`` | ``h5``."""
+    ``uniref_dataset.py:249-268``).  ``fmt`` = ``pbxds`` | ``h5``.
+
+    ``.pbxds`` records are streamed to raw side files as they arrive (only the per-record lengths
+    stay in memory), then converted to ``.npy`` in bounded chunks on :meth:`close`, so a
+    UniRef90-sized dataset is written in O(n) host memory of 16 B per record."""
+
+    _CHUNK = 1 << 24
 
     def __init__(self, path: str, included_annotations: Sequence[str], fmt: str = "auto"):
         if fmt == "auto":
@@ -124,21 +130,44 @@ class ProteinStoreWriter:
         self.path, self.fmt = path, fmt
         self.included_annotations = list(included_annotations)
         self.n_ann = len(self.included_annotations)
-        self._seqs: List[bytes] = []
-        self._ids: List[bytes] = []
-        self._bits: List[np.ndarray] = []
+        self._nbytes = (self.n_ann + 7) // 8
+        self._seq_lens: List[int] = []
+        self._id_lens: List[int] = []
+        if fmt == "pbxds":
+            os.makedirs(path, exist_ok=True)
+            self._fseq = open(os.path.join(path, "seq_bytes.raw"), "wb")
+            self._fid = open(os.path.join(path, "id_bytes.raw"), "wb")
+            self._fbits = open(os.path.join(path, "annotation_bits.raw"), "wb")
+        else:  # pragma: no cover - needs h5py
+            self._seqs: List[bytes] = []
+            self._ids: List[bytes] = []
+            self._bits: List[np.ndarray] = []
 
     def append(self, uniprot_id: str, seq: str, annotation_indices: Iterable[int]) -> None:
         mask = np.zeros(self.n_ann, dtype=bool)
         idx = np.fromiter((int(i) for i in annotation_indices), dtype=np.int64)
         if idx.size:
             mask[idx] = True
-        self._ids.append(uniprot_id.encode("utf-8"))
-        self._seqs.append(seq.encode("ascii"))
-        self._bits.append(np.packbits(mask, bitorder="little"))
+        self.append_mask(uniprot_id, seq, mask)
+
+    def append_mask(self, uniprot_id: str, seq: str, mask: np.ndarray) -> None:
+        uid, sq = uniprot_id.encode("utf-8"), seq.encode("ascii")
+        bits = np.packbits(np.asarray(mask, dtype=bool)[:self.n_ann], bitorder="little")
+        if bits.size < self._nbytes:
+            bits = np.pad(bits, (0, self._nbytes - bits.size))
+        self._seq_lens.append(len(sq))
+        self._id_lens.append(len(uid))
+        if self.fmt == "pbxds":
+            self._fseq.write(sq)
+            self._fid.write(uid)
+            self._fbits.write(bits.tobytes())
+        else:  # pragma: no cover
+            self._seqs.append(sq)
+            self._ids.append(uid)
+            self._bits.append(bits)
 
     def __len__(self) -> int:
-        return len(self._seqs)
+        return len(self._seq_lens)
 
     def close(self) -> None:
         if self.fmt == "pbxds":
@@ -146,24 +175,40 @@ class ProteinStoreWriter:
         else:  # pragma: no cover
             self._write_h5()
 
+    def _raw_to_npy(self, raw_name: str, npy_name: str, shape) -> None:
+        raw = os.path.join(self.path, raw_name)
+        out = np.lib.format.open_memmap(os.path.join(self.path, npy_name), mode="w+", dtype=np.uint8, shape=shape)
+        flat = out.reshape(-1)
+        with open(raw, "rb") as f:
+            pos = 0
+            while True:
+                buf = f.read(self._CHUNK)
+                if not buf:
+                    break
+                flat[pos:pos + len(buf)] = np.frombuffer(buf, dtype=np.uint8)
+                pos += len(buf)
+        if pos != flat.size:
+            raise IOError(f"{raw}: wrote {pos} bytes, expected {flat.size}")
+        out.flush()
+        del out, flat
+        os.remove(raw)
+
     def _write_pbxds(self) -> None:
-        os.makedirs(self.path, exist_ok=True)
-        n = len(self._seqs)
-        lens = np.array([len(s) for s in self._seqs], dtype=np.int64)
+        for fh in (self._fseq, self._fid, self._fbits):
+            fh.close()
+        n = len(self._seq_lens)
+        lens = np.asarray(self._seq_lens, dtype=np.int64)
         offs = np.zeros(n + 1, dtype=np.int64)
         np.cumsum(lens, out=offs[1:])
-        id_lens = np.array([len(s) for s in self._ids], dtype=np.int64)
         id_offs = np.zeros(n + 1, dtype=np.int64)
-        np.cumsum(id_lens, out=id_offs[1:])
-        nbytes = (self.n_ann + 7) // 8
-        bits = np.stack(self._bits) if n else np.zeros((0, nbytes), dtype=np.uint8)
+        np.cumsum(np.asarray(self._id_lens, dtype=np.int64), out=id_offs[1:])
         sv = lambda name, arr: np.save(os.path.join(self.path, name), arr, allow_pickle=False)  # noqa: E731
         sv("seq_offsets.npy", offs)
-        sv("seq_bytes.npy", np.frombuffer(b"".join(self._seqs), dtype=np.uint8))
         sv("seq_lengths.npy", lens.astype(np.int32))
-        sv("annotation_bits.npy", bits)
         sv("id_offsets.npy", id_offs)
-        sv("id_bytes.npy", np.frombuffer(b"".join(self._ids), dtype=np.uint8))
+        self._raw_to_npy("seq_bytes.raw", "seq_bytes.npy", (int(offs[-1]),))
+        self._raw_to_npy("id_bytes.raw", "id_bytes.npy", (int(id_offs[-1]),))
+        self._raw_to_npy("annotation_bits.raw", "annotation_bits.npy", (n, self._nbytes))
         with open(os.path.join(self.path, "meta.json"), "w") as f:
             json.dump({"version": PBXDS_VERSION, "n": n, "n_annotations": self.n_ann,
                        "included_annotations": self.included_annotations}, f)

@@ -377,8 +377,9 @@ __global__ void __launch_bounds__(256) go_head_kernel(const float* __restrict__ 
     }
     atomicAdd(dbias + c, dsum);
   }
-  lsum = wave_reduce_sum(lsum);
-  if ((threadIdx.x & 63) == 0) atomicAdd(loss, lsum * inv_ba);
+  __shared__ float red[8];
+  lsum = block_reduce(lsum, red);
+  if (threadIdx.x == 0) atomicAdd(loss, lsum * inv_ba);
 }
 }  // namespace
 
@@ -434,7 +435,7 @@ PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, c
 
 PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, const float* w, long wsr, long wsc,
                            void* dz, float* dbias, float* loss, int B, int A, hipStream_t st) {
-  const int gy = B < 64 ? B : 64;
+  const int gy = B < 16 ? B : 16;
   hipLaunchKernelGGL(go_head_kernel, dim3((A + 255) / 256, gy), dim3(256), 0, st, z, bias, y, w, wsr, wsc,
                      (bf16_t*)dz, dbias, loss, B, A, 1.0f / ((float)B * (float)A));
   return pbx_launch_status();

@@ -68,6 +68,7 @@ __device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict
 // and the next sample's rows are prefetched while the current one is in the MFMA.
 // Thread t (of 512) owns row j = t >> 4 (position l0 + j) and channel chunk ch = t & 15.
 constexpr int PB = 32;
+constexpr int YS = CH + 4;   // padded row stride of the fp32 D^T tile (lanes write 32 different rows)
 
 __device__ __forceinline__ uint4 ldq(const bf16_t* p, bool ok) {
   return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* ht = smem + 32768;                                  // h1 tile bf16, PB x 256 B
   float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // D^T tile fp32 [PB][128]
-  float* sh = yt + PB * CH;                                          // stats + reduction scratch
+  float* sh = yt + PB * YS;                                          // stats + reduction scratch
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int j = tid >> 4, ch = tid & 15;
@@ -136,13 +137,13 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
         acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(yt + r * CH + w * 32 + 8 * g + 4 * h) =
+        *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
             make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
     __syncthreads();
     float pre[8], o[8], lsum = 0.f;
-    const float4 ya = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8);
-    const float4 yb = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8 + 4);
+    const float4 ya = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
+    const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
     const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -356,7 +357,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16
   unsigned char* ht = dt + PB * 256;                                 // h1 tile bf16
   float* yt = reinterpret_cast<float*>(ht + PB * 256);               // [PB][128] fp32
-  float* sh = yt + PB * CH;
+  float* sh = yt + PB * YS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       }
 #pragma unroll
       for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(yt + r * CH + w * 32 + 8 * g + 4 * h) =
+        *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
             make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
     // dWl[co][ci] += sum_pos dpre[pos][co] h1[pos][ci]   (both operands transposed LDS reads)
@@ -456,8 +457,8 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       aw1 = mfma32(fa, fb1, aw1);
     }
     __syncthreads();
-    const float4 ya = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8);
-    const float4 yb = *reinterpret_cast<const float4*>(yt + j * CH + ch * 8 + 4);
+    const float4 ya = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
+    const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
     const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
     float o[8], sa = 0.f, sc = 0.f;
 #pragma unroll
@@ -574,19 +575,21 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restr
   *reinterpret_cast<uint4*>(out + row * CH + c8 * 8) = packq8(v);
 }
 
+// one wave per row: lane l adds channels 2l, 2l+1 of the row into the LDS copy of its token's row,
+// so every LDS atomic wave-instruction touches 64 consecutive addresses (no intra-instruction
+// conflicts); each workgroup then adds its 26 x 128 partial table into dE.
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restrict__ tok,
                                                         const bf16_t* __restrict__ dout, float* __restrict__ dE,
                                                         long rows, int V) {
   __shared__ float acc[32 * CH];
   for (int i = threadIdx.x; i < V * CH; i += 256) acc[i] = 0.f;
   __syncthreads();
-  const int c8 = threadIdx.x & 15;
-  for (long row = (long)blockIdx.x * 16 + (threadIdx.x >> 4); row < rows; row += (long)gridDim.x * 16) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (long row = (long)blockIdx.x * 4 + w; row < rows; row += (long)gridDim.x * 4) {
     const int t = (int)tok[row];
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(dout + row * CH + c8 * 8), v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(&acc[t * CH + c8 * 8 + e], v[e]);
+    const unsigned int q = *reinterpret_cast<const unsigned int*>(dout + row * CH + 2 * lane);
+    atomicAdd(&acc[t * CH + 2 * lane], __uint_as_float(q << 16));
+    atomicAdd(&acc[t * CH + 2 * lane + 1], __uint_as_float(q & 0xffff0000u));
   }
   __syncthreads();
   for (int i = threadIdx.x; i < V * CH; i += 256) atomicAdd(dE + i, acc[i]);
@@ -629,7 +632,7 @@ PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int B
                                  const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
                                  float* st2, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int lds = 32768 + PB * 256 + PB * CH * 4 + 128;
+  const int lds = 32768 + PB * 256 + PB * YS * 4 + 128;
   hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
                      (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
   return pbx_launch_status();
@@ -666,7 +669,7 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int lds = 32768 + 2 * PB * 256 + PB * CH * 4 + 128;
+  const int lds = 32768 + 2 * PB * 256 + PB * YS * 4 + 128;
   hipLaunchKernelGGL(ln2_linear_bwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh2, (const bf16_t*)s2, st2,
                      sums2, TS2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
                      (const bf16_t*)wl, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L, eps);
@@ -692,8 +695,8 @@ PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long ro
 
 PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long rows, int V, hipStream_t st) {
   if (V > 32) return (int)hipErrorInvalidValue;
-  long g = (rows + 15) / 16;
-  if (g > 128) g = 128;    // few adders per address: the 26 x 128 table is tiny and hot
+  long g = (rows + 3) / 4;
+  if (g > 256) g = 256;    // few adders per address: the 26 x 128 table is tiny and hot
   hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
                      (const bf16_t*)dout, dE, rows, V);
   return pbx_launch_status();
