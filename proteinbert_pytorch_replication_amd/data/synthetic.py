@@ -134,3 +134,35 @@ class SyntheticUniRefGO:
     def next_batch(self) -> Batch:
         tok, ann = self.clean_batch()
         return self.corrupt(tok, ann)
+
+
+class SyntheticSecondaryStructure(torch.utils.data.Dataset):
+    """Per-residue labelled synthetic proteins for the fine-tuning path (BASELINE cfg 5).
+
+    Item: ``(tokens int64 [L], labels int64 [L])``; labels are a fixed function of the residue
+    window ``(x[i-1], x[i], x[i+1])`` (so a head on a contextual encoder can learn them), ``-100``
+    on ``<sos>``/``<eos>``/``<pad>``.  ``n_classes`` 3 (H/E/C) or 8 (DSSP) by convention.
+    """
+
+    def __init__(self, n: int, seq_len: int, n_classes: int = 8, min_length: int = 16,
+                 max_length: Optional[int] = None, seed: int = 0):
+        g = torch.Generator().manual_seed(seed)
+        L = seq_len
+        max_length = max_length if max_length is not None else L - 2
+        lens = torch.randint(min_length, max_length + 1, (n,), generator=g)
+        aa = torch.randint(4, VOCAB_SIZE, (n, L), generator=g)
+        pos = torch.arange(L).unsqueeze(0)
+        tok = torch.where(pos == 0, torch.full_like(aa, SOS_ID), aa)
+        tok = torch.where(pos == lens.unsqueeze(1) + 1, torch.full_like(aa, EOS_ID), tok)
+        tok = torch.where(pos > lens.unsqueeze(1) + 1, torch.full_like(aa, PAD_ID), tok)
+        prev = torch.roll(tok, 1, 1)
+        nxt = torch.roll(tok, -1, 1)
+        lab = (tok * 7 + prev * 3 + nxt * 5) % n_classes
+        lab = torch.where(tok > EOS_ID, lab, torch.full_like(lab, -100))
+        self.tokens, self.labels = tok, lab
+
+    def __len__(self) -> int:
+        return self.tokens.shape[0]
+
+    def __getitem__(self, i: int):
+        return self.tokens[i], self.labels[i]

@@ -55,3 +55,21 @@ def corrupt_batch(tokens: torch.Tensor, ann: torch.Tensor, params, seed: int, st
     return ({"local": x_local, "global": x_global},
             {"local": tokens, "global": ann},
             {"local": w_local, "global": w_sample.unsqueeze(1).expand(B, A)})
+
+
+_lib.register("pbx_unpack_batch", [_P, _P, _P, _P, _I, _I, _I, _I, _P])
+
+
+def unpack_batch(tok_u8: torch.Tensor, bits: torch.Tensor, A: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Expand a compact loader batch on the device: u8 tokens -> int64, annotation bits -> f32."""
+    _check(tok_u8, torch.uint8, "tok_u8")
+    _check(bits, torch.uint8, "bits")
+    B, L = tok_u8.shape
+    nbytes = bits.shape[1]
+    if bits.shape[0] != B or nbytes * 8 < A:
+        raise ValueError("bits shape does not cover the annotation count")
+    tokens = torch.empty((B, L), dtype=torch.long, device=tok_u8.device)
+    ann = torch.empty((B, A), dtype=torch.float32, device=tok_u8.device)
+    _lib.call("pbx_unpack_batch", tok_u8.data_ptr(), bits.data_ptr(), tokens.data_ptr(), ann.data_ptr(), B, L, A,
+              nbytes, _lib.stream_ptr(tok_u8.device))
+    return tokens, ann

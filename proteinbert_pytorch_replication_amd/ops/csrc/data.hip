@@ -126,3 +126,33 @@ PBX_EXPORT int pbx_corrupt_batch(const void* tokens, const void* ann, void* x_lo
                      (const long long*)step_dev);
   return pbx_launch_status();
 }
+
+// ---- expansion of a compact host batch (ops/csrc/pbx_loader.cpp) -----------------------------
+// tokens_u8 [B, L] -> int64 [B, L]; bits [B, nbytes] (little-endian per byte) -> f32 [B, A].
+// grid (B), block 256; each thread expands one byte (8 annotations) per iteration.
+__global__ void __launch_bounds__(256) unpack_batch_kernel(const unsigned char* __restrict__ tok_u8,
+                                                           const unsigned char* __restrict__ bits,
+                                                           long long* __restrict__ tokens,
+                                                           float* __restrict__ ann, int L, int A, int nbytes) {
+  const int b = blockIdx.x;
+  const unsigned char* tb = tok_u8 + (size_t)b * L;
+  long long* to = tokens + (size_t)b * L;
+  for (int j = threadIdx.x; j < L; j += blockDim.x) to[j] = (long long)tb[j];
+  const unsigned char* bb = bits + (size_t)b * nbytes;
+  float* ao = ann + (size_t)b * A;
+  for (int k = threadIdx.x; k < nbytes; k += blockDim.x) {
+    const unsigned v = bb[k];
+    const int a0 = k * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (a0 + i < A) ao[a0 + i] = (float)((v >> i) & 1u);
+  }
+}
+
+PBX_EXPORT int pbx_unpack_batch(const void* tok_u8, const void* bits, void* tokens, void* ann, int B, int L, int A,
+                                int nbytes, hipStream_t stream) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(unpack_batch_kernel, dim3(B), dim3(256), 0, stream, (const unsigned char*)tok_u8,
+                     (const unsigned char*)bits, (long long*)tokens, (float*)ann, L, A, nbytes);
+  return pbx_launch_status();
+}

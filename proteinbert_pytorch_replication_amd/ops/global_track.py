@@ -45,6 +45,10 @@ def bf16_of(p: torch.Tensor) -> torch.Tensor:
     """bf16 copy of a parameter: the optimizer-maintained shadow view when the arena has one."""
     v = getattr(p, "_pbx_bf16", None)
     if v is not None:
+        if p._version != p._pbx_bf16_ver:      # written outside the optimizer: refresh the mirror
+            with torch.no_grad():
+                v.copy_(p.detach())
+            p._pbx_bf16_ver = p._version
         return v
     return p.detach().to(BF16)
 

@@ -23,6 +23,7 @@ import torch
 
 from . import _lib
 from ..train.arena import notify_grads_ready
+from .global_track import bf16_of
 
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
@@ -113,7 +114,7 @@ class LocalBlockFn(torch.autograd.Function):
         T2 = (L + PB - 1) // PB
         wpn, wtn = pack_conv(wn)
         wpw, wtw = pack_conv(ww)
-        wl_b = wl.detach().to(torch.bfloat16).contiguous()
+        wl_b = bf16_of(wl)
         gb = gb.detach().float().contiguous()
         pre_n = torch.empty_like(x)
         pre_w = torch.empty_like(x)

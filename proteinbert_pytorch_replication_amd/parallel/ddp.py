@@ -138,6 +138,7 @@ class BucketedAllReduce:
         if not self.enabled:
             return
         dist.broadcast(self.arena.data, src, group=self.pg)
+        self.arena.invalidate_bf16_shadow()
         if module is not None:
             for buf in module.buffers():
                 dist.broadcast(buf.data, src, group=self.pg)

@@ -110,6 +110,8 @@ def broadcast_module(module: torch.nn.Module, src: int = 0) -> None:
     with torch.no_grad():
         for t in list(module.parameters()) + list(module.buffers()):
             dist.broadcast(t.data, src)
+    from ..train.arena import invalidate_bf16_mirrors
+    invalidate_bf16_mirrors(module.parameters())
 
 
 def destroy() -> None:

@@ -68,11 +68,34 @@ class FlatArena:
             self.attach_grads()
         self.grad.zero_()
 
+    def attach_bf16_shadow(self, shadow: torch.Tensor) -> None:
+        """Point every parameter's ``_pbx_bf16`` at its segment of a bf16 mirror of the arena that
+        the fused optimizer rewrites on each update, so forward/backward GEMMs read bf16 weights
+        without a cast launch per use.  A parameter written outside the optimizer (``p.copy_``,
+        ``load_state_dict``) bumps its version counter and its segment is refreshed on next use
+        (:func:`ops.global_track.bf16_of`)."""
+        if shadow.numel() != self.numel or shadow.dtype != torch.bfloat16:
+            raise ValueError("shadow must be a bf16 tensor with the arena's element count")
+        for p, (o, n) in zip(self.params, self.offsets):
+            p._pbx_bf16 = shadow[o:o + n].view(p.shape)
+            p._pbx_bf16_ver = p._version
+
+    def invalidate_bf16_shadow(self) -> None:
+        """Force a refresh of every bf16 mirror on next use (after writes that bypass autograd's
+        version counter, e.g. a collective broadcast into ``arena.data``)."""
+        invalidate_bf16_mirrors(self.params)
+
     def param_index(self) -> Dict[int, int]:
         return {id(p): i for i, p in enumerate(self.params)}
 
     def segment(self, i: int) -> Tuple[int, int]:
         return self.offsets[i]
+
+
+def invalidate_bf16_mirrors(params: Iterable[torch.Tensor]) -> None:
+    for p in params:
+        if getattr(p, "_pbx_bf16", None) is not None:
+            p._pbx_bf16_ver = -1
 
 
 # --- direct gradient writes ---------------------------------------------------------------------

@@ -27,7 +27,7 @@ def _hip_ok(t: torch.Tensor) -> bool:
 
 class FusedAdam(torch.optim.Optimizer):
     def __init__(self, params, lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.0, arena: Optional[FlatArena] = None, bf16_shadow: bool = False):
+                 weight_decay: float = 0.0, arena: Optional[FlatArena] = None, bf16_shadow: Optional[bool] = None):
         if isinstance(params, FlatArena):
             arena, params = params, params.params
         params = [p for p in params if p.requires_grad]
@@ -41,7 +41,11 @@ class FusedAdam(torch.optim.Optimizer):
         a = self.arena
         self.exp_avg = torch.zeros_like(a.data)
         self.exp_avg_sq = torch.zeros_like(a.data)
+        if bf16_shadow is None:   # default: keep a bf16 weight mirror whenever the arena is on the GPU
+            bf16_shadow = a.data.is_cuda
         self.shadow = a.data.to(torch.bfloat16) if bf16_shadow else None
+        if self.shadow is not None:
+            a.attach_bf16_shadow(self.shadow)
         self.step_count = 0
         self.grad_scale = 1.0   # set to 1/world by the DP wrapper (SUM all-reduce -> mean)
         self.skip_flag: Optional[torch.Tensor] = None  # device int32; non-zero -> skip update

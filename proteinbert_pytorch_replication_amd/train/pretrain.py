@@ -42,6 +42,12 @@ def _to_device(d: Dict[str, torch.Tensor], device) -> Dict[str, torch.Tensor]:
     return {k: v.to(device, non_blocking=True) for k, v in d.items()}
 
 
+def _loader_state(loader) -> Dict[str, Any]:
+    """Resumable loaders (NativeStoreLoader) store their cursor in the checkpoint."""
+    sd = getattr(loader, "state_dict", None)
+    return {"loader": sd()} if callable(sd) and not isinstance(loader, torch.nn.Module) else {}
+
+
 def _maybe_fuse_optimizer(model, optimizer) -> torch.optim.Optimizer:
     if isinstance(optimizer, FusedAdam) or type(optimizer) is not torch.optim.Adam:
         return optimizer
@@ -101,6 +107,9 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             model.load_attention_heads_state(extra["attention_heads"])
         if "rng" in extra and extra.get("world_size", 1) == info.world_size:
             set_rng_state(extra["rng"], device)
+        if "loader" in extra and hasattr(train_dataloader, "load_state_dict") \
+                and extra.get("world_size", 1) == info.world_size:
+            train_dataloader.load_state_dict(extra["loader"])
         logging.info("Checkpoint loaded!")
 
     fault_at = int(os.environ.get("PBX_FAULT_AT_STEP", "0") or 0)
@@ -150,7 +159,7 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             if current % nb_iterations_checkpoint == 0:
                 ckpt = build_checkpoint(current, model, optimizer, scheduler, last_loss,
                                         extra={"rng": rng_state(device), "world_size": info.world_size,
-                                               "data_cursor": current})
+                                               "data_cursor": current, **_loader_state(train_dataloader)})
                 writer.save(ckpt, checkpoint_name(current))
                 pdist.barrier()
         if not progressed:

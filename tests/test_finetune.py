@@ -1,0 +1,84 @@
+"""Fine-tune mode (T2/T3 semantics): frozen-encoder per-residue head, train_step/test_step contract."""
+import pytest
+import torch
+from torch.utils.data import DataLoader
+
+from proteinbert_pytorch_replication_amd.data.synthetic import SyntheticSecondaryStructure
+from proteinbert_pytorch_replication_amd.models import (ProteinBERT, ProteinBERTForSequenceClassification,
+                                                        ProteinBERTForTokenClassification)
+from proteinbert_pytorch_replication_amd.train.finetune import finetune, test_step, token_accuracy, train_step
+from proteinbert_pytorch_replication_amd.train.optim import FusedAdam
+
+
+def _encoder(device="cpu", L=32, backend="torch"):
+    torch.manual_seed(0)
+    return ProteinBERT(sequences_length=L, num_annotations=64, local_dim=32, global_dim=64, key_dim=16,
+                       num_heads=2, num_blocks=2, device=device, backend=backend)
+
+
+def test_frozen_encoder_token_head_learns():
+    enc = _encoder()
+    before = {k: v.clone() for k, v in enc.state_dict().items()}
+    model = ProteinBERTForTokenClassification(enc, n_classes=3)
+    ds = SyntheticSecondaryStructure(96, 32, n_classes=3, seed=1)
+    dl = DataLoader(ds, batch_size=16, shuffle=True)
+    opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=2e-2)
+    assert sum(p.numel() for p in model.parameters() if p.requires_grad) == 32 * 3 + 3 + 64 * 3
+    res = finetune(model, dl, opt, epochs=6, test_dataloader=DataLoader(ds, batch_size=32),
+                   metrics={"accuracy": token_accuracy()}, device="cpu")
+    assert res["train_loss"][-1] < res["train_loss"][0]
+    assert 0.0 <= res["test_metrics"][-1]["accuracy"] <= 1.0
+    for k, v in enc.state_dict().items():
+        assert torch.equal(v, before[k]), k          # frozen
+    assert not enc.training                           # encoder stays in eval mode
+
+
+def test_train_step_reference_contract_and_clipping():
+    enc = _encoder()
+    model = ProteinBERTForTokenClassification(enc, n_classes=8, freeze_encoder=False, use_global=False)
+    ds = SyntheticSecondaryStructure(32, 32, n_classes=8, seed=2)
+    dl = DataLoader(ds, batch_size=8)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    loss_fn = torch.nn.CrossEntropyLoss(ignore_index=-100)
+    w0 = enc.local_embedding.weight.detach().clone()
+    tl, tm = train_step(model, dl, loss_fn, opt, {"acc": token_accuracy()}, True, 1.0, "cpu")
+    assert isinstance(tl, float) and set(tm) == {"acc"}
+    assert not torch.equal(w0, enc.local_embedding.weight)   # unfrozen encoder trains
+    vl, vm = test_step(model, dl, loss_fn, {"acc": token_accuracy()}, "cpu")
+    assert isinstance(vl, float) and 0 <= vm["acc"] <= 1
+    X, y = next(iter(dl))
+    assert model(X).shape == (8, 8, 32)                         # class axis = dim 1
+
+
+def test_sequence_head_on_global_track():
+    enc = _encoder()
+    model = ProteinBERTForSequenceClassification(enc, n_classes=5)
+    tok = torch.randint(4, 26, (4, 32))
+    out = model({"local": tok, "global": torch.zeros(4, 64)})
+    assert out.shape == (4, 5)
+    out.sum().backward()
+    assert model.head.weight.grad is not None and enc.local_embedding.weight.grad is None
+
+
+@pytest.mark.gpu
+def test_hip_encoder_finetune_matches_torch_encoder():
+    L = 128
+    torch.manual_seed(0)
+    enc = ProteinBERT(sequences_length=L, num_annotations=256, local_dim=128, global_dim=256, key_dim=64,
+                      num_heads=4, num_blocks=2, device="cuda", backend="hip")
+    m_hip = ProteinBERTForTokenClassification(enc, n_classes=8)
+    ds = SyntheticSecondaryStructure(16, L, n_classes=8)
+    X, y = ds.tokens.cuda(), ds.labels.cuda()
+    out_hip = m_hip(X)
+    enc.backend = "torch"
+    out_ref = m_hip(X)
+    enc.backend = "hip"
+    torch.testing.assert_close(out_hip, out_ref, rtol=0.05, atol=0.05)
+    # unfrozen: gradients reach the encoder through the fused HIP backward
+    m2 = ProteinBERTForTokenClassification(enc, n_classes=8, freeze_encoder=False)
+    for p in enc.parameters():
+        p.requires_grad_(True)
+    opt = FusedAdam(m2.parameters(), lr=1e-4)
+    tl, _ = train_step(m2, [(X, y)], torch.nn.CrossEntropyLoss(ignore_index=-100), opt, {}, True, 1.0, "cuda")
+    assert tl == tl
+    assert enc.proteinBERT_blocks[0].local_narrow_conv_layer[0].weight.grad.abs().sum() > 0

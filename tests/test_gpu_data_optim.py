@@ -84,3 +84,32 @@ def test_synth_and_corrupt_kernels():
     assert 0.4 < blank.float().mean().item() < 0.6
     kept = X["global"][~blank][ann[~blank] > 0]
     assert abs((kept > 0).float().mean().item() - 0.75) < 0.05
+
+
+def test_native_loader_gpu_expansion_matches_cpu(tmp_path):
+    """Compact loader batches expanded by pbx_unpack_batch == the NumPy expansion."""
+    import numpy as np
+    from proteinbert_pytorch_replication_amd.data.native_loader import NativeStoreLoader
+    from proteinbert_pytorch_replication_amd.data.store import ProteinStoreWriter
+    rng = np.random.default_rng(1)
+    A = 8943
+    path = str(tmp_path / "g.pbxds")
+    w = ProteinStoreWriter(path, ["a%d" % i for i in range(A)])
+    for i in range(70):
+        w.append_mask("p%d" % i, "".join(rng.choice(list("ACDEFGHIKLMNPQRSTVWY"), int(rng.integers(5, 700)))),
+                      rng.random(A) < 0.01)
+    w.close()
+    g = NativeStoreLoader(path, 16, 512, device="cuda", seed=4)
+    c = NativeStoreLoader(path, 16, 512, device="cpu", seed=4)
+    for _ in range(6):
+        Xg, Yg, Wg = g.next_batch()
+        Xc, Yc, Wc = c.next_batch()
+        torch.cuda.synchronize()
+        assert torch.equal(Yg["local"].cpu(), Yc["local"])
+        assert torch.equal(Yg["global"].cpu(), Yc["global"])
+        assert torch.equal(Wg["local"].cpu(), Wc["local"])
+        assert torch.equal(Wg["global"].cpu(), Wc["global"])
+        special = Yg["local"] <= 2
+        assert torch.equal(Xg["local"][special], Yg["local"][special])
+    g.close()
+    c.close()

@@ -33,6 +33,9 @@ def test_graphed_step_matches_eager():
         assert abs(a - b) < 1e-4 * abs(a) + 1e-6, (eager, graphed)
     assert o2.step_count == o1.step_count == 5
     for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
-        # Adam normalises updates: gradient noise from float atomics can flip a ~lr-sized step on
-        # parameters whose true gradient is ~0, so parameters are compared at the lr scale
-        assert torch.allclose(p1, p2, rtol=1e-3, atol=3e-3), n
+        # Adam normalises updates: float-atomic noise in a gradient whose true value is ~0 can flip
+        # the sign of an lr-sized step.  Bound every element by the largest possible divergence
+        # (2*lr per step after the two shared warmup steps) and require nearly all to agree closely.
+        d = (p1 - p2).abs()
+        assert float(d.max()) <= 2 * 1e-3 * 3 + 1e-5, n
+        assert float((d > 1e-4).float().mean()) < 0.02, (n, float((d > 1e-4).float().mean()))
