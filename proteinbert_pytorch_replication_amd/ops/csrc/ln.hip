@@ -93,6 +93,9 @@ __device__ __forceinline__ void sample_stats(float* sh, const float* __restrict_
 
 // h1 = LN(s1) ; pre = h1 Wl^T + bl ; s2 = h1 + GELU(pre)  (+ s2 (mean, M2) partial per 32 positions)
 // grid (ceil(L/PB), nbg), 512 threads; waves 0-3 run the 32x32 MFMA tiles of D[co][pos].
+// Per-sample LN1 statistics are computed for all of the workgroup's samples up front (one wave per
+// sample, parallel partial loads) and the s2 tile partials are merged per wave into an LDS table
+// that is reduced once at the end, so a sample costs two barriers.
 __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
     const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ bl,
@@ -100,8 +103,8 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* ht = smem + 32768;                                  // h1 tile bf16, PB x 256 B
-  float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // D^T tile fp32 [PB][128]
-  float* sh = yt + PB * YS;                                          // stats + reduction scratch
+  float* yt = reinterpret_cast<float*>(smem + 32768 + PB * 256);     // D^T tile fp32 [PB][YS]
+  float* tab = yt + PB * YS;                                         // [nb][2] stats, [nb][8][2] partials
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int j = tid >> 4, ch = tid & 15;
@@ -110,19 +113,25 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
   const int TP = (L + PB - 1) / PB;
   const int nbg = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
+  const int nb = b1 - b0;
+  float* part = tab + 2 * nb;
   stage_weight(ws, wl, CH);
+  for (int i = w; i < nb; i += 8) {
+    float mean, rstd;
+    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    if (lane == 0) { tab[2 * i] = mean; tab[2 * i + 1] = rstd; }
+  }
   float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bb[8];
   if (okl) {
     load_f8(g1 + (size_t)l * CH + ch * 8, gam);
     load_f8(be1 + (size_t)l * CH + ch * 8, bet);
   }
   load_f8(bl + ch * 8, bb);
-  const int vrows = min(PB, L - l0);
-  uint4 nxt = ldq(s1 + ((size_t)b0 * L + l) * CH + ch * 8, okl && b0 < b1);
+  uint4 nxt = ldq(s1 + ((size_t)b0 * L + l) * CH + ch * 8, okl && nb > 0);
+  __syncthreads();
   for (int b = b0; b < b1; ++b) {
-    sample_stats(sh, st1 + (size_t)b * T1 * 2, T1, BM1, L, eps, nullptr, 0, 0.f);
-    __syncthreads();
-    const float mean = sh[0], rstd = sh[1];
+    const int i = b - b0;
+    const float mean = tab[2 * i], rstd = tab[2 * i + 1];
     float sv[8], h1[8];
     unpack8(nxt, sv);
 #pragma unroll
@@ -156,15 +165,24 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
       *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);
       *reinterpret_cast<uint4*>(s2 + off) = packq8(o);
     }
-    const float tmean = block_sum(lsum, sh + 8, 8) / (float)(vrows * CH);
-    float m2 = 0.f;
+    // this thread's (count, mean, M2), merged across the wave into the LDS partial table
+    float n = okl ? 8.f : 0.f, m = okl ? lsum * 0.125f : 0.f, M2 = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) m2 += okl ? (o[e] - tmean) * (o[e] - tmean) : 0.f;
-    m2 = block_sum(m2, sh + 16, 8);
-    if (tid == 0) {
-      st2[((size_t)b * TP + blockIdx.x) * 2] = tmean;
-      st2[((size_t)b * TP + blockIdx.x) * 2 + 1] = m2;
+    for (int e = 0; e < 8; ++e) M2 += okl ? (o[e] - m) * (o[e] - m) : 0.f;
+    wave_chan(n, m, M2);
+    if (lane == 0) { part[(i * 8 + w) * 2] = m; part[(i * 8 + w) * 2 + 1] = M2; }
+  }
+  __syncthreads();
+  const int vrows = min(PB, L - l0);
+  for (int i = tid; i < nb; i += 512) {
+    float n = 0.f, m = 0.f, M2 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) {
+      const float nw = (float)(max(0, min(4, vrows - 4 * ww)) * CH);
+      chan_merge(n, m, M2, nw, part[(i * 8 + ww) * 2], part[(i * 8 + ww) * 2 + 1]);
     }
+    st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = m;
+    st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = M2;
   }
 }
 
@@ -203,7 +221,7 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
     const int b = tile / TA, t = tile - (tile / TA) * TA;
     const int pos0 = t * BMA;
     float mean, rstd;
-    ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
     for (int j = tid; j < NJ; j += blockDim.x) red[j] = 0.f;
     const int pos = pos0 + w * 32 + r;
     const bool okb = pos < L;
@@ -305,7 +323,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
     }
     // Y[ci][pos]; LN2 backward partials
     float mean, rstd;
-    ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
     float sa = 0.f, sc = 0.f;
     if (okb) {
 #pragma unroll
@@ -369,7 +387,21 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   const int nbg = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
   const float inv_n = 1.0f / (float)(L * CH);
+  const int nb = b1 - b0;
+  float* tab = sh;                      // [nb][8]: mean2 rstd2 m1 m2 mean1 rstd1
+  float* part = sh + 8 * nb;            // [nb][8 waves][2]: LN1 backward partial sums
   stage_weight(ws, wl, CH);
+  for (int i = w; i < nb; i += 8) {
+    const int b = b0 + i;
+    float mean2, rstd2, m1, m2, mean1, rstd1;
+    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, PB, L, CH, eps, mean2, rstd2);
+    wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, inv_n, m1, m2);
+    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
+    if (lane == 0) {
+      tab[8 * i] = mean2; tab[8 * i + 1] = rstd2; tab[8 * i + 2] = m1; tab[8 * i + 3] = m2;
+      tab[8 * i + 4] = mean1; tab[8 * i + 5] = rstd1;
+    }
+  }
   float ga2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (okl) {
     load_f8(g2 + (size_t)l * CH + ch * 8, ga2);
@@ -387,17 +419,10 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   uint4 n_s2 = ldq(s2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
   uint4 n_pr = ldq(pre_l + (size_t)b0 * L * CH + coff, okl && b0 < b1);
   uint4 n_s1 = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  __syncthreads();
   for (int b = b0; b < b1; ++b) {
-    if (threadIdx.x == 0) {
-      float mean, rstd, m1, m2;
-      ln_stats(st2 + (size_t)b * T2 * 2, T2, PB, L, CH, eps, mean, rstd);
-      ln_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, inv_n, m1, m2);
-      sh[0] = mean; sh[1] = rstd; sh[2] = m1; sh[3] = m2;
-      ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
-      sh[4] = mean; sh[5] = rstd;
-    }
-    __syncthreads();
-    const float mean2 = sh[0], rstd2 = sh[1], m1 = sh[2], m2 = sh[3], mean1 = sh[4], rstd1 = sh[5];
+    const float* tb = tab + 8 * (b - b0);
+    const float mean2 = tb[0], rstd2 = tb[1], m1 = tb[2], m2 = tb[3], mean1 = tb[4], rstd1 = tb[5];
     float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
     unpack8(n_dh, dh);
     unpack8(n_s2, sv2);
@@ -471,12 +496,20 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       adb1[e] += o[e];
     }
     if (okl) *reinterpret_cast<uint4*>(dh1 + off) = packq8(o);
-    sa = block_sum(sa, sh + 8, 8);
-    sc = block_sum(sc, sh + 16, 8);
-    if (tid == 0) {
-      sums1[((size_t)b * TP + blockIdx.x) * 2] = sa;
-      sums1[((size_t)b * TP + blockIdx.x) * 2 + 1] = sc;
+    sa = wave_reduce_sum(sa);
+    sc = wave_reduce_sum(sc);
+    if (lane == 0) {
+      part[((b - b0) * 8 + w) * 2] = sa;
+      part[((b - b0) * 8 + w) * 2 + 1] = sc;
     }
+  }
+  __syncthreads();
+  for (int i = tid; i < nb; i += 512) {
+    float a = 0.f, c = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < 8; ++ww) { a += part[(i * 8 + ww) * 2]; c += part[(i * 8 + ww) * 2 + 1]; }
+    sums1[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = a;
+    sums1[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = c;
   }
   // [L, C] affine gradients: transpose through LDS so each wave-instruction adds 256 contiguous bytes
   float* accs[4] = {adg2, adb2, adg1, adb1};
@@ -519,24 +552,33 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     const bf16_t* __restrict__ dh1, const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1,
     const float* __restrict__ sums1, int TS1, const float* __restrict__ g1, bf16_t* __restrict__ ds1,
     float* __restrict__ dgb, int B, int L, float eps) {
-  __shared__ float red[PB * CH];
-  __shared__ float sh[8];
-  const int tid = threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* red = reinterpret_cast<float*>(smem);            // 2 x [PB][CH] (double-buffered)
+  float* tab = red + 2 * PB * CH;                          // [nb][4]: mean rstd m1 m2
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j = tid >> 4, ch = tid & 15;
   const int l0 = blockIdx.x * PB, l = l0 + j;
   const bool okl = l < L;
   const int nbg = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
+  const int nb = b1 - b0;
   const float inv_n = 1.0f / (float)(L * CH);
+  for (int i = w; i < nb; i += 8) {
+    float mean, rstd, m1, m2;
+    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    wave_bwd_consts(sums1 + (size_t)(b0 + i) * TS1 * 2, TS1, inv_n, m1, m2);
+    if (lane == 0) { tab[4 * i] = mean; tab[4 * i + 1] = rstd; tab[4 * i + 2] = m1; tab[4 * i + 3] = m2; }
+  }
   float ga[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (okl) load_f8(g1 + (size_t)l * CH + ch * 8, ga);
   const size_t coff = (size_t)l * CH + ch * 8;
   uint4 n_dh = ldq(dh1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
   uint4 n_s = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  __syncthreads();
   for (int b = b0; b < b1; ++b) {
-    sample_stats(sh, st1 + (size_t)b * T1 * 2, T1, BM1, L, eps, sums1 + (size_t)b * TS1 * 2, TS1, inv_n);
-    __syncthreads();
-    const float mean = sh[0], rstd = sh[1], m1 = sh[2], m2 = sh[3];
+    const float* tb = tab + 4 * (b - b0);
+    const float mean = tb[0], rstd = tb[1], m1 = tb[2], m2 = tb[3];
+    float* rb = red + ((b - b0) & 1) * PB * CH;
     float dv[8], sv[8], o[8];
     unpack8(n_dh, dv);
     unpack8(n_s, sv);
@@ -549,15 +591,14 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + coff) = qv;
     unpack8(qv, o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) red[j * CH + ch * 8 + e] = o[e];
-    __syncthreads();
+    for (int e = 0; e < 8; ++e) rb[j * CH + ch * 8 + e] = o[e];
+    __syncthreads();   // (double buffer: the next sample writes the other half)
     if (tid < CH) {
       float a = 0.f;
 #pragma unroll 8
-      for (int k = 0; k < PB; ++k) a += red[k * CH + tid];
+      for (int k = 0; k < PB; ++k) a += rb[k * CH + tid];
       atomicAdd(dgb + (size_t)b * CH + tid, a);
     }
-    __syncthreads();
   }
 }
 
@@ -619,6 +660,9 @@ static void set_ln_attrs() {
   if (ln_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
 }
 
@@ -632,7 +676,10 @@ PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int B
                                  const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
                                  float* st2, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int lds = 32768 + PB * 256 + PB * YS * 4 + 128;
+  const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
+  const int lds = 32768 + PB * 256 + PB * YS * 4 + nbmax * 18 * 4;
+  if (lds > 163840) return (int)hipErrorInvalidValue;
+  set_ln_attrs();
   hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
                      (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
   return pbx_launch_status();
@@ -669,7 +716,10 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int lds = 32768 + 2 * PB * 256 + PB * YS * 4 + 128;
+  const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
+  const int lds = 32768 + 2 * PB * 256 + PB * YS * 4 + nbmax * 24 * 4;
+  if (lds > 163840) return (int)hipErrorInvalidValue;
+  set_ln_attrs();
   hipLaunchKernelGGL(ln2_linear_bwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh2, (const bf16_t*)s2, st2,
                      sums2, TS2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
                      (const bf16_t*)wl, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L, eps);
@@ -681,7 +731,11 @@ PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st
                                 const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
                                 float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), 0, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
+  const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
+  const int lds = 2 * PB * CH * 4 + nbmax * 16;
+  if (lds > 163840) return (int)hipErrorInvalidValue;
+  set_ln_attrs();
+  hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
                      BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, B, L, eps);
   return pbx_launch_status();
 }

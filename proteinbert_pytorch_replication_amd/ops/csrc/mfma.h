@@ -143,4 +143,59 @@ __device__ __forceinline__ void ln_bwd_consts(const float* __restrict__ part, in
   m2 = c * inv_n;
 }
 
+// Chan et al. merge of (count, mean, M2) partials: (n, m, M2) <- (n, m, M2) + (nb, mb, M2b)
+__device__ __forceinline__ void chan_merge(float& n, float& m, float& M2, float nb, float mb, float M2b) {
+  const float nn = n + nb;
+  if (nn > 0.f) {
+    const float d = mb - m;
+    const float f = nb / nn;
+    m += d * f;
+    M2 += M2b + d * d * n * f;
+  }
+  n = nn;
+}
+
+// ln_stats computed by a whole wave: lane t loads tile t (t, t+64, ...), then a butterfly merge, so
+// the latency is one load round trip instead of T dependent ones.  Every lane gets the result.
+__device__ __forceinline__ void wave_ln_stats(const float* __restrict__ part, int T, int BM, int L, int C, float eps,
+                                              float& mean, float& rstd) {
+  const int lane = threadIdx.x & 63;
+  float n = 0.f, m = 0.f, M2 = 0.f;
+  for (int t = lane; t < T; t += 64) {
+    const float2 pm = *reinterpret_cast<const float2*>(part + 2 * t);
+    chan_merge(n, m, M2, (float)(min(BM, L - t * BM) * C), pm.x, pm.y);
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), M2b = __shfl_xor(M2, o, 64);
+    chan_merge(n, m, M2, nb, mb, M2b);
+  }
+  mean = m;
+  rstd = rsqrtf(M2 / n + eps);
+}
+
+// ln_bwd_consts computed by a whole wave (parallel loads + butterfly sums)
+__device__ __forceinline__ void wave_bwd_consts(const float* __restrict__ part, int T, float inv_n, float& m1,
+                                                float& m2) {
+  const int lane = threadIdx.x & 63;
+  float a = 0.f, c = 0.f;
+  for (int t = lane; t < T; t += 64) {
+    const float2 pm = *reinterpret_cast<const float2*>(part + 2 * t);
+    a += pm.x;
+    c += pm.y;
+  }
+  m1 = wave_reduce_sum(a) * inv_n;
+  m2 = wave_reduce_sum(c) * inv_n;
+}
+
+// (count, mean, M2) of one wave's values: each lane contributes cnt values with sum s and sum of
+// squared deviations from its own mean q; merged across the wave.  Returned on every lane.
+__device__ __forceinline__ void wave_chan(float& n, float& m, float& M2) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), M2b = __shfl_xor(M2, o, 64);
+    chan_merge(n, m, M2, nb, mb, M2b);
+  }
+}
+
 }  // namespace pbx

@@ -46,7 +46,7 @@ def torch_local(x, gb, blk):
     return h2, vsum
 
 
-@pytest.mark.parametrize("L,B", [(512, 3), (200, 2), (300, 2), (64, 4)])
+@pytest.mark.parametrize("L,B", [(512, 3), (200, 2), (300, 2), (64, 4), (1024, 2), (4096, 1)])
 def test_local_block_forward(L, B):
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     m, blk = make_block(L)
@@ -60,7 +60,7 @@ def test_local_block_forward(L, B):
     assert rel(vpart.sum(1), rv) < 1.5e-2
 
 
-@pytest.mark.parametrize("L,B", [(512, 2), (200, 3)])
+@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1)])
 def test_local_block_backward(L, B):
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     m, blk = make_block(L, seed=1)
