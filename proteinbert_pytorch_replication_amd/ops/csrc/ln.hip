@@ -356,52 +356,57 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Per-sample constants for the LayerNorm-2 / local-MLP backward: one wave per sample combines the
+// tile partials once (instead of every consumer workgroup doing it):
+//   c[b] = (mean2, rstd2, m1_2, m2_2, mean1, rstd1, 0, 0)
+__global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict__ st2, int T2, int BM2,
+                                                         const float* __restrict__ sums2, int TS2,
+                                                         const float* __restrict__ st1, int T1, int BM1,
+                                                         float* __restrict__ consts, int B, int L, float eps) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float mean2, rstd2, m1, m2, mean1, rstd1;
+  wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BM2, L, CH, eps, mean2, rstd2);
+  wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, 1.0f / (float)(L * CH), m1, m2);
+  wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
+  if ((threadIdx.x & 63) == 0) {
+    float4* c = reinterpret_cast<float4*>(consts + (size_t)b * 8);
+    c[0] = make_float4(mean2, rstd2, m1, m2);
+    c[1] = make_float4(mean1, rstd1, 0.f, 0.f);
+  }
+}
+
 // LayerNorm-2 backward + local MLP backward (input AND weight gradient) + LayerNorm-1 backward
-// partials + both [L, C] affine gradients, position-major (grid (ceil(L/PB), nbg), 512 threads):
+// partials + both [L, C] affine gradients:
 //   ds2 = rstd2 (dh2 g2 - m1 - xhat2 m2) ; dpre = ds2 GELU'(pre) ; dh1 = ds2 + Wl^T dpre
-//   dWl += dpre^T h1 ; dbl += sum dpre                        (MFMA, registers across samples)
-//   dg2 += dh2 xhat2 ; db2 += dh2 ; dg1 += dh1 xhat1 ; db1 += dh1   (registers across samples)
-// and the per-sample LN1 partials (sum dxhat1, sum dxhat1*xhat1) per 32 positions.  All parameter
-// gradients are added into their destinations (flat-arena .grad views) once per workgroup.
+//   dWl += dpre^T h1 ; dbl += sum dpre ; dg2 += dh2 xhat2 ; db2 += dh2 ; dg1 += dh1 xhat1 ; db1 += dh1
+// A workgroup owns a PAIR of positions (l0, l0 + 1) for a range of samples (grid (ceil(L/2), nsplit));
+// an MFMA tile row is (sample, position) = (bc + j/2, l0 + j%2), 16 samples per tile.  The [L, C]
+// affine gradients therefore accumulate in registers over every sample the workgroup sees and are
+// written once (no cross-workgroup reduction when nsplit == 1); dWl sums 32 x nsamples rows per
+// workgroup before its one atomic flush.  LN1 partials: sums1[b][pair][2].
 __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
-    const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ sums2, int TS2, const float* __restrict__ g2, const bf16_t* __restrict__ pre_l,
-    const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
-    const float* __restrict__ be1, const bf16_t* __restrict__ wl, bf16_t* __restrict__ dh1,
-    float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2, float* __restrict__ dg1,
-    float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B, int L, float eps) {
+    const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ g2,
+    const bf16_t* __restrict__ pre_l, const bf16_t* __restrict__ s1, const float* __restrict__ g1,
+    const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ consts,
+    bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
+    float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B,
+    int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
-  unsigned char* dt = smem + 32768;                                  // dpre tile bf16
-  unsigned char* ht = dt + PB * 256;                                 // h1 tile bf16
-  float* yt = reinterpret_cast<float*>(ht + PB * 256);               // [PB][128] fp32
-  float* sh = yt + PB * YS;
+  unsigned char* dt = smem + 32768;                                  // dpre tile bf16 [32][128]
+  unsigned char* ht = dt + 32 * 256;                                 // h1 tile bf16
+  float* yt = reinterpret_cast<float*>(ht + 32 * 256);               // [32][YS] fp32
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int j = tid >> 4, ch = tid & 15;
-  const int l0 = blockIdx.x * PB, l = l0 + j;
+  const int l = blockIdx.x * 2 + (j & 1);
   const bool okl = l < L;
-  const int TP = (L + PB - 1) / PB;
-  const int T2 = TP;
-  const int nbg = gridDim.y;
-  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
-  const float inv_n = 1.0f / (float)(L * CH);
-  const int nb = b1 - b0;
-  float* tab = sh;                      // [nb][8]: mean2 rstd2 m1 m2 mean1 rstd1
-  float* part = sh + 8 * nb;            // [nb][8 waves][2]: LN1 backward partial sums
+  const int TS1 = gridDim.x;
+  const int nsplit = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / nsplit), b1 = (int)((long)B * (blockIdx.y + 1) / nsplit);
   stage_weight(ws, wl, CH);
-  for (int i = w; i < nb; i += 8) {
-    const int b = b0 + i;
-    float mean2, rstd2, m1, m2, mean1, rstd1;
-    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, PB, L, CH, eps, mean2, rstd2);
-    wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, inv_n, m1, m2);
-    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
-    if (lane == 0) {
-      tab[8 * i] = mean2; tab[8 * i + 1] = rstd2; tab[8 * i + 2] = m1; tab[8 * i + 3] = m2;
-      tab[8 * i + 4] = mean1; tab[8 * i + 5] = rstd1;
-    }
-  }
   float ga2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (okl) {
     load_f8(g2 + (size_t)l * CH + ch * 8, ga2);
@@ -415,14 +420,21 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   f32x16_t aw0 = zero16(), aw1 = zero16();
   const int wco = (w >> 1) * 32, wci = (w & 1) * 64;
   const size_t coff = (size_t)l * CH + ch * 8;
-  uint4 n_dh = ldq(dh2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
-  uint4 n_s2 = ldq(s2 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
-  uint4 n_pr = ldq(pre_l + (size_t)b0 * L * CH + coff, okl && b0 < b1);
-  uint4 n_s1 = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
-  __syncthreads();
-  for (int b = b0; b < b1; ++b) {
-    const float* tb = tab + 8 * (b - b0);
-    const float mean2 = tb[0], rstd2 = tb[1], m1 = tb[2], m2 = tb[3], mean1 = tb[4], rstd1 = tb[5];
+  // prefetch the first chunk
+  int bs = b0 + (j >> 1);
+  bool ok = okl && bs < b1;
+  size_t off = (size_t)bs * L * CH + coff;
+  uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_pr = ldq(pre_l + off, ok), n_s1 = ldq(s1 + off, ok);
+  float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
+  if (bs < b1) {
+    n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
+    n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+  }
+  for (int bc = b0; bc < b1; bc += 16) {
+    const int bcur = bs;
+    const bool okc = ok;
+    const size_t offc = off;
+    const float mean2 = n_c0.x, rstd2 = n_c0.y, m1 = n_c0.z, m2 = n_c0.w, mean1 = n_c1.x, rstd1 = n_c1.y;
     float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
     unpack8(n_dh, dh);
     unpack8(n_s2, sv2);
@@ -431,12 +443,12 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xh2 = (sv2[e] - mean2) * rstd2;
-      adg2[e] += okl ? dh[e] * xh2 : 0.f;
-      adb2[e] += okl ? dh[e] : 0.f;
-      ds2[e] = okl ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
+      adg2[e] += okc ? dh[e] * xh2 : 0.f;
+      adb2[e] += okc ? dh[e] : 0.f;
+      ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
       dp[e] = ds2[e] * gelu_grad_f(pr[e]);
       xh1[e] = (sv1[e] - mean1) * rstd1;
-      hv[e] = okl ? xh1[e] * ga1[e] + bt1[e] : 0.f;
+      hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
     }
     const uint4 dq = packq8(dp);
     *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
@@ -447,16 +459,21 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) adbl[e] += dpr[e];
     }
-    const size_t off = (size_t)b * L * CH + coff;
     __syncthreads();
-    const size_t noff = (size_t)(b + 1) * L * CH + coff;
-    const bool nok = okl && b + 1 < b1;
-    n_dh = ldq(dh2 + noff, nok);
-    n_s2 = ldq(s2 + noff, nok);
-    n_pr = ldq(pre_l + noff, nok);
-    n_s1 = ldq(s1 + noff, nok);
+    // prefetch the next chunk while the MFMAs run
+    bs = bc + 16 + (j >> 1);
+    ok = okl && bs < b1;
+    off = (size_t)bs * L * CH + coff;
+    n_dh = ldq(dh2 + off, ok);
+    n_s2 = ldq(s2 + off, ok);
+    n_pr = ldq(pre_l + off, ok);
+    n_s1 = ldq(s1 + off, ok);
+    if (bs < b1) {
+      n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
+      n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+    }
     if (w < 4) {
-      // D[ci][pos] = sum_co Wl[co][ci] dpre[pos][co]: A = Wl^T (transposed LDS read), B = dpre rows
+      // D[ci][row] = sum_co Wl[co][ci] dpre[row][co]: A = Wl^T (transposed LDS read), B = dpre rows
       f32x16_t acc = zero16();
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
@@ -470,7 +487,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
         *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
             make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
-    // dWl[co][ci] += sum_pos dpre[pos][co] h1[pos][ci]   (both operands transposed LDS reads)
+    // dWl[co][ci] += sum_row dpre[row][co] h1[row][ci]   (both operands transposed LDS reads)
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int rlo = ks * 16 + 8 * h + q;
@@ -488,30 +505,27 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     float o[8], sa = 0.f, sc = 0.f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      o[e] = okl ? bfround(ds2[e] + yv[e]) : 0.f;
+      o[e] = okc ? bfround(ds2[e] + yv[e]) : 0.f;
       const float dxh = o[e] * ga1[e];
       sa += dxh;
       sc += dxh * xh1[e];
       adg1[e] += o[e] * xh1[e];
       adb1[e] += o[e];
     }
-    if (okl) *reinterpret_cast<uint4*>(dh1 + off) = packq8(o);
-    sa = wave_reduce_sum(sa);
-    sc = wave_reduce_sum(sc);
-    if (lane == 0) {
-      part[((b - b0) * 8 + w) * 2] = sa;
-      part[((b - b0) * 8 + w) * 2 + 1] = sc;
+    if (okc) *reinterpret_cast<uint4*>(dh1 + offc) = packq8(o);
+    // LN1 partial of (sample, position pair): 16 lanes per row, rows j and j+1 share the sample
+#pragma unroll
+    for (int m = 1; m <= 16; m <<= 1) {
+      sa += __shfl_xor(sa, m, 64);
+      sc += __shfl_xor(sc, m, 64);
+    }
+    if ((lane & 31) == 0 && bcur < b1) {
+      sums1[((size_t)bcur * TS1 + blockIdx.x) * 2] = sa;
+      sums1[((size_t)bcur * TS1 + blockIdx.x) * 2 + 1] = sc;
     }
   }
-  __syncthreads();
-  for (int i = tid; i < nb; i += 512) {
-    float a = 0.f, c = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 8; ++ww) { a += part[(i * 8 + ww) * 2]; c += part[(i * 8 + ww) * 2 + 1]; }
-    sums1[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = a;
-    sums1[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = c;
-  }
-  // [L, C] affine gradients: transpose through LDS so each wave-instruction adds 256 contiguous bytes
+  // [L, C] affine gradients: sum the 16 rows of each position through LDS, one add per element
+  const int l0 = blockIdx.x * 2;
   float* accs[4] = {adg2, adb2, adg1, adb1};
   float* dsts[4] = {dg2, db2, dg1, db1};
 #pragma unroll
@@ -520,11 +534,15 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = accs[a][e];
     __syncthreads();
-    for (int i = tid; i < PB * CH; i += 512) {
-      if (l0 + (i >> 7) < L) atomicAdd(dsts[a] + (size_t)l0 * CH + i, yt[i]);
+    if (tid < 2 * CH) {
+      const int par = tid >> 7, c = tid & (CH - 1);
+      float v = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) v += yt[(2 * k + par) * CH + c];
+      if (l0 + par < L) atomicAdd(dsts[a] + (size_t)(l0 + par) * CH + c, v);
     }
   }
-  // local-MLP bias: column sums over the workgroup's positions
+  // local-MLP bias: column sums over all rows
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = adbl[e];
@@ -532,7 +550,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   if (tid < CH) {
     float a = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < PB; ++k) a += yt[k * CH + tid];
+    for (int k = 0; k < 32; ++k) a += yt[k * CH + tid];
     atomicAdd(dbl + tid, a);
   }
   // local-MLP weight: D[co][ci], lane -> ci (128 contiguous bytes per half-wave)
@@ -709,20 +727,25 @@ PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, co
   return pbx_launch_status();
 }
 
-// dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics)
+// dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics).
+// consts: [B][8] fp32 workspace; sums1: [B][ceil(L/2)][2] LN1 partials (TS1 = ceil(L/2)).
 PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
-                                  int BM1, const float* g1, const float* be1, const void* wl, void* dh1,
-                                  float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
+                                  int BM1, const float* g1, const float* be1, const void* wl, float* consts,
+                                  void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, int B, int L, float eps, hipStream_t st) {
-  dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
-  const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
-  const int lds = 32768 + 2 * PB * 256 + PB * YS * 4 + nbmax * 24 * 4;
-  if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
-  hipLaunchKernelGGL(ln2_linear_bwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh2, (const bf16_t*)s2, st2,
-                     sums2, TS2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
-                     (const bf16_t*)wl, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L, eps);
+  const int T2 = (L + PB - 1) / PB;
+  hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
+                     consts, B, L, eps);
+  const int pairs = (L + 1) / 2;
+  int nsplit = (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
+  if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
+  if (nsplit < 1) nsplit = 1;
+  const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
+  hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(pairs, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
+                     (const bf16_t*)s2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
+                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L);
   return pbx_launch_status();
 }
 
