@@ -199,37 +199,40 @@ __device__ __forceinline__ f32x16_t wv_chain(const unsigned char* ws, const bf16
 }
 
 // ------------------------------------------------------------------------------------------------
-// h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in tile} GELU(h2[pos] . Wv[j])
-// NW waves (blockDim = 64 NW), tile = 32 NW positions; the MFMA chain of column block jt+1 is
-// issued before the GELU/column-sum VALU work of block jt so the two pipes overlap.
+// h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in 32-row tile t} GELU(h2[pos] . Wv[j])
+// NW waves (blockDim = 64 NW), workgroup tile = 32 NW positions; every wave owns 32 positions and
+// writes its own vpart row (no cross-wave reduction, no barrier in the tile loop).  The MFMA chain
+// of column block jt+1 is issued before the GELU/column-sum VALU work of block jt so the two pipes
+// overlap.
 __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
     float* __restrict__ vpart, int B, int L, int NJ, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // NJ rows x 256 B
-  float* red = reinterpret_cast<float*>(smem + NJ * 256);            // NJ floats
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int NW = blockDim.x >> 6, BMA = NW * 32;
   const int T2 = (L + BML - 1) / BML;
   const int TA = (L + BMA - 1) / BMA;
+  const int TW = (L + 31) / 32;
   const int NJT = NJ / 32;
   stage_weight(ws, wv, NJ);
   __syncthreads();
   for (int tile = blockIdx.x; tile < B * TA; tile += gridDim.x) {
     const int b = tile / TA, t = tile - (tile / TA) * TA;
-    const int pos0 = t * BMA;
+    const int tw = t * NW + w;                  // this wave's 32-position row of vpart
+    if (tw >= TW) continue;                     // (no barrier below: waves are independent)
+    const int pos0 = tw * 32;
     float mean, rstd;
     wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    for (int j = tid; j < NJ; j += blockDim.x) red[j] = 0.f;
-    const int pos = pos0 + w * 32 + r;
+    const int pos = pos0 + r;
     const bool okb = pos < L;
     const size_t rowoff = ((size_t)b * L + pos) * CH;
     bf16x8 hf[8];
     ln_row_frags(hf, s2 + rowoff, g2 + (size_t)pos * CH, be2 + (size_t)pos * CH, mean, rstd, okb, h, h2 + rowoff);
-    __syncthreads();   // red zeroed
-    const int rowbase = pos0 + w * 32 + 4 * h;
+    const int rowbase = pos0 + 4 * h;
+    float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
     auto colsum = [&](const f32x16_t& acc, int jt) {
       float sacc = 0.f;
 #pragma unroll
@@ -238,7 +241,7 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
         sacc += prow < L ? gelu_f(acc[i]) : 0.f;
       }
       sacc += __shfl_xor(sacc, 32, 64);
-      if (h == 0) atomicAdd(&red[jt * 32 + r], sacc);
+      if (h == 0) vrow[jt * 32 + r] = sacc;
     };
     f32x16_t a0 = wv_chain<true>(ws, hf, 0, r, h);
     for (int jt = 0; jt < NJT; jt += 2) {
@@ -247,9 +250,6 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
       if (jt + 2 < NJT) a0 = wv_chain<true>(ws, hf, jt + 2, r, h);
       colsum(a1, jt + 1);
     }
-    __syncthreads();
-    for (int j = tid; j < NJ; j += blockDim.x) vpart[((size_t)b * TA + t) * NJ + j] = red[j];
-    __syncthreads();
   }
 }
 
@@ -266,6 +266,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;
   float* scratch = reinterpret_cast<float*>(smem + NJ * 256);
+  float* dvs = scratch + 32;                                         // [NW][NJ] dv rows of the tile
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
@@ -292,7 +293,15 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
     f32x16_t y[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    const float* dv = dvpart + ((size_t)b * TV + (okb ? pos / BMV : 0)) * NJ;
+    // stage each wave's dv row (its 32 positions lie in one forward tile) into LDS
+    for (int idx = tid; idx < NW * (NJ / 4); idx += blockDim.x) {
+      const int ww = idx / (NJ / 4), c4 = idx - ww * (NJ / 4);
+      const int pw = min(pos0 + ww * 32, L - 1);
+      *reinterpret_cast<float4*>(dvs + ww * NJ + c4 * 4) =
+          *reinterpret_cast<const float4*>(dvpart + ((size_t)b * TV + pw / BMV) * NJ + c4 * 4);
+    }
+    __syncthreads();
+    const float* dv = dvs + w * NJ;
     auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
 #pragma unroll
@@ -703,13 +712,13 @@ PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int B
   return pbx_launch_status();
 }
 
-// nw: waves per workgroup (tile = 32 nw positions); vpart is [B][ceil(L / (32 nw))][NJ]
+// nw: waves per workgroup (tile = 32 nw positions); vpart is [B][ceil(L / 32)][NJ] (one row per wave tile)
 PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
                                void* h2, float* vpart, int B, int L, int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
   if (NJ % 64 != 0 || NJ * 256 + NJ * 4 > 163840 || nw < 1 || nw > 16) return (int)hipErrorInvalidValue;
   const int TA = (L + 32 * nw - 1) / (32 * nw);
-  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + NJ * 4, st,
+  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256, st,
                      (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, B, L, NJ, eps);
   return pbx_launch_status();
 }
@@ -719,9 +728,9 @@ PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, co
                             const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
                             int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + 128 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  if (NJ % 64 != 0 || NJ * 256 + 128 + nw * NJ * 4 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
   const int TA = (L + 32 * nw - 1) / (32 * nw);
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + 128, st,
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + 128 + nw * NJ * 4, st,
                      (const bf16_t*)h2, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
                      (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ, eps);
   return pbx_launch_status();
