@@ -47,11 +47,13 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
   const int XR = BM + 2 * halo;
   unsigned char* xs = smem;
   unsigned char* wb = smem + XR * 256;
+  float* bsm = reinterpret_cast<float*>(wb + 65536);      // bn | bw | gb[b]  (3 x 128 fp32)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   constexpr int WM = BM / 64, WN = 8 / WM, CT = 4 / WN;   // BM=256: 4x2 waves, BM=128: 2x4 waves
   const int wm = w / WN, wn = w % WN;
   const bf16_t* xsmp = x + (size_t)b * L * CH;
+  if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
 
   for (int idx = tid; idx < XR * 16; idx += 512) {
     const int j = idx >> 4, ch = idx & 15;
@@ -131,7 +133,42 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
   }
 
   // ---- epilogue: bias, GELU x2, residual, broadcast, LN partials --------------------------------
+  // Outputs are staged through the (now free) weight buffer as a swizzled [BM][128] bf16 tile and
+  // written with 16-B-per-lane row-contiguous stores; biases / broadcast vector come from LDS.
   const int vrows = min(BM, L - pos0);
+  unsigned char* ot = wb;                       // BM x 256 B output staging tile
+  auto copy_out = [&](bf16_t* __restrict__ dst) {
+    __syncthreads();                            // tile complete
+    for (int idx = tid; idx < BM * 16; idx += 512) {
+      const int row = idx >> 4, c = idx & 15;
+      if (row < vrows)
+        *reinterpret_cast<uint4*>(dst + ((size_t)b * L + pos0 + row) * CH + c * 8) =
+            *reinterpret_cast<const uint4*>(ot + swz256(row, c));
+    }
+    __syncthreads();                            // tile drained before it is rewritten
+  };
+  // pre_n, pre_w = accumulators + bias (bf16)
+#pragma unroll
+  for (int cv = 0; cv < 2; ++cv) {
+    const float* bias = bsm + cv * CH;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct)
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int ch0 = wn * CT * 32 + ct * 32 + 8 * g + 4 * h;
+          const int p = wm * 64 + pt * 32 + r;
+          const float4 bv = *reinterpret_cast<const float4*>(bias + ch0);
+          const float ba[4] = {bv.x, bv.y, bv.z, bv.w};
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = (cv == 0 ? an : aw)[ct][pt][4 * g + e] + ba[e];
+          *reinterpret_cast<uint2*>(ot + swz256e(p, ch0)) = packq4(v);
+        }
+    copy_out(cv == 0 ? pre_n : pre_w);
+  }
+  // s1 = x + GELU(pre_n) + GELU(pre_w) + gb  (kept in an[] for the LN partials)
   float lsum = 0.f;
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
@@ -142,51 +179,56 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
         const int ch0 = wn * CT * 32 + ct * 32 + 8 * g + 4 * h;
         const int p = wm * 64 + pt * 32 + r;
         const bool ok = p < vrows;
-        float xv[4], vn[4], vw[4], o[4];
+        float xv[4], o[4];
         unpack4(*reinterpret_cast<const uint2*>(xs + swz256e(halo + p, ch0)), xv);
-        const float4 bnv = *reinterpret_cast<const float4*>(bn + ch0);
-        const float4 bwv = *reinterpret_cast<const float4*>(bw + ch0);
-        const float4 gbv = *reinterpret_cast<const float4*>(gb + (size_t)b * CH + ch0);
+        const float4 bnv = *reinterpret_cast<const float4*>(bsm + ch0);
+        const float4 bwv = *reinterpret_cast<const float4*>(bsm + CH + ch0);
+        const float4 gbv = *reinterpret_cast<const float4*>(bsm + 2 * CH + ch0);
         const float bna[4] = {bnv.x, bnv.y, bnv.z, bnv.w};
         const float bwa[4] = {bwv.x, bwv.y, bwv.z, bwv.w};
         const float gba[4] = {gbv.x, gbv.y, gbv.z, gbv.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          vn[e] = an[ct][pt][4 * g + e] + bna[e];
-          vw[e] = aw[ct][pt][4 * g + e] + bwa[e];
-          o[e] = bfround(xv[e] + gelu_f(vn[e]) + gelu_f(vw[e]) + gba[e]);
-        }
-        if (ok) {
-          const size_t off = ((size_t)b * L + pos0 + p) * CH + ch0;
-          *reinterpret_cast<uint2*>(pre_n + off) = packq4(vn);
-          *reinterpret_cast<uint2*>(pre_w + off) = packq4(vw);
-          *reinterpret_cast<uint2*>(s1 + off) = packq4(o);
-        }
+        for (int e = 0; e < 4; ++e)
+          o[e] = bfround(xv[e] + gelu_f(an[ct][pt][4 * g + e] + bna[e]) + gelu_f(aw[ct][pt][4 * g + e] + bwa[e]) +
+                         gba[e]);
+        *reinterpret_cast<uint2*>(ot + swz256e(p, ch0)) = packq4(o);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           an[ct][pt][4 * g + e] = ok ? o[e] : 0.f;
           lsum += ok ? o[e] : 0.f;
         }
       }
-  float* scratch = reinterpret_cast<float*>(wb);
-  const float cnt = (float)(vrows * CH);
-  const float mean = block_sum(lsum, scratch, 8) / cnt;
-  float m2 = 0.f;
+  copy_out(s1);
+  // LN partial (mean, M2) of the tile: per-lane -> wave (Chan merge) -> 8 wave partials in LDS
+  float n = 0.f, m = 0.f, M2 = 0.f;
+  {
+    int cnt = 0;
 #pragma unroll
-  for (int ct = 0; ct < CT; ++ct)
+    for (int pt = 0; pt < 2; ++pt) cnt += (wm * 64 + pt * 32 + r) < vrows ? CT * 16 : 0;
+    n = (float)cnt;
+    m = cnt > 0 ? lsum / n : 0.f;
 #pragma unroll
-    for (int pt = 0; pt < 2; ++pt) {
-      const bool ok = (wm * 64 + pt * 32 + r) < vrows;
+    for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float d = an[ct][pt][i] - mean;
-        m2 += ok ? d * d : 0.f;
+      for (int pt = 0; pt < 2; ++pt) {
+        const bool ok = (wm * 64 + pt * 32 + r) < vrows;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float d = an[ct][pt][i] - m;
+          M2 += ok ? d * d : 0.f;
+        }
       }
-    }
-  m2 = block_sum(m2, scratch + 8, 8);
+  }
+  wave_chan(n, m, M2);
+  float* scratch = reinterpret_cast<float*>(wb);
+  if (lane == 0) { scratch[3 * w] = n; scratch[3 * w + 1] = m; scratch[3 * w + 2] = M2; }
+  __syncthreads();
   if (tid == 0) {
-    stats[((size_t)b * T + t) * 2] = mean;
-    stats[((size_t)b * T + t) * 2 + 1] = m2;
+    float tn = 0.f, tm = 0.f, tM2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) chan_merge(tn, tm, tM2, scratch[3 * i], scratch[3 * i + 1], scratch[3 * i + 2]);
+    stats[((size_t)b * T + t) * 2] = tm;
+    stats[((size_t)b * T + t) * 2 + 1] = tM2;
   }
 }
 
@@ -286,24 +328,37 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
     }
   }
 
+  // epilogue: dx = ds1 + D^T.  The fp32 accumulators are staged through LDS (the x / weight buffers
+  // are free: [BM][128] fp32, 16-B chunks XOR-swizzled by row so the 32 rows a half-wave writes hit
+  // distinct banks), then combined with row-contiguous 16-B loads of ds1 and 16-B stores of dx.
   const int vrows = min(BM, L - pos0);
+  float* ft = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int ct = 0; ct < CT; ++ct)
 #pragma unroll
     for (int pt = 0; pt < 2; ++pt) {
       const int p = wm * 64 + pt * 32 + r;
-      if (p >= vrows) continue;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int ci0 = wn * CT * 32 + ct * 32 + 8 * g + 4 * h;
-        const size_t off = sbase + (size_t)(pos0 + p) * CH + ci0;
-        float gv[4], o[4];
-        unpack4(*reinterpret_cast<const uint2*>(ds1 + off), gv);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = gv[e] + acc[ct][pt][4 * g + e];
-        *reinterpret_cast<uint2*>(dx + off) = packq4(o);
+        const int c4 = (wn * CT * 32 + ct * 32 + 8 * g + 4 * h) >> 2;
+        *reinterpret_cast<float4*>(ft + p * CH + ((c4 ^ (p & 31)) << 2)) =
+            make_float4(acc[ct][pt][4 * g], acc[ct][pt][4 * g + 1], acc[ct][pt][4 * g + 2], acc[ct][pt][4 * g + 3]);
       }
     }
+  __syncthreads();
+  for (int idx = tid; idx < BM * 16; idx += 512) {
+    const int row = idx >> 4, c = idx & 15;
+    if (row >= vrows) continue;
+    const size_t off = sbase + (size_t)(pos0 + row) * CH + c * 8;
+    float gv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
+    const float4 f0 = *reinterpret_cast<const float4*>(ft + row * CH + (((2 * c) ^ (row & 31)) << 2));
+    const float4 f1 = *reinterpret_cast<const float4*>(ft + row * CH + (((2 * c + 1) ^ (row & 31)) << 2));
+    const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
+    *reinterpret_cast<uint4*>(dx + off) = packq8(o);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -447,7 +502,7 @@ int launch_fwd(const void* x, const void* wpn, const void* wpw, const float* bn,
                const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS, int dil,
                hipStream_t st) {
   const int T = (L + BM - 1) / BM;
-  const int lds = (BM + 2 * (KS / 2) * dil) * 256 + 65536;
+  const int lds = (BM + 2 * (KS / 2) * dil) * 256 + 65536 + 3 * CH * 4;
   if (lds > 163840) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(conv_fwd_kernel<BM>, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16_t*)wpn,
                      (const bf16_t*)wpw, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
