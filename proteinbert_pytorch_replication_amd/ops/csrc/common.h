@@ -45,6 +45,36 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x, p, c);
 }
 
+// Packed (2-wide) versions on v_pk_fma_f32 / v_pk_mul_f32: the polynomial, the squares and the
+// final products run two lanes' values per instruction; rcp / exp2 stay scalar (transcendental).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_parts2(f32x2 x, f32x2& cdf, f32x2& pdf) {
+  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+  const f32x2 den = z * 0.3275911f + 1.0f;
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 pl = __builtin_elementwise_fma(t, (f32x2){1.061405429f, 1.061405429f}, (f32x2){-1.453152027f, -1.453152027f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){1.421413741f, 1.421413741f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.284496736f, -0.284496736f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){0.254829592f, 0.254829592f});
+  pl = pl * t;
+  const f32x2 q = (z * z) * -1.4426950408889634f;          // -z^2 log2(e)
+  const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 erfz = __builtin_elementwise_fma(-pl, e, (f32x2){1.0f, 1.0f});
+  const f32x2 se = {copysignf(erfz.x, x.x), copysignf(erfz.y, x.y)};
+  cdf = __builtin_elementwise_fma(se, (f32x2){0.5f, 0.5f}, (f32x2){0.5f, 0.5f});
+  pdf = e * 0.3989422804014327f;
+}
+__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
+  f32x2 c, p;
+  gelu_parts2(x, c, p);
+  return x * c;
+}
+__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
+  f32x2 c, p;
+  gelu_parts2(x, c, p);
+  return __builtin_elementwise_fma(x, p, c);
+}
+
 __device__ __forceinline__ float wave_reduce_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

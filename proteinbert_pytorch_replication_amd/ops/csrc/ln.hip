@@ -233,13 +233,20 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
     ln_row_frags(hf, s2 + rowoff, g2 + (size_t)pos * CH, be2 + (size_t)pos * CH, mean, rstd, okb, h, h2 + rowoff);
     const int rowbase = pos0 + 4 * h;
     float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
+    const bool full = pos0 + 32 <= L;
     auto colsum = [&](const f32x16_t& acc, int jt) {
-      float sacc = 0.f;
+      f32x2 s2v = {0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int prow = rowbase + (i & 3) + 8 * (i >> 2);
-        sacc += prow < L ? gelu_f(acc[i]) : 0.f;
+      for (int i = 0; i < 16; i += 2) {
+        f32x2 gv = gelu2((f32x2){acc[i], acc[i + 1]});
+        if (!full) {
+          const int prow = rowbase + (i & 3) + 8 * (i >> 2);
+          gv.x = prow < L ? gv.x : 0.f;
+          gv.y = prow + 1 < L ? gv.y : 0.f;
+        }
+        s2v += gv;
       }
+      float sacc = s2v.x + s2v.y;
       sacc += __shfl_xor(sacc, 32, 64);
       if (h == 0) vrow[jt * 32 + r] = sacc;
     };
@@ -257,7 +264,9 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
 // attention pool backward + LayerNorm-2 backward partials.
 // dP[j][pos] = dv[b][t][j] * GELU'(Wv[j] . h2[pos]) ; dh2 = dh2_in + Wv^T dP  (dP never leaves
 // registers: the 32x32 accumulator of the recompute is the B operand of the second MFMA).
-// NW waves, tile = 32 NW positions (sums2 partials per tile); dv rows are per ln_attn_fwd tile.
+// Work items are 32-position wave tiles taken by each wave independently (no workgroup barrier
+// after the Wv staging, so the waves of a CU drift apart and one wave's loads overlap another's
+// MFMAs), and the LN2 partials are written per wave tile: sums2[b][ceil(L/32)][2].
 __global__ void __launch_bounds__(512) attn_bwd_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
@@ -265,43 +274,43 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
     float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;
-  float* scratch = reinterpret_cast<float*>(smem + NJ * 256);
-  float* dvs = scratch + 32;                                         // [NW][NJ] dv rows of the tile
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
-  const int NW = blockDim.x >> 6, BMA = NW * 32;
+  const int NW = blockDim.x >> 6;
   const int T2 = (L + BML - 1) / BML;
-  const int TA = (L + BMA - 1) / BMA;
+  const int TW = (L + 31) / 32;
   const int TV = (L + BMV - 1) / BMV;
   const int NJT = NJ / 32;
+  const long items = (long)B * TW;
+  const long stride = (long)gridDim.x * NW;
   stage_weight(ws, wv, NJ);
   __syncthreads();
-  for (int tile = blockIdx.x; tile < B * TA; tile += gridDim.x) {
-    const int b = tile / TA, t = tile - (tile / TA) * TA;
-    const int pos0 = t * BMA;
-    const int pos = pos0 + w * 32 + r;
-    const bool okb = pos < L;
-    const size_t rowoff = ((size_t)b * L + pos) * CH;
-    bf16x8 hf[8];
+  auto load_rows = [&](long item, bf16x8* f) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos = tw * 32 + r;
+    const bool ok = item < items && pos < L;
+    const bf16_t* src = h2 + ((size_t)b * L + pos) * CH;
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (okb) v = *reinterpret_cast<const uint4*>(h2 + rowoff + kk * 16 + 8 * h);
-      hf[kk] = __builtin_bit_cast(bf16x8, v);
+      if (ok) v = *reinterpret_cast<const uint4*>(src + kk * 16 + 8 * h);
+      f[kk] = __builtin_bit_cast(bf16x8, v);
     }
+  };
+  for (long item = (long)blockIdx.x * NW + w; item < items; item += stride) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos0 = tw * 32;
+    const int pos = pos0 + r;
+    const bool okb = pos < L;
+    const size_t rowoff = ((size_t)b * L + pos) * CH;
+    bf16x8 hf[8];
+    load_rows(item, hf);
     f32x16_t y[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    // stage each wave's dv row (its 32 positions lie in one forward tile) into LDS
-    for (int idx = tid; idx < NW * (NJ / 4); idx += blockDim.x) {
-      const int ww = idx / (NJ / 4), c4 = idx - ww * (NJ / 4);
-      const int pw = min(pos0 + ww * 32, L - 1);
-      *reinterpret_cast<float4*>(dvs + ww * NJ + c4 * 4) =
-          *reinterpret_cast<const float4*>(dvpart + ((size_t)b * TV + pw / BMV) * NJ + c4 * 4);
-    }
-    __syncthreads();
-    const float* dv = dvs + w * NJ;
+    const float* dv = dvpart + ((size_t)b * TV + pos0 / BMV) * NJ;
+    const bool full = pos0 + 32 <= L;
     auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
 #pragma unroll
@@ -309,7 +318,15 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
         float dvv[4];
         load_f4(dv + jt * 32 + 8 * g + 4 * h, dvv);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) dp[4 * g + e] = okb ? dvv[e] * gelu_grad_f(d1[4 * g + e]) : 0.f;
+        for (int e = 0; e < 4; e += 2) {
+          const f32x2 gg = gelu_grad2((f32x2){d1[4 * g + e], d1[4 * g + e + 1]}) * (f32x2){dvv[e], dvv[e + 1]};
+          dp[4 * g + e] = gg.x;
+          dp[4 * g + e + 1] = gg.y;
+        }
+      }
+      if (!full) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dp[i] = okb ? dp[i] : 0.f;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -330,7 +347,7 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
       if (jt + 2 < NJT) d0 = wv_chain<false>(ws, hf, jt + 2, r, h);
       proc(d1, jt + 1);
     }
-    // Y[ci][pos]; LN2 backward partials
+    // Y[ci][pos]; LN2 backward partials of this wave tile
     float mean, rstd;
     wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
     float sa = 0.f, sc = 0.f;
@@ -355,11 +372,11 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
           *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
         }
     }
-    sa = block_sum(sa, scratch, NW);
-    sc = block_sum(sc, scratch + 16, NW);
-    if (tid == 0) {
-      sums2[((size_t)b * TA + t) * 2] = sa;
-      sums2[((size_t)b * TA + t) * 2 + 1] = sc;
+    sa = wave_reduce_sum(sa);
+    sc = wave_reduce_sum(sc);
+    if (lane == 0) {
+      sums2[((size_t)b * TW + tw) * 2] = sa;
+      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
     }
   }
 }
@@ -723,16 +740,19 @@ PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2
   return pbx_launch_status();
 }
 
-// dvpart rows follow the forward tiling (bmv positions); sums2 is [B][ceil(L / (32 nw))][2]
+// dvpart rows follow the forward tiling (bmv positions, a multiple of 32); sums2 is [B][ceil(L / 32)][2]
 PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
                             const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
                             int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + 128 + nw * NJ * 4 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
-  const int TA = (L + 32 * nw - 1) / (32 * nw);
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256 + 128 + nw * NJ * 4, st,
-                     (const bf16_t*)h2, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
-                     (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ, eps);
+  if (NJ % 64 != 0 || NJ * 256 > 163840 || nw < 1 || nw > 8 || bmv % 32 != 0) return (int)hipErrorInvalidValue;
+  const long items = (long)B * ((L + 31) / 32);
+  long wgl = (items + nw - 1) / nw;
+  if (wgl > num_cus()) wgl = num_cus();
+  const int wgs = (int)wgl;
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(wgs), dim3(64 * nw), NJ * 256, st, (const bf16_t*)h2, (const bf16_t*)s2,
+                     st2, g2, (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ,
+                     eps);
   return pbx_launch_status();
 }
 

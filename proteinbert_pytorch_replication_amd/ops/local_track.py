@@ -55,7 +55,8 @@ def attn_fwd_waves(L: int) -> int:
 
 
 def attn_bwd_waves(L: int) -> int:
-    return max(4, min(8, (L + 31) // 32))
+    """attn_bwd workgroup: 8 independent waves (work items are 32-position wave tiles)."""
+    return 8
 
 
 def _p(t: Optional[torch.Tensor]):
@@ -157,11 +158,11 @@ class LocalBlockFn(torch.autograd.Function):
         if dvpart.dim() == 3 and dvpart.stride(1) == 0:
             # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
             dvpart = dvpart[:, 0, :].float().contiguous()
-            BMV = L
+            BMV = (L + 31) // 32 * 32
         dvpart = dvpart.float().contiguous()
         # attention pool + LN2 partials
         nwb = attn_bwd_waves(L)
-        TA = (L + 32 * nwb - 1) // (32 * nwb)
+        TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_attn_bwd", h2.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
