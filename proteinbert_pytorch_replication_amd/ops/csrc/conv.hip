@@ -55,13 +55,14 @@ __global__ void __launch_bounds__(512) conv_fwd_kernel(
   const bf16_t* xsmp = x + (size_t)b * L * CH;
   if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
 
-  for (int idx = tid; idx < XR * 16; idx += 512) {
-    const int j = idx >> 4, ch = idx & 15;
-    const int pos = pos0 - halo + j;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (pos >= 0 && pos < L) v = *reinterpret_cast<const uint4*>(xsmp + (size_t)pos * CH + ch * 8);
-    *reinterpret_cast<uint4*>(xs + swz256(j, ch)) = v;
-  }
+  stage_chunks(
+      XR * 16,
+      [&](int idx) {
+        const int pos = pos0 - halo + (idx >> 4);
+        return (pos >= 0 && pos < L) ? *reinterpret_cast<const uint4*>(xsmp + (size_t)pos * CH + (idx & 15) * 8)
+                                     : make_uint4(0u, 0u, 0u, 0u);
+      },
+      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
 
   f32x16_t an[CT][2], aw[CT][2];
 #pragma unroll
@@ -278,21 +279,38 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
     uint4 w0 = *wptr(0, 0), w1 = *wptr(1, 0), w2 = *wptr(2, 0), w3 = *wptr(3, 0);
     // stage dpre = dS1 * GELU'(pre) with halo; central rows also go to global for the wgrad
     const int AR = BM + 2 * halo;
-    for (int idx = tid; idx < AR * 16; idx += 512) {
-      const int j = idx >> 4, ch = idx & 15;
-      const int pos = pos0 - halo + j;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (pos >= 0 && pos < L) {
-        const size_t off = sbase + (size_t)pos * CH + ch * 8;
-        float g[8], p[8], o[8];
-        unpack8(*reinterpret_cast<const uint4*>(ds1 + off), g);
-        unpack8(*reinterpret_cast<const uint4*>(pre + off), p);
+    const int nch = AR * 16;
+    for (int base = tid; base < nch; base += 4 * 512) {   // 4 chunk pairs in flight per thread
+      uint4 gq[4], pq[4];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = g[e] * gelu_grad_f(p[e]);
-        v = packq8(o);
-        if (j >= halo && j < halo + BM) *reinterpret_cast<uint4*>(dpo + off) = v;
+      for (int i = 0; i < 4; ++i) {
+        const int idx = base + i * 512;
+        const int pos = pos0 - halo + (idx >> 4);
+        const bool ok = idx < nch && pos >= 0 && pos < L;
+        const size_t off = sbase + (size_t)pos * CH + (idx & 15) * 8;
+        gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
+        pq[i] = ok ? *reinterpret_cast<const uint4*>(pre + off) : make_uint4(0u, 0u, 0u, 0u);
       }
-      *reinterpret_cast<uint4*>(as + swz256(j, ch)) = v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = base + i * 512;
+        if (idx >= nch) break;
+        const int j = idx >> 4, ch = idx & 15;
+        const int pos = pos0 - halo + j;
+        float g[8], pv[8], o[8];
+        unpack8(gq[i], g);
+        unpack8(pq[i], pv);
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 d = gelu_grad2((f32x2){pv[e], pv[e + 1]}) * (f32x2){g[e], g[e + 1]};
+          o[e] = d.x;
+          o[e + 1] = d.y;
+        }
+        const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
+        if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
+          *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
+        *reinterpret_cast<uint4*>(as + swz256(j, ch)) = v;
+      }
     }
     *reinterpret_cast<uint4*>(wb + wdst(0)) = w0;
     *reinterpret_cast<uint4*>(wb + wdst(1)) = w1;
@@ -396,21 +414,25 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
     const int pos0 = t * BM;
     const size_t sbase = (size_t)b * L * CH;
     __syncthreads();
-    for (int idx = tid; idx < BM * 4; idx += 256) {
-      const int j = idx >> 2, ch = idx & 3;
-      const int pos = pos0 + j;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (pos < L) v = *reinterpret_cast<const uint4*>(dy + sbase + (size_t)pos * CH + cg * 32 + ch * 8);
-      *reinterpret_cast<uint4*>(dys + j * 64 + ch * 16) = v;
-    }
     const int XR = BM + 2 * halo;
-    for (int idx = tid; idx < XR * 16; idx += 256) {
-      const int j = idx >> 4, ch = idx & 15;
-      const int pos = pos0 - halo + j;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (pos >= 0 && pos < L) v = *reinterpret_cast<const uint4*>(x + sbase + (size_t)pos * CH + ch * 8);
-      *reinterpret_cast<uint4*>(xs + swz256(j, ch)) = v;
-    }
+    // one batched pass: chunks [0, BM*4) are the dy tile (64-B rows), the rest the x tile (with halo)
+    stage_chunks(
+        BM * 4 + XR * 16,
+        [&](int idx) {
+          if (idx < BM * 4) {
+            const int pos = pos0 + (idx >> 2);
+            return pos < L ? *reinterpret_cast<const uint4*>(dy + sbase + (size_t)pos * CH + cg * 32 + (idx & 3) * 8)
+                           : make_uint4(0u, 0u, 0u, 0u);
+          }
+          const int i2 = idx - BM * 4;
+          const int pos = pos0 - halo + (i2 >> 4);
+          return (pos >= 0 && pos < L) ? *reinterpret_cast<const uint4*>(x + sbase + (size_t)pos * CH + (i2 & 15) * 8)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+        },
+        [&](int idx, uint4 v) {
+          if (idx < BM * 4) *reinterpret_cast<uint4*>(dys + (idx >> 2) * 64 + (idx & 3) * 16) = v;
+          else { const int i2 = idx - BM * 4; *reinterpret_cast<uint4*>(xs + swz256(i2 >> 4, i2 & 15)) = v; }
+        });
     __syncthreads();
 #pragma unroll 2
     for (int kk = 0; kk < BM / 16; ++kk) {

@@ -12,6 +12,7 @@
 // Tiles are 128 positions of one sequence; a workgroup (4 waves, 32 positions each) is persistent
 // over tiles so the weight matrix it needs is staged into LDS once.
 #include "mfma.h"
+#include <stdlib.h>
 
 using namespace pbx;
 typedef unsigned short bf16_t;
@@ -32,29 +33,40 @@ __device__ __forceinline__ void load_f4(const float* p, float* v) {
 
 // stage a [rows x 128] bf16 weight matrix into a swz256 LDS image (whole workgroup)
 __device__ __forceinline__ void stage_weight(unsigned char* dst, const bf16_t* __restrict__ w, int rows) {
-  for (int idx = threadIdx.x; idx < rows * 16; idx += blockDim.x) {
-    const int row = idx >> 4, ch = idx & 15;
-    *reinterpret_cast<uint4*>(dst + swz256(row, ch)) =
-        *reinterpret_cast<const uint4*>(w + (size_t)row * CH + ch * 8);
-  }
+  stage_chunks(
+      rows * 16, [&](int idx) { return *reinterpret_cast<const uint4*>(w + (size_t)idx * 8); },
+      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(dst + swz256(idx >> 4, idx & 15)) = v; });
 }
 
 // LN-normalised B/A fragment of one position row: 8 x (8 channels kk*16 + 8h .. +8)
+// The caller passes in-bounds pointers (rows clamped); `ok` only masks the values, so every load is
+// unconditional and all 24 of them are in flight together (a load under a divergent branch costs
+// one exposed memory round trip per branch).
 __device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict__ src, const float* __restrict__ gam,
                                              const float* __restrict__ bet, float mean, float rstd, bool ok,
                                              int h, bf16_t* __restrict__ out) {
+  uint4 sq[8];
+  float4 ga[8][2], ba[8][2];
 #pragma unroll
   for (int kk = 0; kk < 8; ++kk) {
     const int ci = kk * 16 + 8 * h;
-    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (ok) {
-      float sv[8], g[8], be[8];
-      unpack8(*reinterpret_cast<const uint4*>(src + ci), sv);
-      load_f8(gam + ci, g);
-      load_f8(bet + ci, be);
+    sq[kk] = *reinterpret_cast<const uint4*>(src + ci);
+    ga[kk][0] = *reinterpret_cast<const float4*>(gam + ci);
+    ga[kk][1] = *reinterpret_cast<const float4*>(gam + ci + 4);
+    ba[kk][0] = *reinterpret_cast<const float4*>(bet + ci);
+    ba[kk][1] = *reinterpret_cast<const float4*>(bet + ci + 4);
+  }
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (sv[e] - mean) * rstd * g[e] + be[e];
-    }
+  for (int kk = 0; kk < 8; ++kk) {
+    const int ci = kk * 16 + 8 * h;
+    float sv[8], v[8];
+    unpack8(sq[kk], sv);
+    const float g[8] = {ga[kk][0].x, ga[kk][0].y, ga[kk][0].z, ga[kk][0].w,
+                        ga[kk][1].x, ga[kk][1].y, ga[kk][1].z, ga[kk][1].w};
+    const float be[8] = {ba[kk][0].x, ba[kk][0].y, ba[kk][0].z, ba[kk][0].w,
+                         ba[kk][1].x, ba[kk][1].y, ba[kk][1].z, ba[kk][1].w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ok ? (sv[e] - mean) * rstd * g[e] + be[e] : 0.f;
     const uint4 q = packq8(v);
     if (ok && out != nullptr) *reinterpret_cast<uint4*>(out + ci) = q;
     f[kk] = __builtin_bit_cast(bf16x8, q);
@@ -199,12 +211,13 @@ __device__ __forceinline__ f32x16_t wv_chain(const unsigned char* ws, const bf16
 }
 
 // ------------------------------------------------------------------------------------------------
-// h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in 32-row tile t} GELU(h2[pos] . Wv[j])
-// NW waves (blockDim = 64 NW), workgroup tile = 32 NW positions; every wave owns 32 positions and
-// writes its own vpart row (no cross-wave reduction, no barrier in the tile loop).  The MFMA chain
-// of column block jt+1 is issued before the GELU/column-sum VALU work of block jt so the two pipes
-// overlap.
-__global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
+// h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in 64-row tile t} GELU(h2[pos] . Wv[j])
+// Work item = 64 positions of one sample, owned by one wave (waves are independent: no barrier after
+// the Wv staging).  Each Wv fragment read from LDS feeds two MFMAs (the wave's two 32-row position
+// tiles), the two accumulator chains are interleaved, and the 8 Wv fragments of column block jt+1
+// are loaded while block jt runs, so neither LDS latency nor MFMA dependency stalls the wave; the
+// packed-fp32 GELU / column sums of block jt-1 fill the MFMA shadow.
+__global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
     float* __restrict__ vpart, int B, int L, int NJ, float eps) {
@@ -212,51 +225,67 @@ __global__ void __launch_bounds__(1024) ln_attn_fwd_kernel(
   unsigned char* ws = smem;                                          // NJ rows x 256 B
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
-  const int NW = blockDim.x >> 6, BMA = NW * 32;
+  const int NW = blockDim.x >> 6;
   const int T2 = (L + BML - 1) / BML;
-  const int TA = (L + BMA - 1) / BMA;
-  const int TW = (L + 31) / 32;
+  const int TW = (L + 63) / 64;
   const int NJT = NJ / 32;
+  const long items = (long)B * TW;
   stage_weight(ws, wv, NJ);
   __syncthreads();
-  for (int tile = blockIdx.x; tile < B * TA; tile += gridDim.x) {
-    const int b = tile / TA, t = tile - (tile / TA) * TA;
-    const int tw = t * NW + w;                  // this wave's 32-position row of vpart
-    if (tw >= TW) continue;                     // (no barrier below: waves are independent)
-    const int pos0 = tw * 32;
+  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos0 = tw * 64;
     float mean, rstd;
     wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    const int pos = pos0 + r;
-    const bool okb = pos < L;
-    const size_t rowoff = ((size_t)b * L + pos) * CH;
-    bf16x8 hf[8];
-    ln_row_frags(hf, s2 + rowoff, g2 + (size_t)pos * CH, be2 + (size_t)pos * CH, mean, rstd, okb, h, h2 + rowoff);
-    const int rowbase = pos0 + 4 * h;
+    bf16x8 hf0[8], hf1[8];
+    {
+      const int pa = pos0 + r, pb = pos0 + 32 + r;
+      const int ca = min(pa, L - 1), cb = min(pb, L - 1);          // clamped: loads stay in bounds
+      const size_t ra = ((size_t)b * L + ca) * CH, rb = ((size_t)b * L + cb) * CH;
+      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
+      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
+    }
     float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
-    const bool full = pos0 + 32 <= L;
-    auto colsum = [&](const f32x16_t& acc, int jt) {
-      f32x2 s2v = {0.f, 0.f};
+    const bool full = pos0 + 64 <= L;
+    auto colsum = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
+      f32x2 sv = {0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 16; i += 2) {
-        f32x2 gv = gelu2((f32x2){acc[i], acc[i + 1]});
+        f32x2 g0 = gelu2((f32x2){c0[i], c0[i + 1]});
+        f32x2 g1 = gelu2((f32x2){c1[i], c1[i + 1]});
         if (!full) {
-          const int prow = rowbase + (i & 3) + 8 * (i >> 2);
-          gv.x = prow < L ? gv.x : 0.f;
-          gv.y = prow + 1 < L ? gv.y : 0.f;
+          const int prow = pos0 + 4 * h + (i & 3) + 8 * (i >> 2);
+          g0.x = prow < L ? g0.x : 0.f;
+          g0.y = prow + 1 < L ? g0.y : 0.f;
+          g1.x = prow + 32 < L ? g1.x : 0.f;
+          g1.y = prow + 33 < L ? g1.y : 0.f;
         }
-        s2v += gv;
+        sv += g0 + g1;
       }
-      float sacc = s2v.x + s2v.y;
+      float sacc = sv.x + sv.y;
       sacc += __shfl_xor(sacc, 32, 64);
       if (h == 0) vrow[jt * 32 + r] = sacc;
     };
-    f32x16_t a0 = wv_chain<true>(ws, hf, 0, r, h);
-    for (int jt = 0; jt < NJT; jt += 2) {
-      const f32x16_t a1 = wv_chain<true>(ws, hf, jt + 1, r, h);
-      colsum(a0, jt);
-      if (jt + 2 < NJT) a0 = wv_chain<true>(ws, hf, jt + 2, r, h);
-      colsum(a1, jt + 1);
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256(r, kk * 2 + h));
+    f32x16_t p0 = zero16(), p1 = zero16();
+    for (int jt = 0; jt < NJT; ++jt) {
+      f32x16_t c0 = zero16(), c1 = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        c0 = mfma32(hf0[kk], wf[kk], c0);
+        c1 = mfma32(hf1[kk], wf[kk], c1);
+      }
+      if (jt + 1 < NJT) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256((jt + 1) * 32 + r, kk * 2 + h));
+      }
+      if (jt > 0) colsum(p0, p1, jt - 1);
+      p0 = c0;
+      p1 = c1;
     }
+    colsum(p0, p1, NJT - 1);
   }
 }
 
@@ -289,13 +318,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
   auto load_rows = [&](long item, bf16x8* f) {
     const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
     const int pos = tw * 32 + r;
-    const bool ok = item < items && pos < L;
-    const bf16_t* src = h2 + ((size_t)b * L + pos) * CH;
+    const bool ok = pos < L;
+    const bf16_t* src = h2 + ((size_t)b * L + min(pos, L - 1)) * CH;     // clamped, unconditional loads
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (ok) v = *reinterpret_cast<const uint4*>(src + kk * 16 + 8 * h);
-      f[kk] = __builtin_bit_cast(bf16x8, v);
+      const uint4 v = *reinterpret_cast<const uint4*>(src + kk * 16 + 8 * h);
+      f[kk] = __builtin_bit_cast(bf16x8, ok ? v : make_uint4(0u, 0u, 0u, 0u));
     }
   };
   for (long item = (long)blockIdx.x * NW + w; item < items; item += stride) {
@@ -351,26 +379,40 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
     float mean, rstd;
     wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
     float sa = 0.f, sc = 0.f;
-    if (okb) {
+    {
+      // all operand loads first (clamped row, unconditional), then the math and masked stores
+      const int pc = min(pos, L - 1);
+      const size_t roff = ((size_t)b * L + pc) * CH;
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
+      for (int ct = 0; ct < 4; ++ct) {
+        uint2 dq[4], sq[4];
+        float4 gq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ci0 = ct * 32 + 8 * i + 4 * h;
+          dq[i] = dh2_in != nullptr ? *reinterpret_cast<const uint2*>(dh2_in + roff + ci0) : make_uint2(0u, 0u);
+          sq[i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
+          gq[i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
+          const int i = g;
           const int ci0 = ct * 32 + 8 * g + 4 * h;
-          float din[4] = {0, 0, 0, 0}, sv[4], gg[4], o[4];
-          if (dh2_in != nullptr) unpack4(*reinterpret_cast<const uint2*>(dh2_in + rowoff + ci0), din);
-          unpack4(*reinterpret_cast<const uint2*>(s2 + rowoff + ci0), sv);
-          load_f4(g2 + (size_t)pos * CH + ci0, gg);
+          float din[4], sv[4], o[4];
+          unpack4(dq[i], din);
+          unpack4(sq[i], sv);
+          const float gg[4] = {gq[i].x, gq[i].y, gq[i].z, gq[i].w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             o[e] = bfround(din[e] + y[ct][4 * g + e]);
             const float xh = (sv[e] - mean) * rstd;
             const float dxh = o[e] * gg[e];
-            sa += dxh;
-            sc += dxh * xh;
+            sa += okb ? dxh : 0.f;
+            sc += okb ? dxh * xh : 0.f;
           }
-          *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
+          if (okb) *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
         }
+      }
     }
     sa = wave_reduce_sum(sa);
     sc = wave_reduce_sum(sc);
@@ -729,14 +771,16 @@ PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int B
   return pbx_launch_status();
 }
 
-// nw: waves per workgroup (tile = 32 nw positions); vpart is [B][ceil(L / 32)][NJ] (one row per wave tile)
+// nw: waves per workgroup; vpart is [B][ceil(L / 64)][NJ] (one row per 64-position wave tile)
 PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
                                void* h2, float* vpart, int B, int L, int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + NJ * 4 > 163840 || nw < 1 || nw > 16) return (int)hipErrorInvalidValue;
-  const int TA = (L + 32 * nw - 1) / (32 * nw);
-  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3(persistent_grid(B * TA, 1)), dim3(64 * nw), NJ * 256, st,
-                     (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, B, L, NJ, eps);
+  if (NJ % 64 != 0 || NJ * 256 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  const long items = (long)B * ((L + 63) / 64);
+  long wgl = (items + nw - 1) / nw;
+  if (wgl > num_cus()) wgl = num_cus();
+  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3((int)wgl), dim3(64 * nw), NJ * 256, st, (const bf16_t*)s2, st2, g2, be2,
+                     (const bf16_t*)wv, (bf16_t*)h2, vpart, B, L, NJ, eps);
   return pbx_launch_status();
 }
 

@@ -143,6 +143,27 @@ __device__ __forceinline__ void ln_bwd_consts(const float* __restrict__ part, in
   m2 = c * inv_n;
 }
 
+// Global -> LDS staging of n 16-byte chunks with up to 8 loads in flight per thread (a plain
+// load -> store loop waits one memory round trip per iteration).  src(idx) -> uint4 (may apply
+// bounds / zero-fill), dst(idx, v) stores into LDS.
+template <typename SrcF, typename DstF>
+__device__ __forceinline__ void stage_chunks(int n, SrcF src, DstF dst) {
+  const int bs = blockDim.x;
+  for (int base = threadIdx.x; base < n; base += 8 * bs) {
+    uint4 v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = base + i * bs;
+      v[i] = idx < n ? src(idx) : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = base + i * bs;
+      if (idx < n) dst(idx, v[i]);
+    }
+  }
+}
+
 // Chan et al. merge of (count, mean, M2) partials: (n, m, M2) <- (n, m, M2) + (nb, mb, M2b)
 __device__ __forceinline__ void chan_merge(float& n, float& m, float& M2, float nb, float mb, float M2b) {
   const float nn = n + nb;

@@ -50,8 +50,8 @@ def conv_tile(L: int) -> int:
 
 
 def attn_fwd_waves(L: int) -> int:
-    """ln_attn_fwd workgroup: 16 waves (4 per SIMD) when the sequence fills them."""
-    return max(4, min(16, (L + 31) // 32))
+    """ln_attn_fwd workgroup: 8 independent waves (work items are 64-position wave tiles)."""
+    return 8
 
 
 def attn_bwd_waves(L: int) -> int:
@@ -132,13 +132,13 @@ class LocalBlockFn(torch.autograd.Function):
                   stream)
         NJ = wv_bf16.shape[0]
         nwf = attn_fwd_waves(L)
-        TV = (L + 31) // 32                     # one vpart row per 32-position wave tile
+        TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
                   wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
-        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 32)
+        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
         ctx.params = params
         return h2, vpart
 

@@ -8,9 +8,10 @@ for path in sys.argv[1:]:
 keys = ['SQ_WAVE_CYCLES', 'SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_INSTS_VMEM_WR',
         'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_WAIT_INST_LDS', 'SQ_WAIT_ANY', 'SQ_INSTS_VMEM_RD', 'SQ_ACTIVE_INST_VALU',
         'GRBM_GUI_ACTIVE', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_LDS', 'SQ_ACTIVE_INST_VMEM', 'SQ_ACTIVE_INST_ANY',
-        'SQ_INSTS_VALU_TRANS_F32', 'SQ_BUSY_CYCLES']
+        'SQ_INSTS_VALU_TRANS_F32', 'SQ_BUSY_CYCLES', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_ACTIVE_INST_SCA',
+        'SQ_INSTS_BRANCH']
 short = ['WAVECYC', 'VALU', 'MFMA', 'LDS', 'BANKCF', 'VMEMWR', 'MFMABUSY', 'WAITLDS', 'WAITANY', 'VMEMRD', 'ACTVALU',
-         'GUI', 'WAITINST', 'ACTLDS', 'ACTVMEM', 'ACTANY', 'TRANS', 'BUSY']
+         'GUI', 'WAITINST', 'ACTLDS', 'ACTVMEM', 'ACTANY', 'TRANS', 'BUSY', 'SALU', 'SMEM', 'ACTSCA', 'BRANCH']
 print(f"{'kernel':34s} " + " ".join(f"{k:>9s}" for k in short))
 for name, d in sorted(agg.items(), key=lambda kv: -sum(kv[1].get('GRBM_GUI_ACTIVE', [0]))):
     vals = []
