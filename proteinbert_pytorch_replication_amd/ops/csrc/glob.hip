@@ -13,9 +13,10 @@
 //   local_head  : logits, softmax over the batch, CE on the probabilities, and the whole backward
 //                 (the loss is terminal, so gradients are produced in the forward pass)
 //   go_head     : sigmoid + BCE + weighted mean + dlogits in one pass over [B, A]
-#include "common.h"
+#include "mfma.h"
 
 typedef unsigned short bf16_t;
+using namespace pbx;
 
 namespace {
 constexpr int MAXG = 1024;   // global_dim supported by the row kernels (<= 4 values per thread)
@@ -347,6 +348,219 @@ __global__ void __launch_bounds__(256) local_head_kernel(
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
 }
 
+// MFMA version of the local head (B <= 512): one workgroup (4 waves) per position l.
+//   logits  Z[b][v]   = h_l[b] . Wo[v] + bo[v]       (MFMA: A = h_l rows, B = Wo rows)
+//   softmax over b, CE on the probabilities, dz      (VALU on the [B][32] logit tile, as above)
+//   dWo_l[v][c]       = sum_b dz[b][v] h_l[b][c]     (MFMA: both operands transposed LDS reads)
+//   dh[b][c]          = sum_v dz[b][v] Wo[v][c]      (MFMA, staged through LDS for 256-B row stores)
+__global__ void __launch_bounds__(256) local_head_mfma_kernel(
+    const bf16_t* __restrict__ h, const float* __restrict__ wo, const float* __restrict__ bo,
+    const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, float* __restrict__ dwo_part,
+    float* __restrict__ dbo_part, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int Bp = (B + 31) & ~31;
+  unsigned char* hs = smem;                                   // [Bp][128] bf16 swz256 (later: dh tile)
+  unsigned char* wos = hs + Bp * 256;                         // [32][128] bf16 swz256
+  unsigned char* dzb = wos + 32 * 256;                        // [Bp][32] bf16, 64-B rows
+  float* zs = reinterpret_cast<float*>(dzb + Bp * 64);        // [Bp][32] fp32
+  float* red = zs + Bp * 32;                                  // [8][32]
+  float* colv = red + 8 * 32;                                 // [32] + [2][32]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int l = blockIdx.x;
+  // stage h_l rows (zero beyond B) and Wo (bf16, zero rows beyond V)
+  stage_chunks(
+      Bp * 16,
+      [&](int idx) {
+        const int b = idx >> 4;
+        return b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
+                     : make_uint4(0u, 0u, 0u, 0u);
+      },
+      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = v; });
+  for (int idx = tid; idx < 32 * 16; idx += 256) {
+    const int v = idx >> 4, c8 = idx & 15;
+    float e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (v < V) {
+      const float4 a = *reinterpret_cast<const float4*>(wo + v * 128 + c8 * 8);
+      const float4 b2 = *reinterpret_cast<const float4*>(wo + v * 128 + c8 * 8 + 4);
+      e[0] = a.x; e[1] = a.y; e[2] = a.z; e[3] = a.w; e[4] = b2.x; e[5] = b2.y; e[6] = b2.z; e[7] = b2.w;
+    }
+    *reinterpret_cast<uint4*>(wos + swz256(v, c8)) = packq8(e);
+  }
+  __syncthreads();
+  // logits
+  const float bov = r < V ? bo[r] : 0.f;
+  for (int rt = w; rt < Bp / 32; rt += 4) {
+    f32x16_t acc = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk)
+      acc = mfma32(lds_frag(hs, swz256(rt * 32 + r, kk * 2 + hh)), lds_frag(wos, swz256(r, kk * 2 + hh)), acc);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int b = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+      zs[b * 32 + r] = acc[i] + bov;
+    }
+  }
+  __syncthreads();
+  // softmax over b for each v (8 partial columns per v)
+  {
+    const int v = tid & 31, part = tid >> 5;
+    float m = -3.4e38f;
+    if (v < V)
+      for (int b = part; b < B; b += 8) m = fmaxf(m, zs[b * 32 + v]);
+    red[part * 32 + v] = m;
+    __syncthreads();
+    if (tid < 32) {
+      float mm = -3.4e38f;
+      for (int k = 0; k < 8; ++k) mm = fmaxf(mm, red[k * 32 + tid]);
+      colv[32 + tid] = mm;
+    }
+    __syncthreads();
+    float sacc = 0.f;
+    if (v < V)
+      for (int b = part; b < B; b += 8) sacc += __expf(zs[b * 32 + v] - colv[32 + v]);
+    red[part * 32 + v] = sacc;
+    __syncthreads();
+    if (tid < 32) {
+      float ss = 0.f;
+      for (int k = 0; k < 8; ++k) ss += red[k * 32 + tid];
+      colv[64 + tid] = ss > 0.f ? 1.0f / ss : 0.f;
+      colv[tid] = 0.f;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < B * 32; i += 256) {
+    const int v = i & 31;
+    zs[i] = v < V ? __expf(zs[i] - colv[32 + v]) * colv[64 + v] : 0.f;
+  }
+  __syncthreads();
+  // CE over v on the probabilities (one thread per sample); colv[v] = sum_b G P
+  float lsum = 0.f;
+  {
+    // per-thread G.P rows, then one wave reduction per v (no contended LDS atomics)
+    float gp[32];
+#pragma unroll
+    for (int v = 0; v < 32; ++v) gp[v] = 0.f;
+    for (int b = tid; b < B; b += 256) {
+      const float* p = zs + b * 32;
+      float pv[32];
+#pragma unroll
+      for (int v = 0; v < 32; ++v) pv[v] = p[v];
+      float mx = -3.4e38f;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) mx = v < V ? fmaxf(mx, pv[v]) : mx;
+      float se = 0.f, ev[32];
+#pragma unroll
+      for (int v = 0; v < 32; ++v) { ev[v] = v < V ? __expf(pv[v] - mx) : 0.f; se += ev[v]; }
+      const int yv = (int)y[(size_t)b * L + l];
+      const float wgt = wl[(size_t)b * L + l];
+      float py = 0.f;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) py = v == yv ? pv[v] : py;
+      lsum += wgt * (mx + __logf(se) - py);
+      const float coef = wgt * inv_bl, inv_se = 1.0f / se;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) gp[v] += coef * (ev[v] * inv_se - (v == yv ? 1.f : 0.f)) * pv[v];
+    }
+#pragma unroll
+    for (int v = 0; v < 32; ++v) {
+      if (v < V) {
+        const float sv = wave_reduce_sum(gp[v]);
+        if (lane == 0) atomicAdd(&colv[v], sv);
+      }
+    }
+  }
+  __syncthreads();
+  // dz = P (G - colv)  (fp32 in zs for dbo, bf16 copy in dzb for the MFMAs)
+  for (int b = tid; b < Bp; b += 256) {
+    float* p = zs + b * 32;
+    float dzv[32];
+#pragma unroll
+    for (int v = 0; v < 32; ++v) dzv[v] = 0.f;
+    if (b < B) {
+      float pv[32], ev[32];
+#pragma unroll
+      for (int v = 0; v < 32; ++v) pv[v] = p[v];
+      float mx = -3.4e38f;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) mx = v < V ? fmaxf(mx, pv[v]) : mx;
+      float se = 0.f;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) { ev[v] = v < V ? __expf(pv[v] - mx) : 0.f; se += ev[v]; }
+      const int yv = (int)y[(size_t)b * L + l];
+      const float coef = wl[(size_t)b * L + l] * inv_bl, inv_se = 1.0f / se;
+#pragma unroll
+      for (int v = 0; v < 32; ++v) {
+        const float g = coef * (ev[v] * inv_se - (v == yv ? 1.f : 0.f));
+        dzv[v] = v < V ? pv[v] * (g - colv[v]) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 32; ++v) p[v] = dzv[v];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(dzb + b * 64 + c * 16) = packq8(dzv + 8 * c);
+  }
+  __syncthreads();
+  // dWo_l: wave w -> channel tile w;  D[v][c] = sum_b dz^T[v][b] h[b][c]
+  {
+    f32x16_t acc = zero16();
+    const int colb = w * 32 + tc;
+    for (int kb = 0; kb < Bp / 16; ++kb) {
+      const int ra = kb * 16 + 8 * hh + q;
+      const bf16x8 fa = cat_tr(lds_tr(dzb, ra * 64 + tc * 2), lds_tr(dzb, (ra + 4) * 64 + tc * 2));
+      const bf16x8 fb = cat_tr(lds_tr(hs, swz256e(ra, colb)), lds_tr(hs, swz256e(ra + 4, colb)));
+      acc = mfma32(fa, fb, acc);
+    }
+    float* dst = dwo_part + (size_t)l * V * 128;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int v = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (v < V) dst[v * 128 + w * 32 + r] = acc[i];
+    }
+  }
+  if (tid < 32 && tid < V) {
+    float a = 0.f;
+    for (int b = 0; b < B; ++b) a += zs[b * 32 + tid];
+    dbo_part[(size_t)l * V + tid] = a;
+  }
+  __syncthreads();   // hs no longer read: it becomes the dh staging tile
+  // dh: D[b][c] = sum_v dz[b][v] Wo[v][c];  wave -> row tiles, all 4 channel tiles
+  for (int rt = w; rt < Bp / 32; rt += 4) {
+    f32x16_t acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const bf16x8 fa = *reinterpret_cast<const bf16x8*>(dzb + (rt * 32 + r) * 64 + (kk * 16 + 8 * hh) * 2);
+      const int rlo = kk * 16 + 8 * hh + q;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int col = ct * 32 + tc;
+        const bf16x8 fb = cat_tr(lds_tr(wos, swz256e(rlo, col)), lds_tr(wos, swz256e(rlo + 4, col)));
+        acc[ct] = mfma32(fa, fb, acc[ct]);
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int b = rt * 32 + 8 * g + 4 * hh;   // rows b .. b+3 (reg = 4g + e), column ct*32 + r
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          *reinterpret_cast<bf16_t*>(hs + swz256e(b + e, ct * 32 + r)) = f2bf(acc[ct][4 * g + e]);
+      }
+  }
+  __syncthreads();
+  for (int idx = tid; idx < B * 16; idx += 256) {
+    const int b = idx >> 4, c8 = idx & 15;
+    *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
+        *reinterpret_cast<const uint4*>(hs + swz256(b, c8));
+  }
+  lsum = wave_reduce_sum(lsum);
+  if (lane == 0) atomicAdd(loss, lsum * inv_bl);
+}
+
 // GO head: P = sigmoid(z), BCE(P, y) with PyTorch's log clamp (>= -100) and backward
 // dz = w/(BA) (P - y) P(1-P) / max(P(1-P), 1e-12)   (BCELoss backward x sigmoid backward).
 // z: [B, A] fp32 (GEMM output without bias); weights w[r * wsr + c * wsc] (wsc = 0: one per row)
@@ -421,13 +635,24 @@ PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float*
 PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
                               void* dh, float* dwo_part, float* dbo_part, float* loss, int B, int L, int V,
                               hipStream_t st) {
-  const int lds = (V * 128 + B * V + 12 * V) * 4;
-  if (V > 32 || lds > 163840) return (int)hipErrorInvalidValue;
+  if (V > 32) return (int)hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)local_head_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)local_head_mfma_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              163840);
     attr = true;
   }
+  const int Bp = (B + 31) & ~31;
+  const int lds_m = Bp * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (8 * 32 + 96) * 4;
+  if (lds_m <= 163840) {
+    hipLaunchKernelGGL(local_head_mfma_kernel, dim3(L), dim3(256), lds_m, st, (const bf16_t*)h, wo, bo,
+                       (const long long*)y, wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V,
+                       1.0f / ((float)B * (float)L));
+    return pbx_launch_status();
+  }
+  const int lds = (V * 128 + B * V + 12 * V) * 4;
+  if (lds > 163840) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(local_head_kernel, dim3(L), dim3(256), lds, st, (const bf16_t*)h, wo, bo, (const long long*)y,
                      wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V, 1.0f / ((float)B * (float)L));
   return pbx_launch_status();
@@ -440,3 +665,4 @@ PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, co
                      (bf16_t*)dz, dbias, loss, B, A, 1.0f / ((float)B * (float)A));
   return pbx_launch_status();
 }
+

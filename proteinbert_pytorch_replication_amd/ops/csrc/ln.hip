@@ -702,24 +702,53 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restr
   *reinterpret_cast<uint4*>(out + row * CH + c8 * 8) = packq8(v);
 }
 
-// one wave per row: lane l adds channels 2l, 2l+1 of the row into the LDS copy of its token's row,
-// so every LDS atomic wave-instruction touches 64 consecutive addresses (no intra-instruction
-// conflicts); each workgroup then adds its 26 x 128 partial table into dE.
+// Embedding backward as a one-hot GEMM on MFMA: dE[v][c] = sum_rows [tok[row] == v] dout[row][c].
+// A workgroup (4 waves) reduces a contiguous run of rows in 256-row tiles: the dout tile is staged
+// in LDS (swz256) and read transposed as the B operand, the one-hot A operand is built in registers
+// from the staged tokens, wave w owns channels 32w..32w+31; one atomic flush of [V][128] per
+// workgroup.  (The previous LDS-atomic scatter serialised on the 26 hot token rows.)
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restrict__ tok,
                                                         const bf16_t* __restrict__ dout, float* __restrict__ dE,
                                                         long rows, int V) {
-  __shared__ float acc[32 * CH];
-  for (int i = threadIdx.x; i < V * CH; i += 256) acc[i] = 0.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (long row = (long)blockIdx.x * 4 + w; row < rows; row += (long)gridDim.x * 4) {
-    const int t = (int)tok[row];
-    const unsigned int q = *reinterpret_cast<const unsigned int*>(dout + row * CH + 2 * lane);
-    atomicAdd(&acc[t * CH + 2 * lane], __uint_as_float(q << 16));
-    atomicAdd(&acc[t * CH + 2 * lane + 1], __uint_as_float(q & 0xffff0000u));
+  __shared__ __attribute__((aligned(16))) unsigned char ds[256 * 256];
+  __shared__ int ts[256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const long per = (rows + gridDim.x - 1) / gridDim.x;
+  const long r0 = (long)blockIdx.x * per, r1 = min(rows, r0 + per);
+  f32x16_t acc = zero16();
+  for (long t0 = r0; t0 < r1; t0 += 256) {
+    const int n = (int)min((long)256, r1 - t0);
+    __syncthreads();
+    stage_chunks(
+        256 * 16,
+        [&](int idx) {
+          const int row = idx >> 4;
+          return row < n ? *reinterpret_cast<const uint4*>(dout + (t0 + row) * CH + (idx & 15) * 8)
+                         : make_uint4(0u, 0u, 0u, 0u);
+        },
+        [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(ds + swz256(idx >> 4, idx & 15)) = v; });
+    ts[tid] = tid < n ? (int)tok[t0 + tid] : -1;
+    __syncthreads();
+    const int colb = w * 32 + tc;
+#pragma unroll 4
+    for (int kb = 0; kb < 16; ++kb) {
+      // A[i = v][k = row]: lane's v = r, rows kb*16 + 8h + j
+      typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+      u16x8 oh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) oh[j] = ts[kb * 16 + 8 * h + j] == r ? (unsigned short)0x3F80 : (unsigned short)0;
+      const int rb = kb * 16 + 8 * h + q;
+      const bf16x8 fb = cat_tr(lds_tr(ds, swz256e(rb, colb)), lds_tr(ds, swz256e(rb + 4, colb)));
+      acc = mfma32(__builtin_bit_cast(bf16x8, oh), fb, acc);
+    }
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < V * CH; i += 256) atomicAdd(dE + i, acc[i]);
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int v = (i & 3) + 8 * (i >> 2) + 4 * h;
+    if (v < V && acc[i] != 0.f) atomicAdd(dE + v * CH + w * 32 + r, acc[i]);
+  }
 }
 
 int g_cus = -1;
@@ -845,8 +874,9 @@ PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long ro
 
 PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long rows, int V, hipStream_t st) {
   if (V > 32) return (int)hipErrorInvalidValue;
-  long g = (rows + 3) / 4;
-  if (g > 256) g = 256;    // few adders per address: the 26 x 128 table is tiny and hot
+  long g = (rows + 511) / 512;
+  if (g > 2 * num_cus()) g = 2 * num_cus();
+  if (g < 1) g = 1;
   hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
                      (const bf16_t*)dout, dE, rows, V);
   return pbx_launch_status();
