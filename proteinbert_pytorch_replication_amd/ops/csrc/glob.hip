@@ -666,3 +666,36 @@ PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, co
   return pbx_launch_status();
 }
 
+
+// dst[c] += scale * sum_r src[r][c]   (scale: optional device scalar).  A block covers 32 columns with
+// 8 row-lanes (row r -> lane r % 8), the 8 partials are combined in LDS in fixed order
+// (deterministic); used to fold per-position partial gradients into the arena.
+__global__ void __launch_bounds__(256) colsum_add_kernel(const float* __restrict__ src, int rows, int cols,
+                                                         float* __restrict__ dst, const float* __restrict__ scale) {
+  __shared__ float part[8][33];
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = blockIdx.x * 32 + cl;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < cols) {
+    int r = rl;
+    for (; r + 8 < rows; r += 16) {
+      a0 += src[(size_t)r * cols + c];
+      a1 += src[(size_t)(r + 8) * cols + c];
+    }
+    for (; r < rows; r += 8) a0 += src[(size_t)r * cols + c];
+  }
+  part[rl][cl] = a0 + a1;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += part[k][cl];
+    dst[c] += scale != nullptr ? s * scale[0] : s;
+  }
+}
+
+PBX_EXPORT int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st) {
+  if (cols <= 0 || rows <= 0) return 0;
+  hipLaunchKernelGGL(colsum_add_kernel, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, dst, scale);
+  return pbx_launch_status();
+}

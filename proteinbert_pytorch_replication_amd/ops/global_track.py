@@ -25,6 +25,7 @@ _lib.register("pbx_row_ln_fwd", [_P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P,
 _lib.register("pbx_row_ln_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
+_lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_go_head", [_P, _P, _P, _P, ctypes.c_long, ctypes.c_long, _P, _P, _P, _I, _I, _P])
 
@@ -107,6 +108,7 @@ class InputLayerFn(torch.autograd.Function):
         ctx.save_for_backward(ann_bf, u, g_bf, ugl)
         ctx.params = (w, b, wgl, bgl)
         ctx.mark_non_differentiable(g_bf)
+        ctx.set_materialize_grads(False)     # no zero-filled gradients for unused outputs
         return g, g_bf, gb
 
     @staticmethod
@@ -118,14 +120,14 @@ class InputLayerFn(torch.autograd.Function):
         B, G = u.shape
         gr = _Grads([w, b, wgl, bgl])
         dw, db, dwgl, dbgl = gr.dst
-        dg = torch.zeros((B, G), dtype=F32, device=dev) if dg is None else dg.float().contiguous().clone()
+        dg = torch.zeros((B, G), dtype=F32, device=dev) if dg is None else dg.float().contiguous()
         if dgb is not None:
             N = ugl.shape[1]
             dugl = torch.empty((B, N), dtype=BF16, device=dev)
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
                       dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
             addmm_into(dwgl, dugl.t(), g_bf)
-            addmm_into(dg, dugl, bf16_of(wgl))
+            dg = torch.addmm(dg, dugl, bf16_of(wgl), out_dtype=F32)      # new buffer: no clone + add
         du = torch.empty((B, G), dtype=BF16, device=dev)
         _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
                   st)
@@ -177,6 +179,7 @@ class GlobalBlockFn(torch.autograd.Function):
         ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
         ctx.TV = TV
         ctx.mark_non_differentiable(g2_bf)
+        ctx.set_materialize_grads(False)
         return g2, g2_bf, gb
 
     @staticmethod
@@ -195,8 +198,7 @@ class GlobalBlockFn(torch.autograd.Function):
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
                       dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
             addmm_into(dwgl, dugl.t(), g2_bf)
-            dg2 = dg2.clone()   # never modify autograd's incoming buffer in place
-            addmm_into(dg2, dugl, bf16_of(wgl))
+            dg2 = torch.addmm(dg2, dugl, bf16_of(wgl), out_dtype=F32)   # new buffer (incoming grad untouched)
         # LN2 + MLP2
         du2 = torch.empty((B, G), dtype=BF16, device=dev)
         dg1 = torch.empty((B, G), dtype=F32, device=dev)
@@ -255,6 +257,7 @@ class HeadsLossFn(torch.autograd.Function):
         ctx.V = V
         total = loss.sum()
         ctx.mark_non_differentiable(loss)
+        ctx.set_materialize_grads(False)
         return total, loss
 
     @staticmethod
@@ -263,18 +266,22 @@ class HeadsLossFn(torch.autograd.Function):
         wo, bo, wa, ba = ctx.params
         gr = _Grads([wo, bo, wa, ba])
         dwo, dbo_dst, dwa, dba_dst = gr.dst
+        st = _s(dh.device)
+        if dtotal is None:
+            return (None,) * 11
         if _UNIT_LOSS_GRAD[0]:
             # loss.backward() from the training step: d(loss) == 1 exactly, skip the rescale passes
             dz_s, dh_s = dz, dh
-            dwo.add_(dwo_part.sum(0))
-            dbo_dst.add_(dbo_part.sum(0))
-            dba_dst.add_(dba)
+            scale = None
         else:
-            s = dtotal.reshape(()).to(F32)
-            dz_s, dh_s = dz * s, dh * s
-            dwo.add_(dwo_part.sum(0) * s)
-            dbo_dst.add_(dbo_part.sum(0) * s)
-            dba_dst.add_(dba * s)
+            scale = dtotal.reshape(1).to(F32).contiguous()
+            s0 = scale.reshape(())
+            dz_s, dh_s = (dz.float() * s0).to(dz.dtype), (dh.float() * s0).to(dh.dtype)
+        # per-position partials of the local head -> its weight / bias gradients (one pass each)
+        L_, V_ = dbo_part.shape
+        _lib.call("pbx_colsum_add", dwo_part.data_ptr(), L_, dwo_part[0].numel(), dwo.data_ptr(), _lib.ptr(scale), st)
+        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), L_, V_, dbo_dst.data_ptr(), _lib.ptr(scale), st)
+        _lib.call("pbx_colsum_add", dba.data_ptr(), 1, dba.numel(), dba_dst.data_ptr(), _lib.ptr(scale), st)
         dg2 = mm32(dz_s, bf16_of(wa))
         addmm_into(dwa, dz_s.t(), g2_bf)
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)

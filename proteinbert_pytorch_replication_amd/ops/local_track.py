@@ -139,6 +139,7 @@ class LocalBlockFn(torch.autograd.Function):
                   wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
         ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
+        ctx.set_materialize_grads(False)
         ctx.params = params
         return h2, vpart
 
@@ -224,10 +225,24 @@ class EmbedFn(torch.autograd.Function):
         return None, dE
 
 
+def _wv_bf16(att) -> torch.Tensor:
+    """bf16 [H*vd, C] copy of the stacked value weights.  In reference semantics the heads are
+    untrained buffers, so the copy is cached and only rebuilt when Wv changes."""
+    Wv = att.Wv
+    if isinstance(Wv, torch.nn.Parameter) and Wv.requires_grad:
+        return att.value_weight_cat().t().to(torch.bfloat16).contiguous()
+    key = (Wv.data_ptr(), Wv._version, Wv.device)
+    cached = getattr(att, "_pbx_wv_cache", None)
+    if cached is None or cached[0] != key:
+        cached = (key, att.value_weight_cat().t().to(torch.bfloat16).contiguous())
+        att._pbx_wv_cache = cached
+    return cached[1]
+
+
 def local_block(x: torch.Tensor, gb: torch.Tensor, blk) -> Tuple[torch.Tensor, torch.Tensor]:
     """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``)."""
     att = blk.global_attention_layer
-    wv = att.value_weight_cat().t().to(torch.bfloat16).contiguous()          # [H*vd, C]
+    wv = _wv_bf16(att)                                                       # [H*vd, C]
     nc = blk.local_narrow_conv_layer[0]
     wc = blk.local_wide_conv_layer[0]
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
