@@ -380,15 +380,28 @@ __global__ void __launch_bounds__(512) conv_dgrad_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// weight gradient. grid (nconv * 4 output-channel groups, R position chunks), 256 threads.
-// Wave w owns input channels w*32..+32 for all KS taps (KS tiles of 32x32 -> 16*KS accumulators).
-// D[co][ci] += sum_pos dy[pos][co] * x[pos + shift][ci]   (A, B both via transposed LDS reads)
+// weight gradient. 1-D grid of nconv * 4 output-channel groups ("types") x R position chunks, 256
+// threads.  Wave w owns input channels w*32..+32 for all KS taps (KS tiles of 32x32 -> 16*KS
+// accumulators).  D[co][ci] += sum_pos dy[pos][co] * x[pos + shift][ci]  (A, B via transposed LDS
+// reads).  XCD-aware mapping: workgroups are dealt to the 8 XCDs round-robin by id, so the types of
+// one chunk (which all stage the same x rows) get ids congruent mod 8 and share one XCD's L2
+// instead of fetching those rows from HBM once per XCD.
 template <int KS, int BM>
 __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ dy0, const bf16_t* __restrict__ dy1,
                                                     const bf16_t* __restrict__ x, float* __restrict__ slab,
-                                                    float* __restrict__ bslab, int B, int L, int dil1, int nconv) {
+                                                    float* __restrict__ bslab, int B, int L, int dil1, int nconv,
+                                                    int R) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int type = blockIdx.x, chunk = blockIdx.y, R = gridDim.y;
+  const int ntypes = nconv * 4;
+  int type, chunk;
+  if ((R & 7) == 0) {
+    const int id = blockIdx.x, j = id >> 3;
+    chunk = (j / ntypes) * 8 + (id & 7);
+    type = j - (j / ntypes) * ntypes;
+  } else {
+    chunk = blockIdx.x / ntypes;
+    type = blockIdx.x - chunk * ntypes;
+  }
   const int cv = type >> 2, cg = type & 3;
   const bf16_t* dy = cv ? dy1 : dy0;
   const int d = cv ? dil1 : 1;
@@ -430,8 +443,10 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
                                        : make_uint4(0u, 0u, 0u, 0u);
         },
         [&](int idx, uint4 v) {
-          if (idx < BM * 4) *reinterpret_cast<uint4*>(dys + (idx >> 2) * 64 + (idx & 3) * 16) = v;
-          else { const int i2 = idx - BM * 4; *reinterpret_cast<uint4*>(xs + swz256(i2 >> 4, i2 & 15)) = v; }
+          // one store site with a 16-B-aligned offset (two sites compile to 4 x ds_write_b32)
+          const int i2 = idx - BM * 4;
+          const int off = idx < BM * 4 ? (idx >> 2) * 64 + (idx & 3) * 16 : BM * 64 + swz256(i2 >> 4, i2 & 15);
+          *reinterpret_cast<uint4*>(__builtin_assume_aligned(smem + off, 16)) = v;
         });
     __syncthreads();
 #pragma unroll 2
@@ -583,13 +598,13 @@ PBX_EXPORT int pbx_wgrad(const void* dy0, const void* dy1, const void* x, float*
   const int halo = (KS / 2) * (nconv > 1 ? dil1 : 1);
   const int lds = BM * 64 + (BM + 2 * halo) * 256;
   if (lds > 163840 || nconv < 1 || nconv > 2) return (int)hipErrorInvalidValue;
-  dim3 grid(nconv * 4, R);
+  dim3 grid(nconv * 4 * R);
   if (KS == 9)
     hipLaunchKernelGGL((wgrad_kernel<9, BM>), grid, dim3(256), lds, st, (const bf16_t*)dy0, (const bf16_t*)dy1,
-                       (const bf16_t*)x, slab, bslab, B, L, dil1, nconv);
+                       (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R);
   else if (KS == 1)
     hipLaunchKernelGGL((wgrad_kernel<1, BM>), grid, dim3(256), lds, st, (const bf16_t*)dy0, (const bf16_t*)dy1,
-                       (const bf16_t*)x, slab, bslab, B, L, dil1, nconv);
+                       (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R);
   else
     return (int)hipErrorInvalidValue;
   (void)accumulate;   // destinations are always accumulated into (zero-initialised when not arena views)

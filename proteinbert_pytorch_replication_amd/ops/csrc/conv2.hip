@@ -1,0 +1,377 @@
+// Dual-dilation residue convolutions with weights streamed as MFMA fragments.
+//
+// Reference: ProteinBERT/modules.py:124-147 (Conv1d C->C, k=9, dilation 1 and 5, padding "same",
+// each + GELU) and :205-212 (x + narrow + wide + broadcast(global->local), LayerNorm over (L, C)).
+//
+// Why a second form (conv.hip holds the LDS-weight-ring kernels): there, every workgroup stages all
+// 590 KB of both convs' weights through LDS (global -> VGPR -> ds_write -> barrier -> ds_read) for
+// only 256 positions; per weight step the LDS spends about as many cycles on those writes plus the
+// fragment reads as the MFMAs take, a barrier separates every step, and the 141 KB footprint allows
+// one workgroup per CU (MFMA busy ~25 %, profiles/r1_hip_v5_*).
+//
+// Here the weights are re-packed once per step (pbx_pack_conv_frag, 2 x 295 KB bf16) into the exact
+// per-lane order of a v_mfma_f32_32x32x16_bf16 A operand, so one wave loads a whole 32x16 fragment
+// with ONE coalesced 1-KB global_load_dwordx4 (an L2 hit: every XCD keeps the 0.6 MB resident).
+// Only the activation tile lives in LDS; the main loop has no barrier and no LDS writes, each wave
+// runs independently with its A fragments prefetched two K-steps ahead, and a workgroup needs
+// < 80 KB of LDS and <= 128 VGPRs, so two workgroups (16 waves) share a CU.
+//
+//   conv_fwd3   : 128 positions / workgroup; waves 0-3 = narrow conv, 4-7 = wide conv; wave q owns
+//                 output channels q*32..+32 for all 128 positions (4 accumulators of 32x32).
+//                 Epilogue: pre_n, pre_w and s1 = x + GELU(pre_n) + GELU(pre_w) + gb staged through
+//                 LDS for row-contiguous 16-B stores, plus the tile's LayerNorm (mean, M2) partial.
+//   conv_dgrad3 : both convs' dpre = dS1 * GELU'(pre) tiles (with their halos) staged once and their
+//                 central rows written for the weight gradient; waves 0-3 = narrow, 4-7 = wide, wave
+//                 q owns input channels q*32..+32; the two halves are summed through LDS in the
+//                 dx = dS1 + W^T dpre epilogue.
+#include "mfma.h"
+
+using namespace pbx;
+typedef unsigned short bf16_t;
+
+namespace {
+constexpr int CH = 128;
+constexpr int BM = 128;               // positions per workgroup
+constexpr int FRAG = 64 * 8;          // bf16 per packed fragment (64 lanes x 8)
+constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging tile
+
+// Packed fragment index (in fragments) of (tap k, K-block kb of 16, M-block mb of 32); lane offset
+// added by the reader.  Forward: M = output channel, K = input channel.  Dgrad: M = input channel,
+// K = output channel.
+__device__ __forceinline__ int frag_index(int k, int kb, int mb) { return (k * 8 + kb) * 4 + mb; }
+
+__global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
+    const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
+    const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
+    bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
+    float* __restrict__ stats, int L, int KS, int dil) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = (L + BM - 1) / BM;
+  const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
+  const int pos0 = t * BM;
+  const int half = KS >> 1;
+  const int halo = half * dil;
+  const int XR = BM + 2 * halo;
+  unsigned char* xs = smem;                                   // XR x 256 B (swz256)
+  unsigned char* ot = smem + XR * 256;                        // [BM][128] bf16 staging tile
+  float* bsm = reinterpret_cast<float*>(ot + OT);             // bn | bw | gb[b] | LN scratch
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int cv = w >> 2, cq = w & 3;
+  const bf16_t* xsmp = x + (size_t)b * L * CH;
+  const bf16x8* fw = (cv ? fww : fwn) + cq * 64 + lane;     // + frag_index(k, kb, 0) * 64
+  const int NI = KS * 8;                                      // K-steps: taps x 16-channel blocks
+  // A-fragment ring: step it uses fr[it & 3], the load for step it + 3 is in flight meanwhile (the
+  // loop is unrolled by the ring size so the ring never rotates registers, which would make the
+  // compiler wait for the newest load every step)
+  bf16x8 fr[4];
+  fr[0] = fw[0];
+  fr[1] = fw[256];
+  fr[2] = fw[512];
+  if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
+  stage_chunks(
+      XR * 16,
+      [&](int idx) {
+        const int pos = pos0 - halo + (idx >> 4);
+        return (pos >= 0 && pos < L) ? *reinterpret_cast<const uint4*>(xsmp + (size_t)pos * CH + (idx & 15) * 8)
+                                     : make_uint4(0u, 0u, 0u, 0u);
+      },
+      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
+  __syncthreads();
+
+  f32x16_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = zero16();
+  const int d = cv ? dil : 1;
+  for (int it0 = 0; it0 < NI; it0 += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = it0 + u;
+      fr[(u + 3) & 3] = fw[min(it + 3, NI - 1) * 256];
+      __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
+      const int k = it >> 3, kb = it & 7;
+      const int rb = halo + r + (k - half) * d;
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[u], lds_frag(xs, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
+    }
+  }
+
+  // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
+  const int vrows = min(BM, L - pos0);
+  const float* bias = bsm + cv * CH;
+  auto stage_acc = [&]() {                        // ot <- bf16(acc + bias)
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch0 = cq * 32 + 8 * g + 4 * h;
+        const float4 bv = *reinterpret_cast<const float4*>(bias + ch0);
+        const float v[4] = {acc[pt][4 * g] + bv.x, acc[pt][4 * g + 1] + bv.y, acc[pt][4 * g + 2] + bv.z,
+                            acc[pt][4 * g + 3] + bv.w};
+        *reinterpret_cast<uint2*>(ot + swz256e(pt * 32 + r, ch0)) = packq4(v);
+      }
+  };
+  auto copy_out = [&](bf16_t* __restrict__ dst) {  // ot -> dst rows (16 B per lane, row-contiguous)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 512 * i;
+      const int row = idx >> 4, c = idx & 15;
+      if (row < vrows)
+        *reinterpret_cast<uint4*>(dst + ((size_t)b * L + pos0 + row) * CH + c * 8) =
+            *reinterpret_cast<const uint4*>(ot + swz256(row, c));
+    }
+  };
+  if (cv == 0) stage_acc();                       // pre_n
+  __syncthreads();
+  copy_out(pre_n);
+  __syncthreads();
+  if (cv == 1) stage_acc();                       // pre_w
+  __syncthreads();
+  copy_out(pre_w);
+  __syncthreads();
+  // narrow waves: s1 = x + GELU(pre_n) + GELU(pre_w) + gb from the bf16 pre-activations the
+  // backward reads, written over pre_w in place (each element belongs to one lane), with the
+  // per-lane (sum, sum of squares) of the LayerNorm partial
+  float* scratch = bsm + 3 * CH;                  // 4 narrow waves x (n, mean, M2)
+  if (cv == 0) {
+    float lsum = 0.f, lsq = 0.f;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ch0 = cq * 32 + 8 * g + 4 * h;
+        const int p = pt * 32 + r;
+        const bool ok = p < vrows;
+        float xv[4], pw[4], o[4];
+        unpack4(*reinterpret_cast<const uint2*>(xs + swz256e(halo + p, ch0)), xv);
+        uint2* op = reinterpret_cast<uint2*>(ot + swz256e(p, ch0));
+        unpack4(*op, pw);
+        const float4 bnv = *reinterpret_cast<const float4*>(bsm + ch0);
+        const float4 gbv = *reinterpret_cast<const float4*>(bsm + 2 * CH + ch0);
+        const float bna[4] = {bnv.x, bnv.y, bnv.z, bnv.w};
+        const float gba[4] = {gbv.x, gbv.y, gbv.z, gbv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float pn = bfround(acc[pt][4 * g + e] + bna[e]);
+          o[e] = bfround(xv[e] + gelu_f(pn) + gelu_f(pw[e]) + gba[e]);
+          lsum += ok ? o[e] : 0.f;
+          lsq += ok ? o[e] * o[e] : 0.f;
+        }
+        *op = packq4(o);
+      }
+    int cnt = 0;
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt) cnt += (pt * 32 + r) < vrows ? 16 : 0;
+    float n = (float)cnt, m = cnt > 0 ? lsum / n : 0.f;
+    float M2 = cnt > 0 ? fmaxf(lsq - lsum * m, 0.f) : 0.f;
+    wave_chan(n, m, M2);
+    if (lane == 0) { scratch[3 * w] = n; scratch[3 * w + 1] = m; scratch[3 * w + 2] = M2; }
+  }
+  __syncthreads();
+  copy_out(s1);
+  if (tid == 0) {
+    float tn = 0.f, tm = 0.f, tM2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) chan_merge(tn, tm, tM2, scratch[3 * i], scratch[3 * i + 1], scratch[3 * i + 2]);
+    stats[((size_t)b * T + t) * 2] = tm;
+    stats[((size_t)b * T + t) * 2 + 1] = tM2;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// data gradient: D[ci][pos] = sum_conv sum_tap sum_co W[co][ci][tap] * dpre_conv[pos - shift][co]
+__global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
+    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ pre_n, const bf16_t* __restrict__ pre_w,
+    const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = (L + BM - 1) / BM;
+  const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
+  const int pos0 = t * BM;
+  const int half = KS >> 1;
+  const int halo_n = half, halo_w = half * dil;
+  const int RN = BM + 2 * halo_n;
+  unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
+  unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int cv = w >> 2, cq = w & 3;
+  const size_t sbase = (size_t)b * L * CH;
+  const bf16x8* fw = (cv ? ftw : ftn) + cq * 64 + lane;
+  const int NI = KS * 8;
+  bf16x8 fr[4];                                   // A-fragment ring, as in conv_fwd3
+  fr[0] = fw[0];
+  fr[1] = fw[256];
+  fr[2] = fw[512];
+
+  // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
+#pragma unroll 1
+  for (int c = 0; c < 2; ++c) {
+    const int halo = c ? halo_w : halo_n;
+    const bf16_t* pre = c ? pre_w : pre_n;
+    bf16_t* dpo = c ? dpre_w : dpre_n;
+    unsigned char* tile = c ? aw : an;
+    const int nch = (BM + 2 * halo) * 16;
+    for (int base = tid; base < nch; base += 2 * 512) {
+      uint4 gq[2], pq[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = base + i * 512;
+        const int pos = pos0 - halo + (idx >> 4);
+        const bool ok = idx < nch && pos >= 0 && pos < L;
+        const size_t off = sbase + (size_t)pos * CH + (idx & 15) * 8;
+        gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
+        pq[i] = ok ? *reinterpret_cast<const uint4*>(pre + off) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = base + i * 512;
+        if (idx >= nch) break;
+        const int j = idx >> 4, ch = idx & 15;
+        const int pos = pos0 - halo + j;
+        float g[8], pv[8], o[8];
+        unpack8(gq[i], g);
+        unpack8(pq[i], pv);
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const f32x2 dd = gelu_grad2((f32x2){pv[e], pv[e + 1]}) * (f32x2){g[e], g[e + 1]};
+          o[e] = dd.x;
+          o[e + 1] = dd.y;
+        }
+        const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
+        if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
+          *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
+        *reinterpret_cast<uint4*>(tile + swz256(j, ch)) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  f32x16_t acc[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] = zero16();
+  const int d = cv ? dil : 1;
+  const unsigned char* as = cv ? aw : an;
+  const int halo = cv ? halo_w : halo_n;
+  for (int it0 = 0; it0 < NI; it0 += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = it0 + u;
+      fr[(u + 3) & 3] = fw[min(it + 3, NI - 1) * 256];
+      __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
+      const int k = it >> 3, kb = it & 7;
+      const int rb = halo + r - (k - half) * d;
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[u], lds_frag(as, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
+    }
+  }
+
+  // epilogue: the wide half stages its fp32 partial ([BM][128] fp32, 16-B chunks XOR-swizzled by
+  // row), the narrow half adds its own in place, then dx = ds1 + sum, row-contiguous 16-B accesses.
+  const int vrows = min(BM, L - pos0);
+  float* ft = reinterpret_cast<float*>(smem);     // 64 KB over the dpre tiles
+  auto fidx = [&](int p, int c4) { return p * CH + ((c4 ^ (p & 31)) << 2); };
+  __syncthreads();                                // every wave is done reading the dpre tiles
+  if (cv == 1) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c4 = (cq * 32 + 8 * g + 4 * h) >> 2;
+        *reinterpret_cast<float4*>(ft + fidx(pt * 32 + r, c4)) =
+            make_float4(acc[pt][4 * g], acc[pt][4 * g + 1], acc[pt][4 * g + 2], acc[pt][4 * g + 3]);
+      }
+  }
+  __syncthreads();
+  if (cv == 0) {
+#pragma unroll
+    for (int pt = 0; pt < 4; ++pt)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c4 = (cq * 32 + 8 * g + 4 * h) >> 2;
+        float4* f = reinterpret_cast<float4*>(ft + fidx(pt * 32 + r, c4));
+        const float4 o = *f;
+        *f = make_float4(o.x + acc[pt][4 * g], o.y + acc[pt][4 * g + 1], o.z + acc[pt][4 * g + 2],
+                         o.w + acc[pt][4 * g + 3]);
+      }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i;
+    const int row = idx >> 4, c = idx & 15;
+    if (row >= vrows) continue;
+    const size_t off = sbase + (size_t)(pos0 + row) * CH + c * 8;
+    float gv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
+    const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c));
+    const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c + 1));
+    const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
+    *reinterpret_cast<uint4*>(dx + off) = packq8(o);
+  }
+}
+
+// fp32 torch conv weight [co][ci][KS] -> bf16 fragment images: fwd[k][kb][mb][lane][8] with
+// (M = co = 32mb + (lane&31), K = ci = 16kb + 8(lane>>5) + j) and dgrad with M = ci, K = co.
+__global__ void __launch_bounds__(256) pack_conv_frag_kernel(const float* __restrict__ w, bf16_t* __restrict__ pf,
+                                                             bf16_t* __restrict__ pt, int KS) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= KS * CH * CH) return;
+  const int j = idx & 7, lane = (idx >> 3) & 63, fi = idx >> 9;
+  const int mb = fi & 3, kb = (fi >> 2) & 7, k = fi >> 5;
+  const int m = mb * 32 + (lane & 31), kk = kb * 16 + 8 * (lane >> 5) + j;
+  pf[idx] = f2bf(w[((size_t)m * CH + kk) * KS + k]);     // M = co, K = ci
+  pt[idx] = f2bf(w[((size_t)kk * CH + m) * KS + k]);     // M = ci, K = co
+}
+
+int fwd3_lds(int KS, int dil) { return (BM + 2 * (KS / 2) * dil) * 256 + OT + (3 * CH + 16) * 4; }
+int dgrad3_lds(int KS, int dil) {
+  const int a = (2 * BM + 2 * (KS / 2) * (1 + dil)) * 256;
+  return a > BM * CH * 4 ? a : BM * CH * 4;
+}
+}  // namespace
+
+static bool conv3_attrs_set = false;
+static void set_conv3_attrs() {
+  if (conv3_attrs_set) return;
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  conv3_attrs_set = true;
+}
+
+// LayerNorm partials in `stats` are per 128-position tile: [B][ceil(L/128)][2].  fwn/fww: forward
+// fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels.
+PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
+                             int dil, hipStream_t st) {
+  set_conv3_attrs();
+  const int lds = fwd3_lds(KS, dil);
+  if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
+  const int T = (L + BM - 1) / BM;
+  hipLaunchKernelGGL(conv_fwd3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
+                     (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* pre_w, const void* ftn,
+                               const void* ftw, void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS, int dil,
+                               hipStream_t st) {
+  set_conv3_attrs();
+  const int lds = dgrad3_lds(KS, dil);
+  if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
+  const int T = (L + BM - 1) / BM;
+  hipLaunchKernelGGL(conv_dgrad3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1, (const bf16_t*)pre_n,
+                     (const bf16_t*)pre_w, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n,
+                     (bf16_t*)dpre_w, L, KS, dil);
+  return pbx_launch_status();
+}
+
+// fwd / dgrad fragment images (KS * 128 * 128 bf16 each) of one fp32 [128][128][KS] conv weight
+PBX_EXPORT int pbx_pack_conv_frag(const float* w, void* pf, void* pt, int KS, hipStream_t st) {
+  const int n = KS * CH * CH;
+  hipLaunchKernelGGL(pack_conv_frag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, w, (bf16_t*)pf, (bf16_t*)pt,
+                     KS);
+  return pbx_launch_status();
+}

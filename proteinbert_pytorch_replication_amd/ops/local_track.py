@@ -17,6 +17,7 @@ Every op raises if the HIP library is missing — there is no silent eager fallb
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -29,6 +30,9 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv", [_P, _P, _P, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
@@ -45,8 +49,36 @@ PB = 32           # positions per workgroup of the position-major LayerNorm kern
 LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 
 
+# conv kernel form: "v3" (csrc/conv2.hip: weights streamed from L2 as packed MFMA fragments,
+# 128-position tiles, two workgroups per CU) or "v1" (csrc/conv.hip: weights staged through an LDS
+# ring, 256/128-position tiles, one workgroup per CU); PBX_CONV=v1 selects the latter.
+CONV_IMPL = os.environ.get("PBX_CONV", "v3")
+
+
 def conv_tile(L: int) -> int:
+    if CONV_IMPL == "v3":
+        return 128
     return 256 if L >= 256 else 128
+
+
+def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, BM, stream) -> None:
+    if CONV_IMPL == "v3":
+        _lib.call("pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                  gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
+                  stream)
+    else:
+        _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                  gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
+                  BM, stream)
+
+
+def conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM, stream) -> None:
+    if CONV_IMPL == "v3":
+        _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, stream)
+    else:
+        _lib.call("pbx_conv_dgrad", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, BM, stream)
 
 
 def attn_fwd_waves(L: int) -> int:
@@ -68,12 +100,14 @@ def _num_cus(dev: torch.device) -> int:
 
 
 def pack_conv(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """fp32 ``[co, ci, KS]`` -> bf16 ``WP[KS][co][ci]`` (forward) and ``WT[KS][ci][co]`` (dgrad)."""
+    """fp32 ``[co, ci, KS]`` -> the forward and dgrad bf16 weight images of the selected conv form:
+    v3: MFMA A-fragment images ``[KS][8][4][64 lanes][8]`` (M = co / ci, K = ci / co);
+    v1: ``WP[KS][co][ci]`` and ``WT[KS][ci][co]``."""
     KS = w.shape[2]
     wp = torch.empty((KS, CH, CH), dtype=torch.bfloat16, device=w.device)
     wt = torch.empty_like(wp)
-    _lib.call("pbx_pack_conv", w.detach().contiguous().data_ptr(), wp.data_ptr(), wt.data_ptr(), KS,
-              _lib.stream_ptr(w.device))
+    fn = "pbx_pack_conv_frag" if CONV_IMPL == "v3" else "pbx_pack_conv"
+    _lib.call(fn, w.detach().contiguous().data_ptr(), wp.data_ptr(), wt.data_ptr(), KS, _lib.stream_ptr(w.device))
     return wp, wt
 
 
@@ -121,9 +155,7 @@ class LocalBlockFn(torch.autograd.Function):
         pre_w = torch.empty_like(x)
         s1 = torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
-                  gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), st1.data_ptr(), B, L, KS, dil,
-                  BM1, stream)
+        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
         pre_l = torch.empty_like(x)
         s2 = torch.empty_like(x)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
@@ -188,8 +220,7 @@ class LocalBlockFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
-        _lib.call("pbx_conv_dgrad", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
-                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, BM1, stream)
+        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
         _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:

@@ -1,0 +1,3 @@
+# rocprofv3 kernel stats of the headline bench; $1 = output dir name under gpurun_out/
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/$1 -- python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 3 > $GRAFT_REPO_ROOT/gpurun_out/$1.log 2>&1

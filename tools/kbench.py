@@ -49,8 +49,9 @@ def report(name, us, flops=None, bytes_=None):
 
 x = (torch.randn(B, L, C, device=dev) * 0.5).to(bf)
 w = torch.randn(C, C, KS, device=dev) * 0.03
-wpn, wtn = lt.pack_conv(w)
-wpw, wtw = lt.pack_conv(w)
+wpn, wtn = torch.empty(KS, C, C, dtype=bf, device=dev), torch.empty(KS, C, C, dtype=bf, device=dev)
+_lib.call("pbx_pack_conv", w.data_ptr(), wpn.data_ptr(), wtn.data_ptr(), KS, st)
+wpw, wtw = wpn, wtn
 bias = torch.zeros(C, device=dev)
 gb = torch.zeros(B, C, device=dev)
 act = lambda: torch.empty_like(x)  # noqa: E731
@@ -68,6 +69,44 @@ for BM in (256, 128):
                                   wtn.data_ptr(), wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L,
                                   KS, dil, BM, st))
     report(f"conv_dgrad BM={BM}", us, conv_flops, 6 * x.numel() * 2)
+# fragment-streamed forms (conv2.hip), checked against the v1 outputs of the same inputs
+bias2 = torch.randn(C, device=dev) * 0.1
+gb2 = torch.randn(B, C, device=dev) * 0.1
+T1 = (L + 255) // 256
+st_a = torch.empty(B, T1, 2, device=dev)
+ref = [act() for _ in range(3)]
+_lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bias2.data_ptr(), bias2.data_ptr(),
+          gb2.data_ptr(), ref[0].data_ptr(), ref[1].data_ptr(), ref[2].data_ptr(), st_a.data_ptr(), B, L, KS, dil, 256,
+          st)
+fpn, ftn_ = torch.empty_like(wpn), torch.empty_like(wpn)
+_lib.call("pbx_pack_conv_frag", w.data_ptr(), fpn.data_ptr(), ftn_.data_ptr(), KS, st)
+T2 = (L + 127) // 128
+st_b = torch.empty(B, T2, 2, device=dev)
+new = [act() for _ in range(3)]
+fwd2 = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fpn.data_ptr(), fpn.data_ptr(), bias2.data_ptr(),  # noqa
+                         bias2.data_ptr(), gb2.data_ptr(), new[0].data_ptr(), new[1].data_ptr(), new[2].data_ptr(),
+                         st_b.data_ptr(), B, L, KS, dil, st)
+fwd2()
+torch.cuda.synchronize()
+for nm, u, v in zip(("pre_n", "pre_w", "s1"), ref, new):
+    print(f"  fwd3 vs fwd {nm}: max|diff| {float((u.float() - v.float()).abs().max()):.4g}  "
+          f"max|ref| {float(u.float().abs().max()):.3g}", flush=True)
+report("conv_fwd3 (frag-streamed W)", timeit(fwd2), conv_flops, 4 * x.numel() * 2)
+dref = [act() for _ in range(3)]
+dnew = [act() for _ in range(3)]
+ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
+_lib.call("pbx_conv_dgrad", ds1.data_ptr(), ref[0].data_ptr(), ref[1].data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
+          dref[0].data_ptr(), dref[1].data_ptr(), dref[2].data_ptr(), B, L, KS, dil, 256, st)
+dg2 = lambda: _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), ref[0].data_ptr(), ref[1].data_ptr(),  # noqa
+                        ftn_.data_ptr(), ftn_.data_ptr(), dnew[0].data_ptr(), dnew[1].data_ptr(), dnew[2].data_ptr(),
+                        B, L, KS, dil, st)
+dg2()
+torch.cuda.synchronize()
+for nm, u, v in zip(("dx", "dpre_n", "dpre_w"), dref, dnew):
+    print(f"  dgrad3 vs dgrad {nm}: max|diff| {float((u.float() - v.float()).abs().max()):.4g}  "
+          f"max|ref| {float(u.float().abs().max()):.3g}", flush=True)
+report("conv_dgrad3 (frag-streamed W)", timeit(dg2), conv_flops, 6 * x.numel() * 2)
+
 dw0 = torch.zeros(C, C, KS, device=dev)
 dw1 = torch.zeros(C, C, KS, device=dev)
 db0 = torch.zeros(C, device=dev)
