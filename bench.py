@@ -50,7 +50,8 @@ def parse():
                     help="hip: fused CDNA4 kernels; torch: eager bf16 oracle; faithful: reference math, eager fp32")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
-                    help="capture the whole step in a hipGraph (auto: single GPU, or PBX_GRAPH_DP=1)")
+                    help="capture the whole step in a hipGraph (auto: only with PBX_GRAPH=1; eager launches "
+                         "measure faster since the conv weight gradients overlap on a second stream)")
     ap.add_argument("--seed", type=int, default=0)
     return ap.parse_args()
 
@@ -94,7 +95,7 @@ def main():
         return step(X, Y, W)
 
     use_graph = a.graph == "on" or (a.graph == "auto" and dev.type == "cuda" and a.impl == "hip" and
-                                     (info.world_size == 1 or os.environ.get("PBX_GRAPH_DP") == "1"))
+                                     os.environ.get("PBX_GRAPH") == "1")
     graphed = False
     if use_graph:
         from proteinbert_pytorch_replication_amd.train.step import GraphedStep

@@ -469,14 +469,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
     }
   }
   (void)halo_max;
+  // slab in the torch weight layout [co][ci][KS] so the reduction streams it with 16-B accesses
+  float* dst = slab + ((size_t)chunk * nconv + cv) * KS * CH * CH + (size_t)(w * 32 + r) * KS;
 #pragma unroll
-  for (int k = 0; k < KS; ++k) {
-    float* dst = slab + ((((size_t)chunk * nconv + cv) * KS + k) * CH) * CH;
+  for (int i = 0; i < 16; ++i) {
+    const int co = cg * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int co = cg * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-      dst[(size_t)co * CH + w * 32 + r] = acc[k][i];
-    }
+    for (int k = 0; k < KS; ++k) dst[(size_t)co * CH * KS + k] = acc[k][i];
   }
   if (w == 0) {
     bsum += __shfl_xor(bsum, 32, 64);
@@ -485,14 +484,15 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const bf16_t* __restrict__ d
 }
 
 // sum the R slabs (fixed order: deterministic) and ADD the result into the torch layouts:
-// weight [co][ci][KS] (KS == 1: [co][ci]), bias [co] -- the destinations are the flat-arena .grad
-// views (or zero-initialised tensors); one thread owns each destination element (no atomics).
+// weight [co][ci][KS] (KS == 1: [co][ci]) -- the slabs already use it, so both sides stream with
+// 16-B accesses -- and bias [co]; the destinations are the flat-arena .grad views (or zero-initialised
+// tensors); one thread owns each destination element (no atomics).
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float4* __restrict__ slab,
                                                            const float* __restrict__ bslab, float* __restrict__ dw0,
                                                            float* __restrict__ dw1, float* __restrict__ db0,
                                                            float* __restrict__ db1, int R, int nconv, int KS) {
-  const int per = KS * CH * CH;
-  const int total4 = nconv * per / 4;
+  const int per4 = KS * CH * CH / 4;
+  const int total4 = nconv * per4;
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx < total4) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -507,13 +507,11 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float4* __restr
       const float4 a = slab[(size_t)rr * total4 + idx];
       s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
     }
-    const int e = idx * 4;
-    const int cv = e / per, rem = e - cv * per;
-    const int k = rem / (CH * CH), co = (rem / CH) % CH, ci = rem % CH;
-    float* dw = cv ? dw1 : dw0;
-    const float sv[4] = {s.x, s.y, s.z, s.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dw[((size_t)co * CH + ci + j) * KS + k] += sv[j];
+    const int cv = idx >= per4;
+    float4* dw = reinterpret_cast<float4*>(cv ? dw1 : dw0) + (idx - cv * per4);
+    float4 o = *dw;
+    o.x += s.x; o.y += s.y; o.z += s.z; o.w += s.w;
+    *dw = o;
   }
   if (idx < nconv * CH) {
     float s = 0.f;

@@ -22,7 +22,7 @@ from typing import Dict, Optional, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, streams
 from ..train.arena import notify_grads_ready
 from .global_track import bf16_of
 
@@ -121,16 +121,22 @@ def _grad_dst(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
 
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
            B: int, L: int, outs):
-    """outs: [(dw, db)] destinations (accumulated into)."""
+    """outs: [(dw, db)] destinations (accumulated into).  Returns the scratch tensors (the caller keeps
+    them alive while the launch may still be running on another stream)."""
     dev = x.device
     ntiles = B * ((L + 127) // 128)
-    R = max(1, min(ntiles, (2 * _num_cus(dev)) // (4 * nconv)))
+    # position chunks: ~3/8 of a CU's worth of workgroups per conv type (R = 48 on 256 CUs), a
+    # multiple of 8 for the XCD-aware mapping; measured best with the wgrad on the aux stream, where
+    # it shares the chip with the main-stream backward kernels (R = 32/40/56/64/128 are slower)
+    R = int(os.environ.get("PBX_WGRAD_R", 0)) or max(8, (3 * _num_cus(dev) // (8 * nconv)) // 8 * 8)
+    R = min(R, ntiles)
     slab = torch.empty((R, nconv, KS, CH, CH), dtype=torch.float32, device=dev)
     bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
     (dw0, db0) = outs[0]
     (dw1, db1) = outs[1] if nconv > 1 else (None, None)
     _lib.call("pbx_wgrad", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
               dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, KS, dil, nconv, R, 1, _lib.stream_ptr(dev))
+    return [slab, bslab]
 
 
 class LocalBlockFn(torch.autograd.Function):
@@ -221,7 +227,13 @@ class LocalBlockFn(torch.autograd.Function):
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
         conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
-        _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
+        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
+            # the weight gradient goes to the aux stream: off the critical path, only the optimizer
+            # and the DP all-reduce read it (its inputs stay referenced until the join)
+            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
+                           keep=[dpn, dpw, x])
+        else:
+            _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)

@@ -23,11 +23,13 @@ collectives per step.
 """
 from __future__ import annotations
 
+import contextlib
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
+from ..ops import streams
 from ..train.arena import FlatArena, add_grad_ready_listener, remove_grad_ready_listener
 
 
@@ -99,12 +101,16 @@ class BucketedAllReduce:
         s, e = self.buckets[b]
         view = self.arena.grad[s:e]
         dt = self._dtype_for(b)
-        if dt != torch.float32:
-            tmp = view.to(dt)
-            self._tmp[b] = tmp
-            self._works[b] = dist.all_reduce(tmp, group=self.pg, async_op=True)
-        else:
-            self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
+        # a bucket may hold conv weight gradients still being produced on the aux stream
+        # (ops/streams.py): enqueue the collective behind both streams without stalling this one
+        ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()
+        with ctx:
+            if dt != torch.float32:
+                tmp = view.to(dt)
+                self._tmp[b] = tmp
+                self._works[b] = dist.all_reduce(tmp, group=self.pg, async_op=True)
+            else:
+                self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
 
     def _launch_ready(self) -> None:
         while self._next < len(self.buckets) and self._pending[self._next] <= 0:
@@ -120,6 +126,8 @@ class BucketedAllReduce:
         """Launch any bucket whose params got no gradient, then wait (stream-ordered)."""
         if not self.enabled:
             return
+        if self.arena.grad.is_cuda:
+            streams.join()
         for b in range(self._next, len(self.buckets)):
             self._launch(b)
         self._next = len(self.buckets)

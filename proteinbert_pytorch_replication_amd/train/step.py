@@ -61,8 +61,10 @@ class PretrainStep:
         loss = self.loss(X, Y, W)
         if self.model.resolved_backend(self.device) == "hip":
             from ..ops.global_track import unit_loss_grad
+            from ..ops import streams
             with unit_loss_grad():
                 loss.backward()
+            streams.join()                      # conv weight gradients ran on the aux stream
         else:
             loss.backward()
         if self.ddp is not None:
