@@ -35,7 +35,9 @@ from ..train.arena import FlatArena, add_grad_ready_listener, remove_grad_ready_
 
 class BucketedAllReduce:
     def __init__(self, arena: FlatArena, bucket_mb: float = 8.0, process_group=None,
-                 comm_dtype: torch.dtype = torch.float32, tail_bf16: bool = False):
+                 comm_dtype: torch.dtype = torch.float32, tail_bf16: bool = False, force: bool = False):
+        """``force`` runs the hooks and collectives even on a 1-rank group (tests of the stream
+        ordering on a single GPU)."""
         self.arena = arena
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -65,7 +67,7 @@ class BucketedAllReduce:
         self._tmp: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._next = 0
         self._hooks = []
-        self.enabled = self.world > 1
+        self.enabled = self.world > 1 or (force and dist.is_initialized())
         self._index = {id(p): i for i, p in enumerate(arena.params)}
         if self.enabled:
             for i, p in enumerate(arena.params):
