@@ -17,7 +17,7 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from . import _lib
+from . import _lib, streams
 from ..train.arena import notify_grads_ready
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -113,7 +113,19 @@ class InputLayerFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dg, _dgbf, dgb):
-        ann_bf, u, g_bf, ugl = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        dev = saved[1].device
+        if streams.GLOBAL_ENABLED and dev.type == "cuda":
+            # weight gradients only: run on the global-track aux stream (ops/streams.py)
+            with streams.on_aux(dev, "global", keep=[*saved, dg, dgb]) as scope:
+                out = InputLayerFn._backward(ctx, saved, dg, dgb)
+                scope.keep(*out)
+            return out
+        return InputLayerFn._backward(ctx, saved, dg, dgb)
+
+    @staticmethod
+    def _backward(ctx, saved, dg, dgb):
+        ann_bf, u, g_bf, ugl = saved
         w, b, wgl, bgl = ctx.params
         dev = u.device
         st = _s(dev)
@@ -184,7 +196,21 @@ class GlobalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dg2, _dg2bf, dgb):
-        g_bf, u1, xh1, r1, vsum, g1_bf, u2, xh2, r2, g2_bf, ugl = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        dev = saved[1].device
+        if streams.GLOBAL_ENABLED and dev.type == "cuda":
+            # on the global-track aux stream: it overlaps the main stream's conv data gradient of the
+            # next block; the next local-block backward waits for dvpart (streams.wait_ready)
+            with streams.on_aux(dev, "global", keep=[*saved, dg2, dgb]) as scope:
+                out = GlobalBlockFn._backward(ctx, saved, dg2, dgb)
+                scope.keep(*out)
+            streams.mark_ready(dev, "global", [out[0], out[2]])
+            return out
+        return GlobalBlockFn._backward(ctx, saved, dg2, dgb)
+
+    @staticmethod
+    def _backward(ctx, saved, dg2, dgb):
+        g_bf, u1, xh1, r1, vsum, g1_bf, u2, xh2, r2, g2_bf, ugl = saved
         w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl = ctx.params
         dev = u1.device
         st = _s(dev)

@@ -183,6 +183,7 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, dvpart):
+        streams.wait_ready(dvpart)           # produced by the global-track backward on its aux stream
         (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
         B, L, KS, dil, BM1, T1, T2, NJ, BMV = ctx.meta
         dev = x.device
@@ -222,6 +223,10 @@ class LocalBlockFn(torch.autograd.Function):
         dgb = torch.zeros((B, CH), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(), TS1,
                   g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, stream)
+        if streams.GLOBAL_ENABLED:
+            # the previous block's global-track backward (next autograd node, aux stream) needs only
+            # dgb: let it start here, beside the conv data gradient below
+            streams.fork(dev, "global")
         # convolutions
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
@@ -231,7 +236,7 @@ class LocalBlockFn(torch.autograd.Function):
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
             streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
-                           keep=[dpn, dpw, x])
+                           keep=[dpn, dpw, x], name="wgrad")
         else:
             _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
         direct = [p for p, (_, d) in zip(params, dsts) if d]

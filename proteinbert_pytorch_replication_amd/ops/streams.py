@@ -1,67 +1,71 @@
-"""Side-stream execution of off-critical-path backward work (the conv weight gradients).
+"""Side-stream execution of off-critical-path backward work.
 
-In one block's backward the conv weight gradient (``pbx_wgrad`` + its slab reduction, ~1 ms of a
-5.8 ms paper-config step) depends only on ``dpre`` and the block input, and nothing else in the
-backward reads its result: the next kernels on the critical path (the previous block's attention /
-LayerNorm / conv-dgrad chain) need only ``dx``.  Issuing it on a second HIP stream lets the
-hardware run its MFMA-bound waves beside the bandwidth-bound LayerNorm/attention kernels.
+Two pieces of one block's backward do not feed the critical path directly:
 
-Protocol (also valid under hipGraph capture, where the fork/join becomes graph edges):
+* ``wgrad``  - the conv weight gradient (``pbx_wgrad`` + slab reduction, ~1 ms of a 5 ms
+  paper-config step): only the optimizer and the DP all-reduce read it;
+* ``global`` - the global-track backward of the previous block (~0.1 ms of small GEMMs and row
+  LayerNorms per block): its outputs are consumed by the NEXT local-block backward, so it can run
+  beside this block's conv data gradient instead of after it (opt-in, see GLOBAL_ENABLED).
 
-* :func:`launch` makes the aux stream wait for the current stream, runs ``fn`` under the aux
-  stream (allocations inside ``fn`` belong to the aux stream's pool) and keeps ``keep`` tensors
-  alive until the join, so the caching allocator cannot hand their memory to the main stream while
-  the aux stream still reads them.
-* :func:`join` makes the main stream wait for the aux stream and drops the kept tensors.  It is
-  queued as an autograd end-of-backward callback, called again by :class:`..train.step.PretrainStep`
-  before the optimizer, and :func:`collective_stream` lets the DP reducer order a bucket's all-reduce
-  after the aux-stream gradients that bucket contains.
+Issuing them on their own HIP streams lets the hardware run them beside the main-stream kernels.
+Protocol (eager and under hipGraph capture, where fork/join become graph edges):
+
+* :func:`on_aux` makes the named aux stream wait for the current stream (or for an earlier
+  :func:`fork` point of it) and runs the body on it;
+  every tensor the body reads that was allocated by the main stream, and every output another
+  stream consumes, is kept referenced until :func:`join` (the caching allocator could otherwise
+  hand the memory to another stream's writer while the aux kernels still use it).
+* :func:`mark_ready` notes which aux stream produced a tensor; a consumer on another stream calls
+  :func:`wait_ready` before reading it (a stream-level wait: work already enqueued on the consumer
+  stream keeps overlapping).
+* :func:`join` makes the main stream wait for every aux stream (queued as an autograd
+  end-of-backward callback and called by :class:`..train.step.PretrainStep`), and
+  :func:`collective_stream` orders a DP all-reduce behind the main stream and every aux stream on a
+  dedicated communication stream.
 """
 from __future__ import annotations
 
 import os
 from contextlib import contextmanager
-from typing import Callable, Dict, List, Optional
+from typing import Dict, Iterable, List, Optional, Tuple
 
 import torch
 
-ENABLED = os.environ.get("PBX_AUX_STREAM", "1") != "0"
+ENABLED = os.environ.get("PBX_AUX_STREAM", "1") != "0"            # conv weight gradient
+# The global-track backward on its own stream measured SLOWER on MI355X (5.2 -> 5.4-5.8 ms/step,
+# paper config): its small hipBLASLt GEMMs take CUs from the critical-path conv data gradient beside
+# the weight-gradient stream; a high-priority critical-path stream did not recover it.  Off by default.
+GLOBAL_ENABLED = os.environ.get("PBX_GLOBAL_STREAM", "0") == "1"
 
-_streams: Dict[int, torch.cuda.Stream] = {}
+_streams: Dict[Tuple[int, str], torch.cuda.Stream] = {}
 _pending: Dict[int, List[torch.Tensor]] = {}
+_used: Dict[int, set] = {}
 _main: Dict[int, torch.cuda.Stream] = {}
+_ready: Dict[int, Tuple[int, str]] = {}
 _callback_queued = {"v": False}
 
 
-def _aux(device: torch.device) -> torch.cuda.Stream:
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    s = _streams.get(idx)
+def _idx(device: torch.device) -> int:
+    return device.index if device.index is not None else torch.cuda.current_device()
+
+
+def _aux(device: torch.device, name: str = "wgrad") -> torch.cuda.Stream:
+    key = (_idx(device), name)
+    s = _streams.get(key)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
-        _streams[idx] = s
+        s = torch.cuda.Stream(device=key[0])
+        _streams[key] = s
     return s
 
 
 def active(device: Optional[torch.device] = None) -> bool:
     if device is None:
         return any(_pending.values())
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    return bool(_pending.get(idx))
+    return bool(_pending.get(_idx(device)))
 
 
-def launch(device: torch.device, fn: Callable[[], Optional[List[torch.Tensor]]], keep: List[torch.Tensor]) -> None:
-    """Run ``fn`` (kernel launches) on the aux stream of ``device`` after the current stream's work.
-    ``keep`` and the tensors ``fn`` returns (its scratch) stay referenced until :func:`join`: an
-    aux-pool block freed earlier could be handed to a main-stream writer while aux kernels still
-    use it."""
-    idx = device.index if device.index is not None else torch.cuda.current_device()
-    main = torch.cuda.current_stream(idx)
-    aux = _aux(device)
-    aux.wait_stream(main)
-    with torch.cuda.stream(aux):
-        scratch = fn() or []
-    _pending.setdefault(idx, []).extend(list(keep) + list(scratch))
-    _main[idx] = main
+def _queue_join() -> None:
     if not _callback_queued["v"]:
         try:
             torch.autograd.Variable._execution_engine.queue_callback(join)
@@ -70,26 +74,98 @@ def launch(device: torch.device, fn: Callable[[], Optional[List[torch.Tensor]]],
             pass
 
 
+class _AuxScope:
+    def __init__(self, idx: int):
+        self.idx = idx
+
+    def keep(self, *tensors) -> None:
+        _pending.setdefault(self.idx, []).extend(t for t in tensors if isinstance(t, torch.Tensor))
+
+
+_forked: Dict[Tuple[int, str], bool] = {}
+
+
+def fork(device: torch.device, name: str) -> None:
+    """Make aux stream ``name`` wait for the current stream's work enqueued SO FAR; the next
+    :func:`on_aux` on it starts from this point instead of the current stream's later tail (the
+    main stream can enqueue more work that the aux body does not need)."""
+    _aux(device, name).wait_stream(torch.cuda.current_stream(_idx(device)))
+    _forked[(_idx(device), name)] = True
+
+
+@contextmanager
+def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
+    """Run the body on aux stream ``name`` of ``device`` after the current stream's work (or after
+    the pending :func:`fork` point of that stream)."""
+    idx = _idx(device)
+    main = torch.cuda.current_stream(idx)
+    aux = _aux(device, name)
+    if not _forked.pop((idx, name), False):
+        aux.wait_stream(main)
+    scope = _AuxScope(idx)
+    scope.keep(*keep)
+    _used.setdefault(idx, set()).add(name)
+    _main[idx] = main
+    with torch.cuda.stream(aux):
+        yield scope
+    _queue_join()
+
+
+def launch(device: torch.device, fn, keep: List[torch.Tensor], name: str = "wgrad") -> None:
+    """Run ``fn`` (kernel launches) on aux stream ``name``; ``keep`` and the tensors ``fn`` returns
+    (its scratch) stay referenced until :func:`join`."""
+    with on_aux(device, name, keep) as scope:
+        scope.keep(*(fn() or []))
+
+
+def mark_ready(device: torch.device, name: str, tensors: Iterable[torch.Tensor]) -> None:
+    """Record that ``tensors`` are outputs of aux stream ``name`` (complete once the work enqueued
+    on it so far has run)."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor):
+            _ready[t.data_ptr()] = (_idx(device), name)
+
+
+def wait_ready(*tensors) -> None:
+    """Current stream waits for the aux-stream producer of any of ``tensors`` (no-op otherwise).
+    The wait is on the producer stream's current tail (``wait_stream``: an event recorded and
+    waited at once, which stays valid under hipGraph capture; an event recorded during capture
+    and waited later would become a graph node owning a soon-destroyed event)."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor):
+            key = _ready.pop(t.data_ptr(), None)
+            if key is not None:
+                torch.cuda.current_stream(t.device).wait_stream(_streams[key])
+
+
 def join() -> None:
-    """Main stream(s) wait for the aux stream(s); release the tensors kept for them."""
+    """Main stream(s) wait for every aux stream; release the tensors kept for them."""
     _callback_queued["v"] = False
     for idx, keep in list(_pending.items()):
-        if not keep:
+        if not keep and not _used.get(idx):
             continue
         main = _main.get(idx) or torch.cuda.current_stream(idx)
-        main.wait_stream(_streams[idx])
+        for name in _used.get(idx, ()):
+            main.wait_stream(_streams[(idx, name)])
         keep.clear()
+        _used[idx] = set()
+    _ready.clear()
+    _forked.clear()
 
 
 @contextmanager
 def collective_stream(device: torch.device):
-    """Context for issuing a collective over gradients that may include aux-stream results: the
-    collective is enqueued behind both the current stream's and the aux stream's work, without
-    making the current stream wait."""
-    if not active(device):
+    """Context for a collective over gradients that may include aux-stream results: it is enqueued
+    on a communication stream behind the current stream and every aux stream in use, without making
+    any of them wait."""
+    idx = _idx(device)
+    names = _used.get(idx)
+    if not names:
         yield
         return
-    aux = _aux(device)
-    aux.wait_stream(torch.cuda.current_stream(device))
-    with torch.cuda.stream(aux):
+    comm = _aux(device, "comm")
+    comm.wait_stream(torch.cuda.current_stream(idx))
+    for name in names:
+        comm.wait_stream(_streams[(idx, name)])
+    with torch.cuda.stream(comm):
         yield

@@ -27,6 +27,8 @@ def _port():
 
 
 def _run(with_ddp: bool, steps: int = 3):
+    """Returns the losses, the parameters after ``steps`` updates and the FIRST step's gradients
+    (later gradients inherit Adam-amplified float-atomic noise from the diverging parameters)."""
     torch.manual_seed(0)
     m = ProteinBERT(sequences_length=256, num_annotations=512, local_dim=128, global_dim=256, key_dim=64,
                     num_heads=4, num_blocks=3, device="cuda", backend="hip")
@@ -36,15 +38,21 @@ def _run(with_ddp: bool, steps: int = 3):
         assert ddp.enabled and len(ddp.buckets) > 4
     step = PretrainStep(m, opt, ddp)
     gen = SyntheticUniRefGO(256, 512, 16, "cuda", seed=5)
-    losses = []
+    losses, g_first = [], None
     for _ in range(steps):
         X, Y, W = gen.next_batch()
         losses.append(float(step(X, Y, W)))
+        if g_first is None:
+            g_first = opt.arena.grad.clone()
     torch.cuda.synchronize()
-    return losses, opt.arena.data.clone(), opt.arena.grad.clone()
+    return losses, opt.arena.data.clone(), g_first
 
 
-def test_rccl_buckets_behind_aux_stream():
+@pytest.mark.parametrize("global_stream", [False, True])
+def test_rccl_buckets_behind_aux_stream(global_stream):
+    from proteinbert_pytorch_replication_amd.ops import streams
+    saved = streams.GLOBAL_ENABLED
+    streams.GLOBAL_ENABLED = global_stream
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
                             timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0))
     try:
@@ -52,6 +60,7 @@ def test_rccl_buckets_behind_aux_stream():
         l1, p1, g1 = _run(True)
     finally:
         dist.destroy_process_group()
+        streams.GLOBAL_ENABLED = saved
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 1e-4 * abs(a) + 1e-6, (l0, l1)
     assert float((g0 - g1).abs().max()) <= 1e-3 * float(g0.abs().max())

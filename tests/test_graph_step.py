@@ -41,27 +41,28 @@ def test_graphed_step_matches_eager():
         assert float((d > 1e-4).float().mean()) < 0.02, (n, float((d > 1e-4).float().mean()))
 
 
-def test_aux_stream_wgrad_matches_inline():
-    """Conv weight gradients on the aux stream (ops/streams.py) equal the inline ones: same kernels,
-    only the stream differs (float-atomic accumulation elsewhere in the backward makes the match
-    approximate, not bitwise)."""
+def test_aux_stream_backward_matches_inline():
+    """Conv weight gradients and global-track backward on aux streams (ops/streams.py) equal the
+    single-stream backward: same kernels, only the streams differ (float-atomic accumulation
+    elsewhere in the backward makes the match approximate, not bitwise)."""
     from proteinbert_pytorch_replication_amd.ops import streams
+    from proteinbert_pytorch_replication_amd.ops.global_track import unit_loss_grad
     grads = []
+    saved = (streams.ENABLED, streams.GLOBAL_ENABLED)
     for enabled in (False, True):
-        streams.ENABLED = enabled
+        streams.ENABLED = streams.GLOBAL_ENABLED = enabled
         try:
             m, o, s, g = _setup()
             X, Y, W = g.next_batch()
             o.zero_grad()
             loss = s.loss(X, Y, W)
-            from proteinbert_pytorch_replication_amd.ops.global_track import unit_loss_grad
             with unit_loss_grad():
                 loss.backward()
             streams.join()
             torch.cuda.synchronize()
             grads.append(o.arena.grad.clone())
         finally:
-            streams.ENABLED = True
+            streams.ENABLED, streams.GLOBAL_ENABLED = saved
     assert torch.isfinite(grads[0]).all()
     scale = float(grads[0].abs().max())
     assert float((grads[0] - grads[1]).abs().max()) <= 1e-3 * scale
