@@ -12,8 +12,8 @@ from typing import Dict, Tuple
 import torch
 import torch.nn.functional as F
 
-from .global_track import GlobalBlockFn, HeadsLossFn, InputLayerFn
-from .local_track import CH, EmbedFn, local_block
+from .global_track import FusedGlobalBlockFn, GlobalBlockFn, HeadsLossFn, InputLayerFn, glob_fused_ok, pack_batch
+from .local_track import CH, EmbedFn, conv_images, local_block
 
 
 def hip_supported(model) -> Tuple[bool, str]:
@@ -47,15 +47,40 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     # g0 and block 0's global->local vector; every GlobalBlockFn then produces the next block's gb
     g, g_bf, gb = InputLayerFn.apply(annotations, lin.weight, lin.bias, gl0.weight, gl0.bias)
     h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
+    # every weight image the fused kernels read this step, built by one launch
+    items, conv_imgs, glob_imgs = [], [], []
     for i, blk in enumerate(blocks):
-        h, vpart = local_block(h, gb, blk)
+        imgs, it = conv_images(blk.local_narrow_conv_layer[0].weight, blk.local_wide_conv_layer[0].weight)
+        conv_imgs.append(imgs)
+        items += it
+        nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
+        if glob_fused_ok(g.shape[1], 0 if nxt is None else nxt.weight.shape[0]):
+            ws = [blk.global_linear_layer_1[0].weight, blk.global_linear_layer_2[0].weight,
+                  None if nxt is None else nxt.weight]
+            imgs = []
+            for w in ws:
+                if w is None:
+                    imgs += [None, None]
+                    continue
+                o1, o2 = (torch.empty(w.numel(), dtype=torch.bfloat16, device=w.device) for _ in range(2))
+                imgs += [o1, o2]
+                items.append((1, w.detach(), o1, o2, w.shape[0], w.shape[1]))
+            glob_imgs.append(tuple(imgs))
+        else:
+            glob_imgs.append(None)
+    pack_batch(items)
+    for i, blk in enumerate(blocks):
+        h, vpart = local_block(h, gb, blk, conv_imgs[i])
         att = blk.global_attention_layer
         nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
         l1, l2 = blk.global_linear_layer_1[0], blk.global_linear_layer_2[0]
         n1, n2 = blk.global_norm_1, blk.global_norm_2
-        g, g_bf, gb = GlobalBlockFn.apply(g, g_bf, vpart, l1.weight, l1.bias, n1.weight, n1.bias, l2.weight, l2.bias,
-                                          n2.weight, n2.bias, att.W_parameter,
-                                          None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
+        args = (g, g_bf, vpart, l1.weight, l1.bias, n1.weight, n1.bias, l2.weight, l2.bias, n2.weight, n2.bias,
+                att.W_parameter, None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
+        if glob_imgs[i] is not None:
+            g, g_bf, gb = FusedGlobalBlockFn.apply(*args, glob_imgs[i])
+        else:
+            g, g_bf, gb = GlobalBlockFn.apply(*args)
     if return_bf16:
         return h, g, g_bf
     return h, g

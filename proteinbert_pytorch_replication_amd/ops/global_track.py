@@ -13,6 +13,7 @@ parameter gradients accumulate straight into the flat-arena ``.grad`` views (wei
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -28,6 +29,10 @@ _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_go_head", [_P, _P, _P, _P, ctypes.c_long, ctypes.c_long, _P, _P, _P, _I, _I, _P])
+
+_lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P])
+_lib.register("pbx_pack_glob_frags", [_P, _P, _P, _I, _I, _P])
 
 LN_EPS = 1e-5
 BF16 = torch.bfloat16
@@ -145,6 +150,127 @@ class InputLayerFn(torch.autograd.Function):
                   st)
         addmm_into(dw, du.t(), ann_bf)
         return (None, *gr.finish())
+
+
+def _ptrs(*ts) -> ctypes.Array:
+    arr = (ctypes.c_void_p * len(ts))()
+    for i, t in enumerate(ts):
+        arr[i] = None if t is None else t.data_ptr()
+    return arr
+
+
+# one-launch global-track kernels (csrc/glob2.hip); PBX_GLOBAL_FUSED=0 selects the library-GEMM path
+GLOBAL_FUSED = os.environ.get("PBX_GLOBAL_FUSED", "1") != "0"
+
+
+def glob_fused_ok(G: int, NGL: int) -> bool:
+    """Shapes the fused global-track kernels are compiled for (pbx_glob_supported)."""
+    return GLOBAL_FUSED and G in (256, 512) and NGL in (0, 128)
+
+
+_lib.register("pbx_pack_batch", [_P, _P, _I, _P])
+
+
+def pack_batch(items) -> None:
+    """One launch building every weight image: items are ``(kind, w, out1, out2, n, k)`` with kind 0 =
+    conv fragments (``n`` = taps) and kind 1 = Linear fragments (``n`` x ``k``)."""
+    if not items:
+        return
+    for i in range(0, len(items), 40):
+        chunk = items[i:i + 40]
+        ptrs = (ctypes.c_void_p * (3 * len(chunk)))()
+        meta = (ctypes.c_int * (3 * len(chunk)))()
+        for j, (kind, w, o1, o2, n, k) in enumerate(chunk):
+            ptrs[3 * j], ptrs[3 * j + 1], ptrs[3 * j + 2] = w.data_ptr(), o1.data_ptr(), o2.data_ptr()
+            meta[3 * j], meta[3 * j + 1], meta[3 * j + 2] = n, k, kind
+        _lib.call("pbx_pack_batch", ptrs, meta, len(chunk), _s(chunk[0][1].device))
+
+
+def pack_glob(w: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """fp32 ``[N, K]`` Linear weight -> bf16 B-fragment images for ``X W^T`` and ``dU W``."""
+    N, K = w.shape
+    ff = torch.empty((N * K,), dtype=BF16, device=w.device)
+    fb = torch.empty_like(ff)
+    _lib.call("pbx_pack_glob_frags", w.detach().contiguous().data_ptr(), ff.data_ptr(), fb.data_ptr(), N, K,
+              _s(w.device))
+    return ff, fb
+
+
+class FusedGlobalBlockFn(torch.autograd.Function):
+    """The global track of one block as ONE kernel forward and ONE kernel backward (``csrc/glob2.hip``;
+    the three weight-gradient GEMMs go to the aux stream).  Same math and outputs as
+    :class:`GlobalBlockFn`."""
+
+    @staticmethod
+    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl, packed=None):
+        """``packed``: the six fragment images (f1, f1T, f2, f2T, fgl, fglT) already built by
+        :func:`pack_batch` for this step, else they are built here."""
+        dev = g.device
+        B, G = g.shape
+        TV = vpart.shape[1]
+        K = wp.numel()
+        NGL = 0 if wgl is None else wgl.shape[0]
+        if packed is not None:
+            f1, f1T, f2, f2T, fgl, fglT = packed
+        else:
+            f1, f1T = pack_glob(w1)
+            f2, f2T = pack_glob(w2)
+            fgl, fglT = pack_glob(wgl) if NGL else (None, None)
+        e = lambda *shape, dt=F32: torch.empty(shape, dtype=dt, device=dev)  # noqa: E731
+        pre1, xh1, vsum, pre2, xh2, g2 = e(B, G), e(B, G), e(B, G), e(B, G), e(B, G), e(B, G)
+        r1, r2 = e(B), e(B)
+        g1_bf, g2_bf = e(B, G, dt=BF16), e(B, G, dt=BF16)
+        pregl, gb = (e(B, NGL), e(B, NGL)) if NGL else (None, torch.zeros((B, 0), dtype=F32, device=dev))
+        vp = vpart.contiguous()
+        _lib.call("pbx_glob_fwd", _ptrs(g.contiguous(), g_bf.contiguous(), vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                        fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                        gb if NGL else None),
+                  B, G, NGL, TV, K, LN_EPS, _s(dev))
+        ctx.save_for_backward(g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT)
+        ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
+        ctx.meta = (TV, NGL)
+        ctx.mark_non_differentiable(g2_bf)
+        ctx.set_materialize_grads(False)
+        return g2, g2_bf, gb
+
+    @staticmethod
+    def backward(ctx, dg2, _dg2bf, dgb):
+        g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT = ctx.saved_tensors
+        w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl = ctx.params
+        TV, NGL = ctx.meta
+        dev = pre1.device
+        B, G = pre1.shape
+        gr = _Grads([w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl])
+        dw1, db1, dn1w, dn1b, dw2, db2, dn2w, dn2b, dwp, dwgl, dbgl = gr.dst
+        dg2 = torch.zeros((B, G), dtype=F32, device=dev) if dg2 is None else dg2.float().contiguous()
+        if NGL:
+            dgb = torch.zeros((B, NGL), dtype=F32, device=dev) if dgb is None else dgb.float().contiguous()
+        else:
+            dgb = None
+        dg = torch.empty((B, G), dtype=F32, device=dev)
+        dvs = torch.empty((B, G), dtype=F32, device=dev)
+        du1 = torch.empty((B, G), dtype=BF16, device=dev)
+        du2 = torch.empty((B, G), dtype=BF16, device=dev)
+        dugl = torch.empty((B, NGL), dtype=BF16, device=dev) if NGL else None
+        _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum, wp,
+                                        f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
+                                        dbgl if NGL else None, dwp),
+                  B, G, NGL, wp.numel(), _s(dev))
+
+        def weight_grads():
+            addmm_into(dw1, du1.t(), g_bf)
+            addmm_into(dw2, du2.t(), g1_bf)
+            if NGL:
+                addmm_into(dwgl, dugl.t(), g2_bf)
+
+        direct = all(gr.direct[i] for i in (0, 4)) and (not NGL or gr.direct[9])
+        if direct and streams.ENABLED and dev.type == "cuda":
+            # dW = dU^T X (K = B rows) is off the critical path: the aux (weight-gradient) stream
+            streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf], name="wgrad")
+        else:
+            weight_grads()
+        dvpart = dvs.unsqueeze(1).expand(B, TV, G)
+        return (dg, None, dvpart, *gr.finish(), None)
 
 
 class GlobalBlockFn(torch.autograd.Function):

@@ -143,7 +143,8 @@ class LocalBlockFn(torch.autograd.Function):
     """Fused local track of one block (reference semantics)."""
 
     @staticmethod
-    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int):
+    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None):
+        """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch)."""
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
         B, L, C = x.shape
         assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -153,8 +154,11 @@ class LocalBlockFn(torch.autograd.Function):
         BM1 = conv_tile(L)
         T1 = (L + BM1 - 1) // BM1
         T2 = (L + PB - 1) // PB
-        wpn, wtn = pack_conv(wn)
-        wpw, wtw = pack_conv(ww)
+        if packed is not None:
+            wpn, wtn, wpw, wtw = packed
+        else:
+            wpn, wtn = pack_conv(wn)
+            wpw, wtw = pack_conv(ww)
         wl_b = bf16_of(wl)
         gb = gb.detach().float().contiguous()
         pre_n = torch.empty_like(x)
@@ -243,7 +247,7 @@ class LocalBlockFn(torch.autograd.Function):
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None)
+        return (dx, dgb, *pgrads, None, None, None)
 
 
 class EmbedFn(torch.autograd.Function):
@@ -287,7 +291,17 @@ def _wv_bf16(att) -> torch.Tensor:
     return cached[1]
 
 
-def local_block(x: torch.Tensor, gb: torch.Tensor, blk) -> Tuple[torch.Tensor, torch.Tensor]:
+def conv_images(wn: torch.Tensor, ww: torch.Tensor):
+    """Output buffers of one block's conv weight images and their pack_batch items (v3 form), or
+    ``(None, [])`` when the selected conv form packs per call."""
+    if CONV_IMPL != "v3":
+        return None, []
+    KS = wn.shape[2]
+    imgs = tuple(torch.empty((KS, CH, CH), dtype=torch.bfloat16, device=wn.device) for _ in range(4))
+    return imgs, [(0, wn.detach(), imgs[0], imgs[1], KS, 0), (0, ww.detach(), imgs[2], imgs[3], KS, 0)]
+
+
+def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``)."""
     att = blk.global_attention_layer
     wv = _wv_bf16(att)                                                       # [H*vd, C]
@@ -295,4 +309,4 @@ def local_block(x: torch.Tensor, gb: torch.Tensor, blk) -> Tuple[torch.Tensor, t
     wc = blk.local_wide_conv_layer[0]
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
-                              blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation)
+                              blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed)
