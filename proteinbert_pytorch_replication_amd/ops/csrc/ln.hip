@@ -296,7 +296,8 @@ __global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
 // Work items are 32-position wave tiles taken by each wave independently (no workgroup barrier
 // after the Wv staging, so the waves of a CU drift apart and one wave's loads overlap another's
 // MFMAs), and the LN2 partials are written per wave tile: sums2[b][ceil(L/32)][2].
-__global__ void __launch_bounds__(512) attn_bwd_kernel(
+template <int MAXT>   // 512: 8 waves at <= 256 VGPRs; 256: 4 waves (one per SIMD) at <= 512 VGPRs
+__global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
     const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, int NJ,
@@ -313,8 +314,6 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
   const int NJT = NJ / 32;
   const long items = (long)B * TW;
   const long stride = (long)gridDim.x * NW;
-  stage_weight(ws, wv, NJ);
-  __syncthreads();
   auto load_rows = [&](long item, bf16x8* f) {
     const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
     const int pos = tw * 32 + r;
@@ -326,6 +325,8 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
       f[kk] = __builtin_bit_cast(bf16x8, ok ? v : make_uint4(0u, 0u, 0u, 0u));
     }
   };
+  stage_weight(ws, wv, NJ);
+  __syncthreads();
   for (long item = (long)blockIdx.x * NW + w; item < items; item += stride) {
     const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
     const int pos0 = tw * 32;
@@ -337,7 +338,12 @@ __global__ void __launch_bounds__(512) attn_bwd_kernel(
     f32x16_t y[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    const float* dv = dvpart + ((size_t)b * TV + pos0 / BMV) * NJ;
+    // this tile's attention-gradient row dv[NJ] -> the wave's LDS slot (2 loads per lane, once per
+    // tile, instead of 4 dependent global loads per 32-column block inside the loop)
+    const float* dvg = dvpart + ((size_t)b * TV + pos0 / BMV) * NJ;
+    float* dv = reinterpret_cast<float*>(ws + NJ * 256) + w * NJ;
+    for (int i = lane * 4; i < NJ; i += 256) *reinterpret_cast<float4*>(dv + i) = *reinterpret_cast<const float4*>(dvg + i);
+    __builtin_amdgcn_wave_barrier();
     const bool full = pos0 + 32 <= L;
     auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
@@ -774,7 +780,8 @@ static bool ln_attrs_set = false;
 static void set_ln_attrs() {
   if (ln_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -818,12 +825,15 @@ PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, co
                             const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
                             int NJ, int nw, float eps, hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 > 163840 || nw < 1 || nw > 8 || bmv % 32 != 0) return (int)hipErrorInvalidValue;
+  if (NJ % 64 != 0 || NJ * 256 + nw * NJ * 4 > 163840 || nw < 1 || nw > 8 || bmv % 32 != 0)
+    return (int)hipErrorInvalidValue;
   const long items = (long)B * ((L + 31) / 32);
   long wgl = (items + nw - 1) / nw;
   if (wgl > num_cus()) wgl = num_cus();
   const int wgs = (int)wgl;
-  hipLaunchKernelGGL(attn_bwd_kernel, dim3(wgs), dim3(64 * nw), NJ * 256, st, (const bf16_t*)h2, (const bf16_t*)s2,
+  hipLaunchKernelGGL(nw > 4 ? attn_bwd_kernel<512> : attn_bwd_kernel<256>, dim3(wgs), dim3(64 * nw),
+                     NJ * 256 + nw * NJ * 4, st, (const bf16_t*)h2,
+                     (const bf16_t*)s2,
                      st2, g2, (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ,
                      eps);
   return pbx_launch_status();
