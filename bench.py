@@ -45,7 +45,12 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: preset)")
     ap.add_argument("--seq-len", type=int, default=None)
-    ap.add_argument("--preset", default="cfg2_paper_l512")
+    ap.add_argument("--preset", default=None, help="config preset (default: cfg2_paper_l512, or "
+                    "cfg5_finetune_ss_l512_dp8 with --mode finetune)")
+    ap.add_argument("--mode", default="pretrain", choices=["pretrain", "finetune"],
+                    help="pretrain: the headline step; finetune: BASELINE cfg 5, frozen encoder + per-residue "
+                         "8-state secondary-structure head")
+    ap.add_argument("--classes", type=int, default=8, help="fine-tune head classes (secondary structure)")
     ap.add_argument("--impl", default="hip", choices=["hip", "torch", "faithful"],
                     help="hip: fused CDNA4 kernels; torch: eager bf16 oracle; faithful: reference math, eager fp32")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
@@ -62,7 +67,7 @@ def main():
     if info.world_size != a.gpus and not (a.gpus == 1 and info.world_size == 1):
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
     dev = info.device
-    cfg = get_preset(a.preset)
+    cfg = get_preset(a.preset or ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else "cfg2_paper_l512"))
     mcfg = cfg.model
     L = a.seq_len or mcfg.sequences_length
     B = a.batch or cfg.train.batch_size
@@ -71,6 +76,8 @@ def main():
     model = ProteinBERT(sequences_length=L, num_annotations=mcfg.num_annotations, local_dim=mcfg.local_dim,
                         global_dim=mcfg.global_dim, key_dim=mcfg.key_dim, num_heads=mcfg.num_heads,
                         num_blocks=mcfg.num_blocks, device=dev, backend=backend)
+    if a.mode == "finetune":
+        return finetune_bench(a, info, model, L, B, mcfg)
     opt = FusedAdam(model.parameters(), lr=2e-4)
     ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb) if info.distributed else None
     if ddp is not None:
@@ -138,6 +145,71 @@ def main():
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
                           "impl": a.impl, "hip_graph": graphed},
                "final_loss": round(final_loss, 5)}
+        print(json.dumps(out), flush=True)
+    pdist.destroy()
+
+
+def _timed(one, a, info, dev):
+    for _ in range(a.warmup):
+        loss = one()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = one()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    pdist.barrier()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    return pdist.all_reduce_max(time.perf_counter() - t0, dev), loss
+
+
+def finetune_bench(a, info, encoder, L, B, mcfg):
+    """BASELINE cfg 5: the fine-tune step of a frozen pretrained encoder (random-init here) with a
+    per-residue secondary-structure head (reference train_step contract, utils.py:110-168: CE over
+    dim 1, gradient clipping at 1.0), synthetic tokens/labels; DP all-reduces the head gradients."""
+    import torch.nn.functional as F
+    from proteinbert_pytorch_replication_amd.models.finetune import ProteinBERTForTokenClassification
+    dev = info.device
+    model = ProteinBERTForTokenClassification(encoder, n_classes=a.classes, freeze_encoder=True)
+    opt = FusedAdam([p for p in model.parameters() if p.requires_grad], lr=1e-3)
+    ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb) if info.distributed else None
+    if ddp is not None:
+        ddp.broadcast_parameters(model)
+    gen = SyntheticUniRefGO(L, mcfg.num_annotations, B, dev, seed=a.seed + 1000 * info.rank)
+    g = torch.Generator(device=dev)
+    g.manual_seed(a.seed + 7 + info.rank)
+
+    def one():
+        X, Y, _ = gen.next_batch()
+        y = torch.randint(0, a.classes, Y["local"].shape, device=dev, generator=g)
+        y = torch.where(Y["local"] == 0, torch.full_like(y, -100), y)          # padding is ignored
+        opt.zero_grad()
+        loss = F.cross_entropy(model(X), y, ignore_index=-100)
+        loss.backward()
+        if ddp is not None:
+            ddp.finish(average=False)
+        opt.clip_grad_norm_(1.0)
+        opt.step()
+        return loss.detach()
+
+    dt, loss = _timed(one, a, info, dev)
+    n = info.world_size
+    value = n * B * a.steps / dt
+    if info.is_main:
+        out = {"metric": "sequences/sec (whole node) ProteinBERT fine-tune (frozen encoder + per-residue "
+                         f"{a.classes}-state head) L={L}", "value": round(value, 2), "unit": "sequences/s",
+               "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+               "data": "synthetic (on-device tokens, random per-residue labels, random-init weights)",
+               "config": {"model": f"ProteinBERT paper config encoder (frozen) + Linear({mcfg.local_dim}+"
+                                   f"{mcfg.global_dim} -> {a.classes}) per residue",
+                          "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
+                          "impl": a.impl}, "final_loss": round(float(loss.item()), 5)}
         print(json.dumps(out), flush=True)
     pdist.destroy()
 

@@ -63,6 +63,8 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     ap.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--async-checkpoint", action="store_true")
+    ap.add_argument("--profile-steps", default=None, help="START[:COUNT] steps traced with torch.profiler")
+    ap.add_argument("--profile-dir", default=None, help="trace output directory (default: save path)")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(format="%(asctime)s [%(levelname)s]: %(message)s", level=logging.INFO)
@@ -99,7 +101,7 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
                    optim_scheduler_patience=cfg.optim.plateau_patience, warmup_duration=cfg.optim.warmup_duration,
                    device=dev, log_every=a.log_every, bucket_mb=cfg.dist.bucket_mb, compute_dtype=cfg.kernel.dtype,
                    grad_clip=cfg.optim.grad_clip, async_checkpoint=a.async_checkpoint, metrics_path=a.metrics,
-                   resume=a.resume)
+                   resume=a.resume, profile_steps=a.profile_steps, profile_dir=a.profile_dir)
     if info.is_main:
         print(json.dumps({"final_loss": res["train_loss"][-1] if res["train_loss"] else None,
                           "iterations": len(res["train_loss"]), "final_model": res.get("final_model_path")}))

@@ -26,6 +26,7 @@ from typing import Any, Dict, Optional
 
 import torch
 
+from ..utils.profiling import StepProfiler, marker
 from ..parallel import dist as pdist
 from ..parallel.ddp import BucketedAllReduce
 from .checkpoint import (CheckpointWriter, build_checkpoint, checkpoint_name, latest_checkpoint, load_checkpoint,
@@ -68,7 +69,8 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
              loaded_checkpoint: Optional[Dict[str, Any]] = None, device=None, *,
              log_every: int = 1, bucket_mb: float = 8.0, compute_dtype="auto", grad_clip: Optional[float] = None,
              async_checkpoint: bool = False, metrics_path: Optional[str] = None, resume: str = "none",
-             fuse_optimizer: bool = True, final_save: bool = True) -> Dict[str, Any]:
+             fuse_optimizer: bool = True, final_save: bool = True, profile_steps: Optional[str] = None,
+             profile_dir: Optional[str] = None) -> Dict[str, Any]:
     info = pdist.init_distributed()
     if device is None:
         device = info.device
@@ -112,6 +114,7 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             train_dataloader.load_state_dict(extra["loader"])
         logging.info("Checkpoint loaded!")
 
+    profiler = StepProfiler.from_spec(profile_steps, profile_dir or save_path, info.rank)
     fault_at = int(os.environ.get("PBX_FAULT_AT_STEP", "0") or 0)
     fault_rank = int(os.environ.get("PBX_FAULT_RANK", "0") or 0)
     model.train()
@@ -125,10 +128,17 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             progressed = True
             start_time = time.time()
             X, Y, W = _to_device(X, device), _to_device(Y, device), _to_device(W, device)
-            loss = step_fn(X, Y, W)
+            if profiler is not None:
+                profiler.before_step(current + 1)
+            with marker("pbx/step"):
+                loss = step_fn(X, Y, W)
             loss_acc += loss.float()
             n_acc += 1
             current += 1
+            if profiler is not None:
+                profiler.after_step(current)
+                if profiler.trace_path:
+                    results["profile_trace"] = profiler.trace_path
             if scheduler.in_warmup:
                 scheduler.step(None)
             if fault_at and current == fault_at and info.rank == fault_rank:

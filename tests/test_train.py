@@ -112,3 +112,22 @@ def test_checkpoint_loads_into_reference(reference_modules, tmp_path):
     m2 = _model(seed=5)
     load_reference_checkpoint(m2, {"model_state_dict": ref.state_dict()})
     torch.testing.assert_close(m2.state_dict()["local_embedding.weight"], ref.state_dict()["local_embedding.weight"])
+
+
+def test_pretrain_profile_window_writes_trace(tmp_path):
+    """a torch.profiler window over steps 2-3 -> Chrome trace + kernel table."""
+    m = _model()
+    gen = SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=1, use_kernel=False)
+
+    class _Loader:
+        def __iter__(self):
+            while True:
+                yield gen.next_batch()
+
+    res = pretrain(m, _Loader(), torch.optim.Adam(m.parameters(), lr=1e-3), max_batch_iterations=4,
+                   save_path=str(tmp_path), nb_iterations_checkpoint=100, warmup_duration=2, final_save=False,
+                   profile_steps="2:2")
+    trace = res["profile_trace"]
+    assert os.path.exists(trace) and os.path.getsize(trace) > 0
+    assert os.path.exists(trace.replace(".json", ".txt"))
+    assert "steps2-3" in trace
