@@ -348,7 +348,9 @@ __global__ void __launch_bounds__(256) local_head_kernel(
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
 }
 
-// MFMA version of the local head (B <= 512): one workgroup (4 waves) per position l.
+// MFMA version of the local head (B <= 608): one workgroup (4 waves) per position l; the h_l rows
+// pass through LDS in chunks of HC = 128 rows (twice: logits, then dWo), so the LDS holds only the
+// [B][32] logit / dz tiles at full batch size.
 //   logits  Z[b][v]   = h_l[b] . Wo[v] + bo[v]       (MFMA: A = h_l rows, B = Wo rows)
 //   softmax over b, CE on the probabilities, dz      (VALU on the [B][32] logit tile, as above)
 //   dWo_l[v][c]       = sum_b dz[b][v] h_l[b][c]     (MFMA: both operands transposed LDS reads)
@@ -358,9 +360,10 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, float* __restrict__ dwo_part,
     float* __restrict__ dbo_part, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int HC = 128;
   const int Bp = (B + 31) & ~31;
-  unsigned char* hs = smem;                                   // [Bp][128] bf16 swz256 (later: dh tile)
-  unsigned char* wos = hs + Bp * 256;                         // [32][128] bf16 swz256
+  unsigned char* hs = smem;                                   // [HC][128] bf16 swz256 (h_l / dh chunk)
+  unsigned char* wos = hs + HC * 256;                         // [32][128] bf16 swz256
   unsigned char* dzb = wos + 32 * 256;                        // [Bp][32] bf16, 64-B rows
   float* zs = reinterpret_cast<float*>(dzb + Bp * 64);        // [Bp][32] fp32
   float* red = zs + Bp * 32;                                  // [8][32]
@@ -369,15 +372,18 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
   const int r = lane & 31, hh = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int l = blockIdx.x;
-  // stage h_l rows (zero beyond B) and Wo (bf16, zero rows beyond V)
-  stage_chunks(
-      Bp * 16,
-      [&](int idx) {
-        const int b = idx >> 4;
-        return b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
-                     : make_uint4(0u, 0u, 0u, 0u);
-      },
-      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = v; });
+  // h_l rows c0 .. c0 + HC - 1 -> hs (zero beyond B)
+  auto stage_h = [&](int c0) {
+    stage_chunks(
+        HC * 16,
+        [&](int idx) {
+          const int b = c0 + (idx >> 4);
+          return b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
+                       : make_uint4(0u, 0u, 0u, 0u);
+        },
+        [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = v; });
+  };
+  // Wo (bf16, zero rows beyond V)
   for (int idx = tid; idx < 32 * 16; idx += 256) {
     const int v = idx >> 4, c8 = idx & 15;
     float e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -388,18 +394,23 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     }
     *reinterpret_cast<uint4*>(wos + swz256(v, c8)) = packq8(e);
   }
-  __syncthreads();
-  // logits
+  // logits, one h chunk at a time (wave w -> row tile w of the chunk)
   const float bov = r < V ? bo[r] : 0.f;
-  for (int rt = w; rt < Bp / 32; rt += 4) {
-    f32x16_t acc = zero16();
+  for (int c0 = 0; c0 < Bp; c0 += HC) {
+    __syncthreads();                            // previous chunk consumed
+    stage_h(c0);
+    __syncthreads();
+    const int rt = c0 / 32 + w;
+    if (rt < Bp / 32) {
+      f32x16_t acc = zero16();
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk)
-      acc = mfma32(lds_frag(hs, swz256(rt * 32 + r, kk * 2 + hh)), lds_frag(wos, swz256(r, kk * 2 + hh)), acc);
+      for (int kk = 0; kk < 8; ++kk)
+        acc = mfma32(lds_frag(hs, swz256(w * 32 + r, kk * 2 + hh)), lds_frag(wos, swz256(r, kk * 2 + hh)), acc);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int b = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-      zs[b * 32 + r] = acc[i] + bov;
+      for (int i = 0; i < 16; ++i) {
+        const int b = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+        zs[b * 32 + r] = acc[i] + bov;
+      }
     }
   }
   __syncthreads();
@@ -502,15 +513,22 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(dzb + b * 64 + c * 16) = packq8(dzv + 8 * c);
   }
   __syncthreads();
-  // dWo_l: wave w -> channel tile w;  D[v][c] = sum_b dz^T[v][b] h[b][c]
+  // dWo_l: wave w -> channel tile w;  D[v][c] = sum_b dz^T[v][b] h[b][c]  (h chunks re-staged)
   {
     f32x16_t acc = zero16();
     const int colb = w * 32 + tc;
-    for (int kb = 0; kb < Bp / 16; ++kb) {
-      const int ra = kb * 16 + 8 * hh + q;
-      const bf16x8 fa = cat_tr(lds_tr(dzb, ra * 64 + tc * 2), lds_tr(dzb, (ra + 4) * 64 + tc * 2));
-      const bf16x8 fb = cat_tr(lds_tr(hs, swz256e(ra, colb)), lds_tr(hs, swz256e(ra + 4, colb)));
-      acc = mfma32(fa, fb, acc);
+    for (int c0 = 0; c0 < Bp; c0 += HC) {
+      __syncthreads();
+      stage_h(c0);
+      __syncthreads();
+      const int nkb = min(HC, Bp - c0) / 16;
+      for (int kb = 0; kb < nkb; ++kb) {
+        const int ra = kb * 16 + 8 * hh + q;
+        const bf16x8 fa =
+            cat_tr(lds_tr(dzb, (c0 + ra) * 64 + tc * 2), lds_tr(dzb, (c0 + ra + 4) * 64 + tc * 2));
+        const bf16x8 fb = cat_tr(lds_tr(hs, swz256e(ra, colb)), lds_tr(hs, swz256e(ra + 4, colb)));
+        acc = mfma32(fa, fb, acc);
+      }
     }
     float* dst = dwo_part + (size_t)l * V * 128;
 #pragma unroll
@@ -524,9 +542,12 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     for (int b = 0; b < B; ++b) a += zs[b * 32 + tid];
     dbo_part[(size_t)l * V + tid] = a;
   }
-  __syncthreads();   // hs no longer read: it becomes the dh staging tile
-  // dh: D[b][c] = sum_v dz[b][v] Wo[v][c];  wave -> row tiles, all 4 channel tiles
-  for (int rt = w; rt < Bp / 32; rt += 4) {
+  // dh: D[b][c] = sum_v dz[b][v] Wo[v][c]; per chunk: wave -> row tile, all 4 channel tiles, staged
+  // in hs for 256-B row stores
+  for (int c0 = 0; c0 < Bp; c0 += HC) {
+    __syncthreads();                            // hs free (previous chunk stored / dWo done)
+    const int rt = c0 / 32 + w;
+    if (rt < Bp / 32) {
     f32x16_t acc[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
@@ -545,17 +566,19 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int b = rt * 32 + 8 * g + 4 * hh;   // rows b .. b+3 (reg = 4g + e), column ct*32 + r
+        const int b = w * 32 + 8 * g + 4 * hh;    // chunk rows b .. b+3 (reg = 4g + e), column ct*32 + r
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           *reinterpret_cast<bf16_t*>(hs + swz256e(b + e, ct * 32 + r)) = f2bf(acc[ct][4 * g + e]);
       }
-  }
-  __syncthreads();
-  for (int idx = tid; idx < B * 16; idx += 256) {
-    const int b = idx >> 4, c8 = idx & 15;
-    *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
-        *reinterpret_cast<const uint4*>(hs + swz256(b, c8));
+    }
+    __syncthreads();
+    for (int idx = tid; idx < HC * 16; idx += 256) {
+      const int b = c0 + (idx >> 4), c8 = idx & 15;
+      if (b < B)
+        *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
+            *reinterpret_cast<const uint4*>(hs + swz256(idx >> 4, c8));
+    }
   }
   lsum = wave_reduce_sum(lsum);
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
@@ -644,7 +667,7 @@ PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, c
     attr = true;
   }
   const int Bp = (B + 31) & ~31;
-  const int lds_m = Bp * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (8 * 32 + 96) * 4;
+  const int lds_m = 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (8 * 32 + 96) * 4;
   if (lds_m <= 163840) {
     hipLaunchKernelGGL(local_head_mfma_kernel, dim3(L), dim3(256), lds_m, st, (const bf16_t*)h, wo, bo,
                        (const long long*)y, wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V,
