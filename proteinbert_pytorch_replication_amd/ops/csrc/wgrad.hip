@@ -1,0 +1,245 @@
+// Conv weight gradient, LDS-DMA pipelined form (SURVEY K3 backward; reference conv layers
+// ProteinBERT/modules.py:185-199 -- there it is autograd's cuDNN wgrad).
+//
+//   dW[co][ci][k] = sum_{b,pos} dy[b][pos][co] * x[b][pos + (k - 4) d][ci],   db[co] = sum dy[b][pos][co]
+//
+// One workgroup (8 waves, ONE per CU) owns one (conv, 64-co half) "type" and a contiguous run of
+// 128-position tiles ("chunk").  Wave w owns input channels 32(w&3).. for both 32-co tiles and
+// taps 0-4 (waves 0-3) or 5-8 (waves 4-7): <= 10 x 32x32 fp32 accumulators, so two waves share a
+// SIMD within 256 registers each, and every x fragment read from LDS feeds two MFMAs (the previous
+// form, one 32-co tile per wave, needed one LDS fragment per MFMA and staged synchronously: ~19 %
+// of MFMA peak).  (One wave per SIMD holding all 9 taps = 288 accumulator registers does not fit
+// the 256 AGPRs: hipcc shuffles accumulators through VGPR copies around every MFMA.)
+//
+// Staging is asynchronous global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave instruction,
+// lane-linear destination) into two LDS buffers: the loads of tile t+1 are issued before the MFMAs
+// of tile t, and one barrier per tile retires them.  The x tile keeps the swz256 image of the other
+// kernels by permuting the per-lane SOURCE chunk (the destination of a DMA cannot be permuted);
+// rows outside the sequence (conv zero padding) read a 16-byte zero block.
+//
+// Partials go to fp32 slabs in tap-major layout [chunk][conv][k][co][ci] (each store instruction
+// covers 2 x 128 contiguous bytes); wgrad2_reduce sums the chunks in fixed order (deterministic)
+// and adds into the torch layouts [co][ci][k] (the flat-arena .grad views).
+#include "mfma.h"
+
+using namespace pbx;
+typedef unsigned short bf16_t;
+
+namespace {
+constexpr int CH = 128;
+
+constexpr int BM = 128;          // positions per tile
+constexpr int KS = 9;
+
+__device__ __attribute__((aligned(16))) unsigned int g_zero16[4];   // zero-initialised device global
+
+// One 1-KiB LDS-DMA wave instruction: lane i's 16 source bytes land at lds_base + 16 i.  Issued as
+// inline asm so hipcc does not treat every later ds_read as a possible alias of the in-flight DMA
+// (with the builtin it waits vmcnt(0) before the first LDS read after the issue, serialising the
+// prefetch with the MFMAs); completion is waited explicitly before the barrier that publishes it.
+__device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
+// The tile loop of one wave: NTAP taps k0.. of input-channel tile cig, both 32-co tiles.
+template <int NTAP, typename StageF>
+__device__ __forceinline__ void wgrad_tiles(unsigned char* smem, int buf_bytes, long t0, long t1, StageF& stage,
+                                            f32x16_t (&acc0)[5], f32x16_t (&acc1)[5], float& bsum, int halo,
+                                            int d, int k0, int cig, int lane) {
+  const int h = lane >> 5, q = tr_q(lane), tc = tr_c(lane);
+  // LDS byte offsets at kk = 0; K-step kk adds kk * 16 rows (swz256's XOR depends on row & 15 only)
+  const int aoff = (8 * h + q) * 64 + tc * 2;
+  int xoff[NTAP], xoff4[NTAP];
+#pragma unroll
+  for (int j = 0; j < NTAP; ++j) {
+    const int rb = halo + 8 * h + q + (k0 + j - KS / 2) * d;
+    xoff[j] = BM * 128 + swz256e(rb, cig * 32 + tc);
+    xoff4[j] = BM * 128 + swz256e(rb + 4, cig * 32 + tc);
+  }
+  // bias partial: every wave sums its co-tile-(cig & 1) A fragments (only waves 0 and 1 are kept)
+  const bool bias_b = (cig & 1) != 0;
+  if (t0 < t1) stage(t0, smem);
+  for (long tile = t0; tile < t1; ++tile) {
+    unsigned char* cur = smem + ((tile - t0) & 1) * buf_bytes;
+    unsigned char* nxt = smem + (((tile - t0) & 1) ^ 1) * buf_bytes;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of `cur` landed
+    __syncthreads();                                   // ... every wave's; `nxt` no longer read
+    if (tile + 1 < t1) stage(tile + 1, nxt);
+#pragma unroll
+    for (int kk = 0; kk < BM / 16; ++kk) {
+      const unsigned char* c = cur + kk * 16 * 64;     // dy rows advance 16 x 64 B
+      const unsigned char* cx = cur + kk * 16 * 256;   // x rows advance 16 x 256 B
+      const bf16x8 fa0 = cat_tr(lds_tr(c, aoff), lds_tr(c, aoff + 256));
+      const bf16x8 fa1 = cat_tr(lds_tr(c, BM * 64 + aoff), lds_tr(c, BM * 64 + aoff + 256));
+      {
+        typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+        const u32x4 u = __builtin_bit_cast(u32x4, bias_b ? fa1 : fa0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          bsum += __builtin_bit_cast(float, u[e] << 16) + __builtin_bit_cast(float, u[e] & 0xffff0000u);
+      }
+#pragma unroll
+      for (int j = 0; j < NTAP; ++j) {
+        const bf16x8 fb = cat_tr(lds_tr(cx, xoff[j]), lds_tr(cx, xoff4[j]));
+        acc0[j] = mfma32(fa0, fb, acc0[j]);
+        acc1[j] = mfma32(fa1, fb, acc1[j]);
+      }
+    }
+  }
+}
+
+// LDS buffer layout: dy sub-tile 0 [BM][64 B] | dy sub-tile 1 [BM][64 B] | x [XRM][256 B] swz256
+__global__ void __launch_bounds__(512, 1) wgrad2_kernel(const bf16_t* __restrict__ dy0, const bf16_t* __restrict__ dy1,
+                                                        const bf16_t* __restrict__ x, float* __restrict__ slab,
+                                                        float* __restrict__ bslab, int B, int L, int dil1,
+                                                        int nconv, int R, int buf_bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int ntypes = nconv * 2;
+  int type, chunk;
+  if ((R & 7) == 0) {
+    // the types of one chunk stage the same x rows: ids congruent mod 8 -> one XCD's L2
+    const int id = blockIdx.x, j = id >> 3;
+    chunk = (j / ntypes) * 8 + (id & 7);
+    type = j - (j / ntypes) * ntypes;
+  } else {
+    chunk = blockIdx.x / ntypes;
+    type = blockIdx.x - chunk * ntypes;
+  }
+  const int cv = type >> 1, half = type & 1;
+  const bf16_t* dy = cv ? dy1 : dy0;
+  const int d = cv ? dil1 : 1;
+  const int halo = (KS / 2) * d;
+  const int XR = BM + 2 * halo;               // x rows per tile (multiple of 4: 2*halo = 8d)
+  // wave index through readfirstlane: hipcc cannot prove threadIdx.x / 64 uniform, and the staging
+  // loop and the tap split branch on it
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  // wave w: input channels (w & 3)*32.. for taps k0 .. k0+NTAP-1 (waves 0-3: taps 0-4, 4-7: taps 5-8)
+  const int cig = w & 3;
+  const int k0 = w < 4 ? 0 : 5;
+  const int ntap = w < 4 ? 5 : 4;     // (the tile loop takes them as template / argument)
+  const int T = (L + BM - 1) / BM;
+  const long NT = (long)B * T;
+  const long t0 = NT * chunk / R, t1 = NT * (chunk + 1) / R;
+
+  // issue the DMA of one tile into buffer `buf` (instructions dealt round-robin to the 8 waves)
+  auto stage = [&](long tile, unsigned char* buf) {
+    const int b = (int)(tile / T), t = (int)(tile - (tile / T) * T);
+    const int pos0 = t * BM;
+    const size_t sbase = (size_t)b * L * CH;
+    const int n = 16 + XR / 4;
+    for (int i = w; i < n; i += 8) {
+      if (i < 16) {                            // dy: 16 rows x 64 B per instruction
+        const int sub = i >> 3, row = (i & 7) * 16 + (lane >> 2);
+        const int pos = pos0 + row;
+        const void* src = pos < L ? (const void*)(dy + sbase + (size_t)pos * CH + half * 64 + sub * 32 + (lane & 3) * 8)
+                                  : (const void*)g_zero16;
+        glds16(src, buf + sub * (BM * 64) + (i & 7) * 1024);
+      } else {                                 // x: 4 rows x 256 B per instruction, swz256 image
+        const int j = i - 16, row = j * 4 + (lane >> 4);
+        const int chunk16 = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const int pos = pos0 - halo + row;
+        const void* src = (pos >= 0 && pos < L) ? (const void*)(x + sbase + (size_t)pos * CH + chunk16 * 8)
+                                                : (const void*)g_zero16;
+        glds16(src, buf + BM * 128 + j * 1024);
+      }
+    }
+  };
+
+  f32x16_t acc0[5], acc1[5];
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    acc0[j] = zero16();
+    acc1[j] = zero16();
+  }
+  float bsum = 0.f;
+  if (w < 4)
+    wgrad_tiles<5>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 0, cig, lane);
+  else
+    wgrad_tiles<4>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 5, cig, lane);
+  // tap-major slab [chunk][conv][k][co][ci]; lane -> ci (32 lanes = 128 contiguous bytes)
+  float* dst = slab + ((size_t)chunk * nconv + cv) * KS * CH * CH + cig * 32 + r;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) {
+    if (j < ntap) {
+      const int k = k0 + j;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int co = half * 64 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        dst[((size_t)k * CH + co) * CH] = acc0[j][i];
+        dst[((size_t)k * CH + co + 32) * CH] = acc1[j][i];
+      }
+    }
+  }
+  if (w < 2) {
+    bsum += __shfl_xor(bsum, 32, 64);
+    if (h == 0) bslab[((size_t)chunk * nconv + cv) * CH + half * 64 + w * 32 + r] = bsum;
+  }
+}
+
+// sum the R tap-major slabs (fixed order) and ADD into weight [co][ci][KS] and bias [co]
+__global__ void __launch_bounds__(256) wgrad2_reduce_kernel(const float4* __restrict__ slab,
+                                                            const float* __restrict__ bslab, float* __restrict__ dw0,
+                                                            float* __restrict__ dw1, float* __restrict__ db0,
+                                                            float* __restrict__ db1, int R, int nconv) {
+  constexpr int per4 = KS * CH * CH / 4;
+  const int total4 = nconv * per4;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx < total4) {
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int rr = 0;
+    for (; rr + 4 <= R; rr += 4) {
+      const float4 a = slab[(size_t)rr * total4 + idx], b = slab[(size_t)(rr + 1) * total4 + idx];
+      const float4 c = slab[(size_t)(rr + 2) * total4 + idx], e = slab[(size_t)(rr + 3) * total4 + idx];
+      s.x += (a.x + b.x) + (c.x + e.x); s.y += (a.y + b.y) + (c.y + e.y);
+      s.z += (a.z + b.z) + (c.z + e.z); s.w += (a.w + b.w) + (c.w + e.w);
+    }
+    for (; rr < R; ++rr) {
+      const float4 a = slab[(size_t)rr * total4 + idx];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    const int cv = idx >= per4;
+    const int rem = idx - cv * per4;
+    const int k = rem / (CH * CH / 4), co = (rem / (CH / 4)) % CH, ci = (rem % (CH / 4)) * 4;
+    float* dw = (cv ? dw1 : dw0) + ((size_t)co * CH + ci) * KS + k;
+    dw[0] += s.x;
+    dw[KS] += s.y;
+    dw[2 * KS] += s.z;
+    dw[3 * KS] += s.w;
+  }
+  if (idx < nconv * CH) {
+    float s = 0.f;
+    for (int rr = 0; rr < R; ++rr) s += bslab[(size_t)rr * nconv * CH + idx];
+    float* db = idx >= CH ? db1 : db0;
+    if (db != nullptr) db[idx % CH] += s;
+  }
+}
+
+bool wgrad2_attr_set = false;
+}  // namespace
+
+// KS = 9 only.  slab: R * nconv * 9 * 128 * 128 floats; bslab: R * nconv * 128 floats.
+PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float* slab, float* bslab, float* dw0,
+                          float* dw1, float* db0, float* db1, int B, int L, int dil1, int nconv, int R,
+                          hipStream_t st) {
+  if (nconv < 1 || nconv > 2 || R < 1 || dil1 < 1) return (int)hipErrorInvalidValue;
+  const int halo_max = (KS / 2) * (nconv > 1 ? dil1 : 1);
+  const int buf = BM * 128 + (BM + 2 * halo_max) * 256;
+  if (2 * buf > 163840) return (int)hipErrorInvalidValue;
+  if (!wgrad2_attr_set) {
+    (void)hipFuncSetAttribute((const void*)wgrad2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    wgrad2_attr_set = true;
+  }
+  hipLaunchKernelGGL(wgrad2_kernel, dim3(nconv * 2 * R), dim3(512), 2 * buf, st, (const bf16_t*)dy0,
+                     (const bf16_t*)dy1, (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R, buf);
+  const int total4 = nconv * KS * CH * CH / 4;
+  hipLaunchKernelGGL(wgrad2_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, (const float4*)slab,
+                     bslab, dw0, dw1, db0, db1, R, nconv);
+  return pbx_launch_status();
+}

@@ -34,6 +34,7 @@ _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, 
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv", [_P, _P, _P, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
@@ -53,6 +54,9 @@ LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 # 128-position tiles, two workgroups per CU) or "v1" (csrc/conv.hip: weights staged through an LDS
 # ring, 256/128-position tiles, one workgroup per CU); PBX_CONV=v1 selects the latter.
 CONV_IMPL = os.environ.get("PBX_CONV", "v3")
+# conv weight-gradient form (k = 9): "v2" (csrc/wgrad.hip: LDS-DMA double buffer, 64 output channels
+# per workgroup, one workgroup per CU) or "v1" (csrc/conv.hip wgrad_kernel); PBX_WGRAD=v1 selects v1.
+WGRAD_IMPL = os.environ.get("PBX_WGRAD", "v2")
 
 
 def conv_tile(L: int) -> int:
@@ -125,6 +129,17 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     them alive while the launch may still be running on another stream)."""
     dev = x.device
     ntiles = B * ((L + 127) // 128)
+    if KS == 9 and WGRAD_IMPL == "v2":
+        # csrc/wgrad.hip: one workgroup per CU -> R chunks x (nconv x 2) channel halves = #CUs
+        R = int(os.environ.get("PBX_WGRAD_R", 0)) or max(8, (_num_cus(dev) // (2 * nconv)) // 8 * 8)
+        R = min(R, ntiles)
+        slab = torch.empty((R, nconv, KS, CH, CH), dtype=torch.float32, device=dev)
+        bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
+        (dw0, db0) = outs[0]
+        (dw1, db1) = outs[1] if nconv > 1 else (None, None)
+        _lib.call("pbx_wgrad2", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
+                  dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, dil, nconv, R, _lib.stream_ptr(dev))
+        return [slab, bslab]
     # position chunks: ~3/8 of a CU's worth of workgroups per conv type (R = 48 on 256 CUs), a
     # multiple of 8 for the XCD-aware mapping; measured best with the wgrad on the aux stream, where
     # it shares the chip with the main-stream backward kernels (R = 32/40/56/64/128 are slower)

@@ -118,3 +118,34 @@ for R in (32, 64, 128):
                                   bslab.data_ptr(), dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(), B,
                                   L, KS, dil, 2, R, 1, st))
     report(f"conv wgrad+reduce R={R}", us, conv_flops)
+
+# LDS-DMA form (csrc/wgrad.hip), checked against the v1 result of the same inputs
+pre_n.copy_((torch.randn(B, L, C, device=dev) * 0.5).to(bf))
+pre_w.copy_((torch.randn(B, L, C, device=dev) * 0.5).to(bf))
+ref = []
+for R, fn in ((48, "pbx_wgrad"), (64, "pbx_wgrad2")):
+    for t in (dw0, dw1, db0, db1):
+        t.zero_()
+    slab = torch.empty(R, 2, KS, C, C, device=dev)
+    bslab = torch.empty(R, 2, C, device=dev)
+    if fn == "pbx_wgrad":
+        call = lambda: _lib.call(fn, pre_n.data_ptr(), pre_w.data_ptr(), x.data_ptr(), slab.data_ptr(),  # noqa: E731
+                                 bslab.data_ptr(), dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(),
+                                 B, L, KS, dil, 2, R, 1, st)
+    else:
+        call = lambda: _lib.call(fn, pre_n.data_ptr(), pre_w.data_ptr(), x.data_ptr(), slab.data_ptr(),  # noqa: E731
+                                 bslab.data_ptr(), dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(),
+                                 B, L, dil, 2, R, st)
+    call()
+    torch.cuda.synchronize()
+    ref.append([t.clone() for t in (dw0, dw1, db0, db1)])
+    report(f"{fn} R={R}", timeit(call), conv_flops)
+for nm, u, v in zip(("dw_n", "dw_w", "db_n", "db_w"), ref[0], ref[1]):
+    print(f"  wgrad2 vs wgrad {nm}: max|diff| {float((u - v).abs().max()):.4g}  max|ref| {float(u.abs().max()):.3g}",
+          flush=True)
+for R in (32, 128):
+    slab = torch.empty(R, 2, KS, C, C, device=dev)
+    bslab = torch.empty(R, 2, C, device=dev)
+    report(f"pbx_wgrad2 R={R}", timeit(lambda: _lib.call(
+        "pbx_wgrad2", pre_n.data_ptr(), pre_w.data_ptr(), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
+        dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(), B, L, dil, 2, R, st)), conv_flops)
