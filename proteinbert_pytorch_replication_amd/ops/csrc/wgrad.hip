@@ -48,7 +48,7 @@ __device__ __forceinline__ void glds16(const void* src, unsigned char* lds_base)
 }
 
 // The tile loop of one wave: NTAP taps k0.. of input-channel tile cig, both 32-co tiles.
-template <int NTAP, typename StageF>
+template <int NTAP, int BIAS, typename StageF>   // BIAS: 0 none, 1 / 2: sum co tile 0 / 1
 __device__ __forceinline__ void wgrad_tiles(unsigned char* smem, int buf_bytes, long t0, long t1, StageF& stage,
                                             f32x16_t (&acc0)[5], f32x16_t (&acc1)[5], float& bsum, int halo,
                                             int d, int k0, int cig, int lane) {
@@ -62,8 +62,6 @@ __device__ __forceinline__ void wgrad_tiles(unsigned char* smem, int buf_bytes, 
     xoff[j] = BM * 128 + swz256e(rb, cig * 32 + tc);
     xoff4[j] = BM * 128 + swz256e(rb + 4, cig * 32 + tc);
   }
-  // bias partial: every wave sums its co-tile-(cig & 1) A fragments (only waves 0 and 1 are kept)
-  const bool bias_b = (cig & 1) != 0;
   if (t0 < t1) stage(t0, smem);
   for (long tile = t0; tile < t1; ++tile) {
     unsigned char* cur = smem + ((tile - t0) & 1) * buf_bytes;
@@ -71,25 +69,40 @@ __device__ __forceinline__ void wgrad_tiles(unsigned char* smem, int buf_bytes, 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of `cur` landed
     __syncthreads();                                   // ... every wave's; `nxt` no longer read
     if (tile + 1 < t1) stage(tile + 1, nxt);
-#pragma unroll
-    for (int kk = 0; kk < BM / 16; ++kk) {
+    // (K-step kk, tap j) steps s = kk * NTAP + j: the x fragment of step s + 2 (and the dy fragments
+    // of the next K-step) are read while the MFMA pair of step s runs -- a 3-slot register ring that
+    // keeps two LDS reads in flight ahead of the MFMAs without the VGPRs of a whole K-step
+    constexpr int NS = (BM / 16) * NTAP;
+    bf16x8 fa0[2], fa1[2], fb[3];
+    auto read_a = [&](int kk) {
       const unsigned char* c = cur + kk * 16 * 64;     // dy rows advance 16 x 64 B
-      const unsigned char* cx = cur + kk * 16 * 256;   // x rows advance 16 x 256 B
-      const bf16x8 fa0 = cat_tr(lds_tr(c, aoff), lds_tr(c, aoff + 256));
-      const bf16x8 fa1 = cat_tr(lds_tr(c, BM * 64 + aoff), lds_tr(c, BM * 64 + aoff + 256));
-      {
+      fa0[kk & 1] = cat_tr(lds_tr(c, aoff), lds_tr(c, aoff + 256));
+      fa1[kk & 1] = cat_tr(lds_tr(c, BM * 64 + aoff), lds_tr(c, BM * 64 + aoff + 256));
+    };
+    auto read_b = [&](int st) {
+      const unsigned char* cx = cur + (st / NTAP) * 16 * 256;   // x rows advance 16 x 256 B
+      fb[st % 3] = cat_tr(lds_tr(cx, xoff[st % NTAP]), lds_tr(cx, xoff4[st % NTAP]));
+    };
+    read_a(0);
+    read_b(0);
+    read_b(1);
+#pragma unroll
+    for (int st = 0; st < NS; ++st) {
+      const int kk = st / NTAP, j = st % NTAP;
+      if (st + 2 < NS) {
+        if ((st + 2) % NTAP == 0) read_a((st + 2) / NTAP);
+        read_b(st + 2);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (BIAS != 0 && j == 0) {
         typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-        const u32x4 u = __builtin_bit_cast(u32x4, bias_b ? fa1 : fa0);
+        const u32x4 u = __builtin_bit_cast(u32x4, BIAS == 2 ? fa1[kk & 1] : fa0[kk & 1]);
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           bsum += __builtin_bit_cast(float, u[e] << 16) + __builtin_bit_cast(float, u[e] & 0xffff0000u);
       }
-#pragma unroll
-      for (int j = 0; j < NTAP; ++j) {
-        const bf16x8 fb = cat_tr(lds_tr(cx, xoff[j]), lds_tr(cx, xoff4[j]));
-        acc0[j] = mfma32(fa0, fb, acc0[j]);
-        acc1[j] = mfma32(fa1, fb, acc1[j]);
-      }
+      acc0[j] = mfma32(fa0[kk & 1], fb[st % 3], acc0[j]);
+      acc1[j] = mfma32(fa1[kk & 1], fb[st % 3], acc1[j]);
     }
   }
 }
@@ -159,10 +172,15 @@ __global__ void __launch_bounds__(512, 1) wgrad2_kernel(const bf16_t* __restrict
     acc1[j] = zero16();
   }
   float bsum = 0.f;
-  if (w < 4)
-    wgrad_tiles<5>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 0, cig, lane);
+  // bias partials: wave 0 -> co tile 0, wave 1 -> co tile 1 (summed from their A fragments)
+  if (w == 0)
+    wgrad_tiles<5, 1>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 0, cig, lane);
+  else if (w == 1)
+    wgrad_tiles<5, 2>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 0, cig, lane);
+  else if (w < 4)
+    wgrad_tiles<5, 0>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 0, cig, lane);
   else
-    wgrad_tiles<4>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 5, cig, lane);
+    wgrad_tiles<4, 0>(smem, buf_bytes, t0, t1, stage, acc0, acc1, bsum, halo, d, 5, cig, lane);
   // tap-major slab [chunk][conv][k][co][ci]; lane -> ci (32 lanes = 128 contiguous bytes)
   float* dst = slab + ((size_t)chunk * nconv + cv) * KS * CH * CH + cig * 32 + r;
 #pragma unroll
@@ -183,25 +201,53 @@ __global__ void __launch_bounds__(512, 1) wgrad2_kernel(const bf16_t* __restrict
   }
 }
 
-// sum the R tap-major slabs (fixed order) and ADD into weight [co][ci][KS] and bias [co]
+// sum the R tap-major slabs (fixed order) and ADD into weight [co][ci][KS] and bias [co].
+// 256 threads = 64 float4 columns x 4 R-quarters (8 loads in flight each); the quarters are combined
+// through LDS in a fixed order (deterministic).  Blocks >= nblk_w reduce the bias slabs.
 __global__ void __launch_bounds__(256) wgrad2_reduce_kernel(const float4* __restrict__ slab,
                                                             const float* __restrict__ bslab, float* __restrict__ dw0,
                                                             float* __restrict__ dw1, float* __restrict__ db0,
                                                             float* __restrict__ db1, int R, int nconv) {
   constexpr int per4 = KS * CH * CH / 4;
   const int total4 = nconv * per4;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < total4) {
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    int rr = 0;
-    for (; rr + 4 <= R; rr += 4) {
-      const float4 a = slab[(size_t)rr * total4 + idx], b = slab[(size_t)(rr + 1) * total4 + idx];
-      const float4 c = slab[(size_t)(rr + 2) * total4 + idx], e = slab[(size_t)(rr + 3) * total4 + idx];
-      s.x += (a.x + b.x) + (c.x + e.x); s.y += (a.y + b.y) + (c.y + e.y);
-      s.z += (a.z + b.z) + (c.z + e.z); s.w += (a.w + b.w) + (c.w + e.w);
+  const int nblk_w = (total4 + 63) / 64;
+  const int tid = threadIdx.x, col = tid & 63, part = tid >> 6;
+  if ((int)blockIdx.x >= nblk_w) {             // bias: one thread per output, R in order
+    const int idx = ((int)blockIdx.x - nblk_w) * 256 + tid;
+    if (idx < nconv * CH) {
+      float s = 0.f;
+      for (int rr = 0; rr < R; ++rr) s += bslab[(size_t)rr * nconv * CH + idx];
+      float* db = idx >= CH ? db1 : db0;
+      if (db != nullptr) db[idx % CH] += s;
     }
-    for (; rr < R; ++rr) {
+    return;
+  }
+  __shared__ float4 red[4][64];
+  const int idx = blockIdx.x * 64 + col;
+  const int r0 = R * part / 4, r1 = R * (part + 1) / 4;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (idx < total4) {
+    int rr = r0;
+    for (; rr + 8 <= r1; rr += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = slab[(size_t)(rr + u) * total4 + idx];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w;
+      }
+    }
+    for (; rr < r1; ++rr) {
       const float4 a = slab[(size_t)rr * total4 + idx];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+  }
+  red[part][col] = s;
+  __syncthreads();
+  if (part == 0 && idx < total4) {
+#pragma unroll
+    for (int p = 1; p < 4; ++p) {
+      const float4 a = red[p][col];
       s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
     }
     const int cv = idx >= per4;
@@ -212,12 +258,6 @@ __global__ void __launch_bounds__(256) wgrad2_reduce_kernel(const float4* __rest
     dw[KS] += s.y;
     dw[2 * KS] += s.z;
     dw[3 * KS] += s.w;
-  }
-  if (idx < nconv * CH) {
-    float s = 0.f;
-    for (int rr = 0; rr < R; ++rr) s += bslab[(size_t)rr * nconv * CH + idx];
-    float* db = idx >= CH ? db1 : db0;
-    if (db != nullptr) db[idx % CH] += s;
   }
 }
 
@@ -239,7 +279,8 @@ PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float
   hipLaunchKernelGGL(wgrad2_kernel, dim3(nconv * 2 * R), dim3(512), 2 * buf, st, (const bf16_t*)dy0,
                      (const bf16_t*)dy1, (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R, buf);
   const int total4 = nconv * KS * CH * CH / 4;
-  hipLaunchKernelGGL(wgrad2_reduce_kernel, dim3((total4 + 255) / 256), dim3(256), 0, st, (const float4*)slab,
+  const int nblk = (total4 + 63) / 64 + (nconv * CH + 255) / 256;
+  hipLaunchKernelGGL(wgrad2_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const float4*)slab,
                      bslab, dw0, dw1, db0, db1, R, nconv);
   return pbx_launch_status();
 }
