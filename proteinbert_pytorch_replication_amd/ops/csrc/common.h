@@ -81,6 +81,77 @@ __device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
 }
 #endif
 
+// Packed GELU / GELU' for VALU-bound epilogues (the attention pool: one GELU per element of a
+// [rows, 512] GEMM output, ~13 VALU + 2 transcendentals each, 3-4x the MFMA time of the GEMM).
+// Same A&S 7.1.26 erf, rearranged so every non-transcendental step is one v_pk_* instruction for
+// two values:  gelu(x) = 0.5 x + |x| * h,  h = 0.5 erf(|x|/sqrt2) = 0.5 - 0.5 t P(t) e  (the -0.5 is
+// folded into the polynomial coefficients), e = exp(-x^2 / 2), t = 1 / (1 + p |x| / sqrt2).
+__device__ __forceinline__ void gelu_core2(f32x2 x, f32x2& ax, f32x2& h, f32x2& e) {
+  ax = __builtin_elementwise_abs(x);
+  const f32x2 den = __builtin_elementwise_fma(ax, (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  const f32x2 q = (x * -0.72134752044448170f) * x;                  // -x^2/2 * log2(e)
+  e = (f32x2){__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  f32x2 pl = __builtin_elementwise_fma(t, (f32x2){-0.5307027145f, -0.5307027145f},
+                                       (f32x2){0.7265760135f, 0.7265760135f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.7107068705f, -0.7107068705f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){0.142248368f, 0.142248368f});
+  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.127414796f, -0.127414796f});
+  h = __builtin_elementwise_fma(pl * t, e, (f32x2){0.5f, 0.5f});
+}
+__device__ __forceinline__ f32x2 gelu2_fast(f32x2 x) {
+  f32x2 ax, h, e;
+  gelu_core2(x, ax, h, e);
+  return __builtin_elementwise_fma(ax, h, x * 0.5f);
+}
+// GELU'(x) = Phi(x) + x phi(x) = 0.5 + sign(x) h + x e / sqrt(2 pi)
+__device__ __forceinline__ f32x2 gelu_grad2_fast(f32x2 x) {
+  f32x2 ax, h, e;
+  gelu_core2(x, ax, h, e);
+  const f32x2 sh = {copysignf(h.x, x.x), copysignf(h.y, x.y)};
+  return __builtin_elementwise_fma(x * 0.3989422804014327f, e, sh + 0.5f);
+}
+
+// N independent pairs evaluated stage by stage (every stage of all N before the next): the
+// one-pair forms above compile to a serial dependency chain with an s_nop between dependent packed
+// ops; N interleaved chains fill those slots and the transcendental latencies.
+template <int N, bool GRAD>
+__device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
+  f32x2 ax[N], t[N], e[N], pl[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    ax[i] = __builtin_elementwise_abs(x[i]);
+    t[i] = __builtin_elementwise_fma(ax[i], (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
+    e[i] = (x[i] * -0.72134752044448170f) * x[i];
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    t[i] = (f32x2){__builtin_amdgcn_rcpf(t[i].x), __builtin_amdgcn_rcpf(t[i].y)};
+    e[i] = (f32x2){__builtin_amdgcn_exp2f(e[i].x), __builtin_amdgcn_exp2f(e[i].y)};
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+    pl[i] = __builtin_elementwise_fma(t[i], (f32x2){-0.5307027145f, -0.5307027145f},
+                                      (f32x2){0.7265760135f, 0.7265760135f});
+#pragma unroll
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.7107068705f, -0.7107068705f});
+#pragma unroll
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){0.142248368f, 0.142248368f});
+#pragma unroll
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.127414796f, -0.127414796f});
+#pragma unroll
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(pl[i] * t[i], e[i], (f32x2){0.5f, 0.5f});   // h
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (GRAD) {
+      const f32x2 sh = {copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)};
+      out[i] = __builtin_elementwise_fma(x[i] * 0.3989422804014327f, e[i], sh + 0.5f);
+    } else {
+      out[i] = __builtin_elementwise_fma(ax[i], pl[i], x[i] * 0.5f);
+    }
+  }
+}
+
 __device__ __forceinline__ float wave_reduce_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

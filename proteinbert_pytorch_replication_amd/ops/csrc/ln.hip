@@ -246,21 +246,16 @@ __global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
       ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
     }
     float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
-    const bool full = pos0 + 64 <= L;
+    // rows beyond L are zero fragments (ln_row_frags) and GELU(0) = 0: no masking needed
     auto colsum = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
       f32x2 sv = {0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < 16; i += 2) {
-        f32x2 g0 = gelu2((f32x2){c0[i], c0[i + 1]});
-        f32x2 g1 = gelu2((f32x2){c1[i], c1[i + 1]});
-        if (!full) {
-          const int prow = pos0 + 4 * h + (i & 3) + 8 * (i >> 2);
-          g0.x = prow < L ? g0.x : 0.f;
-          g0.y = prow + 1 < L ? g0.y : 0.f;
-          g1.x = prow + 32 < L ? g1.x : 0.f;
-          g1.y = prow + 33 < L ? g1.y : 0.f;
-        }
-        sv += g0 + g1;
+      for (int g = 0; g < 4; ++g) {
+        const f32x2 xv[4] = {(f32x2){c0[4 * g], c0[4 * g + 1]}, (f32x2){c0[4 * g + 2], c0[4 * g + 3]},
+                             (f32x2){c1[4 * g], c1[4 * g + 1]}, (f32x2){c1[4 * g + 2], c1[4 * g + 3]}};
+        f32x2 gv[4];
+        gelu2_fast_n<4, false>(xv, gv);
+        sv += (gv[0] + gv[1]) + (gv[2] + gv[3]);
       }
       float sacc = sv.x + sv.y;
       sacc += __shfl_xor(sacc, 32, 64);
@@ -344,23 +339,24 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
     float* dv = reinterpret_cast<float*>(ws + NJ * 256) + w * NJ;
     for (int i = lane * 4; i < NJ; i += 256) *reinterpret_cast<float4*>(dv + i) = *reinterpret_cast<const float4*>(dvg + i);
     __builtin_amdgcn_wave_barrier();
-    const bool full = pos0 + 32 <= L;
+    // positions beyond L get nonzero dP (GELU'(0) = 1/2) but only feed their own output columns,
+    // which are neither stored nor counted in the LN partials
     auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
+      float dvv[16];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        float dvv[4];
-        load_f4(dv + jt * 32 + 8 * g + 4 * h, dvv);
+      for (int g = 0; g < 4; ++g) load_f4(dv + jt * 32 + 8 * g + 4 * h, dvv + 4 * g);
 #pragma unroll
-        for (int e = 0; e < 4; e += 2) {
-          const f32x2 gg = gelu_grad2((f32x2){d1[4 * g + e], d1[4 * g + e + 1]}) * (f32x2){dvv[e], dvv[e + 1]};
-          dp[4 * g + e] = gg.x;
-          dp[4 * g + e + 1] = gg.y;
+      for (int hq = 0; hq < 4; ++hq) {
+        f32x2 xv[2], gv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) xv[i] = (f32x2){d1[4 * hq + 2 * i], d1[4 * hq + 2 * i + 1]};
+        gelu2_fast_n<2, true>(xv, gv);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          dp[4 * hq + 2 * i] = gv[i].x * dvv[4 * hq + 2 * i];
+          dp[4 * hq + 2 * i + 1] = gv[i].y * dvv[4 * hq + 2 * i + 1];
         }
-      }
-      if (!full) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dp[i] = okb ? dp[i] : 0.f;
       }
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
@@ -374,12 +370,18 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
         }
       }
     };
-    f32x16_t d0 = wv_chain<false>(ws, hf, 0, r, h);
-    for (int jt = 0; jt < NJT; jt += 2) {
-      const f32x16_t d1 = wv_chain<false>(ws, hf, jt + 1, r, h);
-      proc(d0, jt);
-      if (jt + 2 < NJT) d0 = wv_chain<false>(ws, hf, jt + 2, r, h);
-      proc(d1, jt + 1);
+    if (MAXT > 256) {
+      // 8 waves (<= 256 VGPRs): one recompute tile in flight; the other wave of the SIMD covers
+      // the chain latency
+      for (int jt = 0; jt < NJT; ++jt) proc(wv_chain<false>(ws, hf, jt, r, h), jt);
+    } else {
+      f32x16_t d0 = wv_chain<false>(ws, hf, 0, r, h);
+      for (int jt = 0; jt < NJT; jt += 2) {
+        const f32x16_t d1 = wv_chain<false>(ws, hf, jt + 1, r, h);
+        proc(d0, jt);
+        if (jt + 2 < NJT) d0 = wv_chain<false>(ws, hf, jt + 2, r, h);
+        proc(d1, jt + 1);
+      }
     }
     // Y[ci][pos]; LN2 backward partials of this wave tile
     float mean, rstd;

@@ -91,8 +91,9 @@ def attn_fwd_waves(L: int) -> int:
 
 
 def attn_bwd_waves(L: int) -> int:
-    """attn_bwd workgroup: 8 independent waves (work items are 32-position wave tiles)."""
-    return 8
+    """attn_bwd workgroup: 8 independent waves (work items are 32-position wave tiles);
+    PBX_ATTN_BWD_WAVES=4 selects the one-wave-per-SIMD (512-register) build."""
+    return int(os.environ.get("PBX_ATTN_BWD_WAVES", 8))
 
 
 def _p(t: Optional[torch.Tensor]):

@@ -1,21 +1,32 @@
-"""Aggregate rocprofv3 counter_collection.csv files per kernel: mean counter value per dispatch."""
-import csv, sys, collections
-agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for path in sys.argv[1:]:
-    for r in csv.DictReader(open(path)):
-        name = r['Kernel_Name'].replace('(anonymous namespace)::', '').replace('void ', '').split('(')[0][:34]
-        agg[name][r['Counter_Name']].append(float(r['Counter_Value']))
-keys = ['SQ_WAVE_CYCLES', 'SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS', 'SQ_LDS_BANK_CONFLICT', 'SQ_INSTS_VMEM_WR',
-        'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_WAIT_INST_LDS', 'SQ_WAIT_ANY', 'SQ_INSTS_VMEM_RD', 'SQ_ACTIVE_INST_VALU',
-        'GRBM_GUI_ACTIVE', 'SQ_WAIT_INST_ANY', 'SQ_ACTIVE_INST_LDS', 'SQ_ACTIVE_INST_VMEM', 'SQ_ACTIVE_INST_ANY',
-        'SQ_INSTS_VALU_TRANS_F32', 'SQ_BUSY_CYCLES', 'SQ_INSTS_SALU', 'SQ_INSTS_SMEM', 'SQ_ACTIVE_INST_SCA',
-        'SQ_INSTS_BRANCH']
-short = ['WAVECYC', 'VALU', 'MFMA', 'LDS', 'BANKCF', 'VMEMWR', 'MFMABUSY', 'WAITLDS', 'WAITANY', 'VMEMRD', 'ACTVALU',
-         'GUI', 'WAITINST', 'ACTLDS', 'ACTVMEM', 'ACTANY', 'TRANS', 'BUSY', 'SALU', 'SMEM', 'ACTSCA', 'BRANCH']
-print(f"{'kernel':34s} " + " ".join(f"{k:>9s}" for k in short))
-for name, d in sorted(agg.items(), key=lambda kv: -sum(kv[1].get('GRBM_GUI_ACTIVE', [0]))):
-    vals = []
-    for k in keys:
-        v = d.get(k)
-        vals.append(f"{sum(v)/len(v):9.3g}" if v else f"{'-':>9s}")
-    print(f"{name:34s} " + " ".join(vals))
+"""Summarise rocprofv3 --pmc passes (gpurun_out/<dir>/runc/*_counter_collection.csv) per kernel."""
+import collections
+import csv
+import glob
+import sys
+
+res = collections.defaultdict(lambda: collections.defaultdict(list))
+for d in sys.argv[1:]:
+    fs = glob.glob(f"gpurun_out/{d}/runc/*_counter_collection.csv")
+    if not fs:
+        print("missing", d)
+        continue
+    agg = collections.defaultdict(lambda: collections.defaultdict(float))
+    names = {}
+    for r in csv.DictReader(open(fs[0])):
+        agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        names[r["Dispatch_Id"]] = r["Kernel_Name"]
+    for k, v in agg.items():
+        for c, x in v.items():
+            res[names[k][:48]][c].append(x)
+for n, v in sorted(res.items()):
+    m = {c: sum(x) / len(x) for c, x in v.items()}
+    clk = m.get("GRBM_GUI_ACTIVE", 0) / 8
+    if clk < 20000:
+        continue
+    mf = m.get("SQ_VALU_MFMA_BUSY_CYCLES", 0) / 1024 / clk
+    nm = max(1.0, m.get("SQ_INSTS_MFMA", 1))
+    wc = max(1.0, m.get("SQ_WAVE_CYCLES", 1))
+    print(f"{n:48s} cyc {clk:9.0f} mfma_busy {mf:5.2f} valu/mfma {m.get('SQ_INSTS_VALU', 0) / nm:6.2f} "
+          f"lds/mfma {m.get('SQ_INSTS_LDS', 0) / nm:5.2f} wait_any {m.get('SQ_WAIT_ANY', 0) / wc:4.2f} "
+          f"wait_inst {m.get('SQ_WAIT_INST_ANY', 0) / wc:4.2f} active_valu/clk/simd "
+          f"{m.get('SQ_ACTIVE_INST_VALU', 0) * 4 / max(1.0, clk) / 1024:5.2f}")
