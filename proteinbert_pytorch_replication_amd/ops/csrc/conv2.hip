@@ -18,8 +18,9 @@
 //
 //   conv_fwd3   : 128 positions / workgroup; waves 0-3 = narrow conv, 4-7 = wide conv; wave q owns
 //                 output channels q*32..+32 for all 128 positions (4 accumulators of 32x32).
-//                 Epilogue: pre_n, pre_w and s1 = x + GELU(pre_n) + GELU(pre_w) + gb staged through
-//                 LDS for row-contiguous 16-B stores, plus the tile's LayerNorm (mean, M2) partial.
+//                 Epilogue: pre_n and pre_w staged through LDS; all 8 waves then write them and
+//                 s1 = x + GELU(pre_n) + GELU(pre_w) + gb with row-contiguous 16-B stores, plus the
+//                 tile's LayerNorm (mean, M2) partial.
 //   conv_dgrad3 : both convs' dpre = dS1 * GELU'(pre) tiles (with their halos) staged once and their
 //                 central rows written for the weight gradient; waves 0-3 = narrow, 4-7 = wide, wave
 //                 q owns input channels q*32..+32; the two halves are summed through LDS in the
@@ -97,9 +98,22 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   }
 
   // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
+  // Both pre-activation tiles are staged in LDS (narrow -> ot, wide -> over the x tile, whose 4 rows
+  // per thread are read into registers first), then all 512 threads take 4 (row, 16-B chunk) units
+  // each: pre_n / pre_w stores, s1 = x + GELU(pre_n) + GELU(pre_w) + gb with interleaved packed GELU
+  // chains, and the LayerNorm (mean, M2) partial -- balanced over the 8 waves (the narrow waves
+  // alone used to evaluate all 2 x 16K GELUs of the tile while the wide waves idled).
   const int vrows = min(BM, L - pos0);
-  const float* bias = bsm + cv * CH;
-  auto stage_acc = [&]() {                        // ot <- bf16(acc + bias)
+  uint4 xq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i;
+    xq[i] = *reinterpret_cast<const uint4*>(xs + swz256(halo + (idx >> 4), idx & 15));
+  }
+  __syncthreads();                                // every wave is done with the x tile
+  {
+    unsigned char* dst = cv ? smem : ot;
+    const float* bias = bsm + cv * CH;
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
@@ -108,71 +122,61 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
         const float4 bv = *reinterpret_cast<const float4*>(bias + ch0);
         const float v[4] = {acc[pt][4 * g] + bv.x, acc[pt][4 * g + 1] + bv.y, acc[pt][4 * g + 2] + bv.z,
                             acc[pt][4 * g + 3] + bv.w};
-        *reinterpret_cast<uint2*>(ot + swz256e(pt * 32 + r, ch0)) = packq4(v);
+        *reinterpret_cast<uint2*>(dst + swz256e(pt * 32 + r, ch0)) = packq4(v);
       }
-  };
-  auto copy_out = [&](bf16_t* __restrict__ dst) {  // ot -> dst rows (16 B per lane, row-contiguous)
+  }
+  __syncthreads();
+  float lsum = 0.f, lsq = 0.f;
+  int cnt = 0;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 512 * i;
-      const int row = idx >> 4, c = idx & 15;
-      if (row < vrows)
-        *reinterpret_cast<uint4*>(dst + ((size_t)b * L + pos0 + row) * CH + c * 8) =
-            *reinterpret_cast<const uint4*>(ot + swz256(row, c));
+  for (int i = 0; i < 4; ++i) {
+    const int idx = tid + 512 * i;
+    const int row = idx >> 4, c = idx & 15;
+    const bool ok = row < vrows;
+    const uint4 pnq = *reinterpret_cast<const uint4*>(ot + swz256(row, c));
+    const uint4 pwq = *reinterpret_cast<const uint4*>(smem + swz256(row, c));
+    const size_t off = ((size_t)b * L + pos0 + row) * CH + c * 8;
+    if (ok) {
+      *reinterpret_cast<uint4*>(pre_n + off) = pnq;
+      *reinterpret_cast<uint4*>(pre_w + off) = pwq;
     }
-  };
-  if (cv == 0) stage_acc();                       // pre_n
-  __syncthreads();
-  copy_out(pre_n);
-  __syncthreads();
-  if (cv == 1) stage_acc();                       // pre_w
-  __syncthreads();
-  copy_out(pre_w);
-  __syncthreads();
-  // narrow waves: s1 = x + GELU(pre_n) + GELU(pre_w) + gb from the bf16 pre-activations the
-  // backward reads, written over pre_w in place (each element belongs to one lane), with the
-  // per-lane (sum, sum of squares) of the LayerNorm partial
-  float* scratch = bsm + 3 * CH;                  // 4 narrow waves x (n, mean, M2)
-  if (cv == 0) {
-    float lsum = 0.f, lsq = 0.f;
+    float xv[8], pn[8], pw[8], o[8];
+    unpack8(xq[i], xv);
+    unpack8(pnq, pn);
+    unpack8(pwq, pw);
+    f32x2 gi[8], go[8];
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
+    for (int e = 0; e < 4; ++e) {
+      gi[e] = (f32x2){pn[2 * e], pn[2 * e + 1]};
+      gi[4 + e] = (f32x2){pw[2 * e], pw[2 * e + 1]};
+    }
+    gelu2_fast_n<8, false>(gi, go);
+    const float4 g0 = *reinterpret_cast<const float4*>(bsm + 2 * CH + c * 8);
+    const float4 g1 = *reinterpret_cast<const float4*>(bsm + 2 * CH + c * 8 + 4);
+    const float gba[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ch0 = cq * 32 + 8 * g + 4 * h;
-        const int p = pt * 32 + r;
-        const bool ok = p < vrows;
-        float xv[4], pw[4], o[4];
-        unpack4(*reinterpret_cast<const uint2*>(xs + swz256e(halo + p, ch0)), xv);
-        uint2* op = reinterpret_cast<uint2*>(ot + swz256e(p, ch0));
-        unpack4(*op, pw);
-        const float4 bnv = *reinterpret_cast<const float4*>(bsm + ch0);
-        const float4 gbv = *reinterpret_cast<const float4*>(bsm + 2 * CH + ch0);
-        const float bna[4] = {bnv.x, bnv.y, bnv.z, bnv.w};
-        const float gba[4] = {gbv.x, gbv.y, gbv.z, gbv.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float pn = bfround(acc[pt][4 * g + e] + bna[e]);
-          o[e] = bfround(xv[e] + gelu_f(pn) + gelu_f(pw[e]) + gba[e]);
-          lsum += ok ? o[e] : 0.f;
-          lsq += ok ? o[e] * o[e] : 0.f;
-        }
-        *op = packq4(o);
-      }
-    int cnt = 0;
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt) cnt += (pt * 32 + r) < vrows ? 16 : 0;
+    for (int e = 0; e < 8; ++e) {
+      const float gn = (e & 1) ? go[e >> 1].y : go[e >> 1].x;
+      const float gw = (e & 1) ? go[4 + (e >> 1)].y : go[4 + (e >> 1)].x;
+      o[e] = bfround(xv[e] + gn + gw + gba[e]);
+      lsum += ok ? o[e] : 0.f;
+      lsq += ok ? o[e] * o[e] : 0.f;
+    }
+    cnt += ok ? 8 : 0;
+    if (ok) *reinterpret_cast<uint4*>(s1 + off) = packq8(o);
+  }
+  float* scratch = bsm + 3 * CH;                  // 8 waves x (n, mean, M2)
+  {
     float n = (float)cnt, m = cnt > 0 ? lsum / n : 0.f;
     float M2 = cnt > 0 ? fmaxf(lsq - lsum * m, 0.f) : 0.f;
     wave_chan(n, m, M2);
     if (lane == 0) { scratch[3 * w] = n; scratch[3 * w + 1] = m; scratch[3 * w + 2] = M2; }
   }
   __syncthreads();
-  copy_out(s1);
   if (tid == 0) {
     float tn = 0.f, tm = 0.f, tM2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) chan_merge(tn, tm, tM2, scratch[3 * i], scratch[3 * i + 1], scratch[3 * i + 2]);
+    for (int i = 0; i < 8; ++i) chan_merge(tn, tm, tM2, scratch[3 * i], scratch[3 * i + 1], scratch[3 * i + 2]);
     stats[((size_t)b * T + t) * 2] = tm;
     stats[((size_t)b * T + t) * 2 + 1] = tM2;
   }
@@ -326,7 +330,10 @@ __global__ void __launch_bounds__(256) pack_conv_frag_kernel(const float* __rest
   pt[idx] = f2bf(w[((size_t)kk * CH + m) * KS + k]);     // M = ci, K = co
 }
 
-int fwd3_lds(int KS, int dil) { return (BM + 2 * (KS / 2) * dil) * 256 + OT + (3 * CH + 16) * 4; }
+int fwd3_lds(int KS, int dil) {
+  const int xt = (BM + 2 * (KS / 2) * dil) * 256;   // x tile, later the pre_w staging tile
+  return (xt > OT ? xt : OT) + OT + (3 * CH + 32) * 4;
+}
 int dgrad3_lds(int KS, int dil) {
   const int a = (2 * BM + 2 * (KS / 2) * (1 + dil)) * 256;
   return a > BM * CH * 4 ? a : BM * CH * 4;

@@ -343,19 +343,19 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
     // which are neither stored nor counted in the LN partials
     auto proc = [&](const f32x16_t& d1, int jt) {
       float dp[16];
-      float dvv[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) load_f4(dv + jt * 32 + 8 * g + 4 * h, dvv + 4 * g);
 #pragma unroll
       for (int hq = 0; hq < 4; ++hq) {
+        // rows 8 hq + 4 h .. +3 of this column block: dv read from the wave's LDS slot per group
+        float dvv[4];
+        load_f4(dv + jt * 32 + 8 * hq + 4 * h, dvv);
         f32x2 xv[2], gv[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) xv[i] = (f32x2){d1[4 * hq + 2 * i], d1[4 * hq + 2 * i + 1]};
         gelu2_fast_n<2, true>(xv, gv);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          dp[4 * hq + 2 * i] = gv[i].x * dvv[4 * hq + 2 * i];
-          dp[4 * hq + 2 * i + 1] = gv[i].y * dvv[4 * hq + 2 * i + 1];
+          dp[4 * hq + 2 * i] = gv[i].x * dvv[2 * i];
+          dp[4 * hq + 2 * i + 1] = gv[i].y * dvv[2 * i + 1];
         }
       }
 #pragma unroll
@@ -420,6 +420,8 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
           }
           if (okb) *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
         }
+        // one channel tile's operands in flight at a time (hoisting all four needs 128 VGPRs)
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     sa = wave_reduce_sum(sa);
