@@ -25,6 +25,7 @@ import torch
 from ..config import RunConfig, apply_overrides, get_preset, load_yaml, PRESETS
 from ..data import SyntheticUniRefGO, CorruptionParams
 from ..models import ProteinBERT, ProteinBERTForTokenClassification, build_model
+from ..utils import determinism
 from ..parallel import dist as pdist
 
 
@@ -70,8 +71,10 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     logging.basicConfig(format="%(asctime)s [%(levelname)s]: %(message)s", level=logging.INFO)
     info = pdist.init_distributed(backend=cfg.dist.backend, timeout_s=cfg.dist.timeout_s)
     dev = info.device
+    if cfg.kernel.deterministic:
+        determinism.enable()
     torch.manual_seed(cfg.train.seed)
-    model = build_model(cfg.model, device=dev, backend=cfg.kernel.backend)
+    model = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
     B, L = cfg.train.batch_size, cfg.model.sequences_length
     corr = CorruptionParams(cfg.data.token_corruption_p, cfg.data.annotation_positive_p,
                             cfg.data.annotation_negative_p, cfg.data.blank_annotation_p)
@@ -139,13 +142,15 @@ def finetune_main(argv: Optional[List[str]] = None) -> dict:
     cfg = _cfg(a)
     logging.basicConfig(format="%(asctime)s [%(levelname)s]: %(message)s", level=logging.INFO)
     info = pdist.init_distributed(backend=cfg.dist.backend)
+    if cfg.kernel.deterministic:
+        determinism.enable()
     dev = info.device
     torch.manual_seed(cfg.train.seed)
     if a.pretrained:
         from ..train.checkpoint import load_model
-        enc = load_model(a.pretrained, device=dev, backend=cfg.kernel.backend)
+        enc = load_model(a.pretrained, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
     else:
-        enc = build_model(cfg.model, device=dev, backend=cfg.kernel.backend)
+        enc = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
     L = enc.config["sequences_length"]
     model = ProteinBERTForTokenClassification(enc, n_classes=len(a.classes), freeze_encoder=not a.unfreeze)
     from torch.utils.data import DataLoader
