@@ -41,21 +41,26 @@ constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging til
 // K = output channel.
 __device__ __forceinline__ int frag_index(int k, int kb, int mb) { return (k * 8 + kb) * 4 + mb; }
 
-__global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
+// TBM = positions per workgroup: 128 (two workgroups per CU, <= 128 VGPRs) or 256 (one workgroup per
+// CU, 8 accumulators per wave: every weight fragment fetched from L2 feeds 8 MFMAs instead of 4)
+template <int TBM, int MINB>
+__global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
     bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
     float* __restrict__ stats, int L, int KS, int dil) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int T = (L + BM - 1) / BM;
+  constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
+  constexpr int TOT = TBM * 256;                              // bytes of one [TBM][128] bf16 tile
+  const int T = (L + TBM - 1) / TBM;
   const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
-  const int pos0 = t * BM;
+  const int pos0 = t * TBM;
   const int half = KS >> 1;
   const int halo = half * dil;
-  const int XR = BM + 2 * halo;
+  const int XR = TBM + 2 * halo;
   unsigned char* xs = smem;                                   // XR x 256 B (swz256)
-  unsigned char* ot = smem + XR * 256;                        // [BM][128] bf16 staging tile
-  float* bsm = reinterpret_cast<float*>(ot + OT);             // bn | bw | gb[b] | LN scratch
+  unsigned char* ot = smem + XR * 256;                        // [TBM][128] bf16 staging tile
+  float* bsm = reinterpret_cast<float*>(ot + TOT);            // bn | bw | gb[b] | LN scratch
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
@@ -80,9 +85,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
   __syncthreads();
 
-  f32x16_t acc[4];
+  f32x16_t acc[NPT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = zero16();
+  for (int i = 0; i < NPT; ++i) acc[i] = zero16();
   const int d = cv ? dil : 1;
   for (int it0 = 0; it0 < NI; it0 += 4) {
 #pragma unroll
@@ -93,7 +98,8 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       const int k = it >> 3, kb = it & 7;
       const int rb = halo + r + (k - half) * d;
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[u], lds_frag(xs, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
+      for (int pt = 0; pt < NPT; ++pt)
+        acc[pt] = mfma32(fr[u], lds_frag(xs, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
     }
   }
 
@@ -103,10 +109,10 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   // each: pre_n / pre_w stores, s1 = x + GELU(pre_n) + GELU(pre_w) + gb with interleaved packed GELU
   // chains, and the LayerNorm (mean, M2) partial -- balanced over the 8 waves (the narrow waves
   // alone used to evaluate all 2 x 16K GELUs of the tile while the wide waves idled).
-  const int vrows = min(BM, L - pos0);
-  uint4 xq[4];
+  const int vrows = min(TBM, L - pos0);
+  uint4 xq[NPT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NPT; ++i) {
     const int idx = tid + 512 * i;
     xq[i] = *reinterpret_cast<const uint4*>(xs + swz256(halo + (idx >> 4), idx & 15));
   }
@@ -115,7 +121,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     unsigned char* dst = cv ? smem : ot;
     const float* bias = bsm + cv * CH;
 #pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
+    for (int pt = 0; pt < NPT; ++pt)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int ch0 = cq * 32 + 8 * g + 4 * h;
@@ -129,7 +135,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   float lsum = 0.f, lsq = 0.f;
   int cnt = 0;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NPT; ++i) {
     const int idx = tid + 512 * i;
     const int row = idx >> 4, c = idx & 15;
     const bool ok = row < vrows;
@@ -330,9 +336,10 @@ __global__ void __launch_bounds__(256) pack_conv_frag_kernel(const float* __rest
   pt[idx] = f2bf(w[((size_t)kk * CH + m) * KS + k]);     // M = ci, K = co
 }
 
-int fwd3_lds(int KS, int dil) {
-  const int xt = (BM + 2 * (KS / 2) * dil) * 256;   // x tile, later the pre_w staging tile
-  return (xt > OT ? xt : OT) + OT + (3 * CH + 32) * 4;
+int fwd3_lds(int KS, int dil, int tbm) {
+  const int xt = (tbm + 2 * (KS / 2) * dil) * 256;  // x tile, later the pre_w staging tile
+  const int ot = tbm * 256;
+  return (xt > ot ? xt : ot) + ot + (3 * CH + 32) * 4;
 }
 int dgrad3_lds(int KS, int dil) {
   const int a = (2 * BM + 2 * (KS / 2) * (1 + dil)) * 256;
@@ -343,22 +350,30 @@ int dgrad3_lds(int KS, int dil) {
 static bool conv3_attrs_set = false;
 static void set_conv3_attrs() {
   if (conv3_attrs_set) return;
-  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<256, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   conv3_attrs_set = true;
 }
 
-// LayerNorm partials in `stats` are per 128-position tile: [B][ceil(L/128)][2].  fwn/fww: forward
+// LayerNorm partials in `stats` are per tbm-position tile: [B][ceil(L/tbm)][2] (tbm = 128 or 256).  fwn/fww: forward
 // fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels.
 PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
-                             int dil, hipStream_t st) {
+                             int dil, int tbm, hipStream_t st) {
   set_conv3_attrs();
-  const int lds = fwd3_lds(KS, dil);
+  if (tbm != 128 && tbm != 256) return (int)hipErrorInvalidValue;
+  const int lds = fwd3_lds(KS, dil, tbm);
   if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
-  const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_fwd3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
-                     (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
+  const int T = (L + tbm - 1) / tbm;
+  if (tbm == 256)
+    hipLaunchKernelGGL((conv_fwd3_kernel<256, 2>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
+                       (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
+                       (bf16_t*)s1, stats, L, KS, dil);
+  else
+    hipLaunchKernelGGL((conv_fwd3_kernel<128, 4>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
+                       (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
+                       (bf16_t*)s1, stats, L, KS, dil);
   return pbx_launch_status();
 }
 

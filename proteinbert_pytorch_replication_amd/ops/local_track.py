@@ -30,7 +30,7 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
@@ -59,9 +59,15 @@ CONV_IMPL = os.environ.get("PBX_CONV", "v3")
 WGRAD_IMPL = os.environ.get("PBX_WGRAD", "v2")
 
 
+# v3 forward tile: 128 positions (two workgroups per CU; measured faster in the full step than 256,
+# one workgroup per CU with each streamed weight fragment feeding 8 MFMAs); PBX_CONV_TILE=256 selects it
+CONV3_TILE = int(os.environ.get("PBX_CONV_TILE", "128"))
+
+
 def conv_tile(L: int) -> int:
+    """Positions per forward conv workgroup (= the tile of the LayerNorm-1 partials)."""
     if CONV_IMPL == "v3":
-        return 128
+        return CONV3_TILE if L >= CONV3_TILE else 128
     return 256 if L >= 256 else 128
 
 
@@ -69,7 +75,7 @@ def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, BM
     if CONV_IMPL == "v3":
         _lib.call("pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
                   gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
-                  stream)
+                  BM, stream)
     else:
         _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
                   gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,

@@ -83,15 +83,17 @@ _lib.call("pbx_pack_conv_frag", w.data_ptr(), fpn.data_ptr(), ftn_.data_ptr(), K
 T2 = (L + 127) // 128
 st_b = torch.empty(B, T2, 2, device=dev)
 new = [act() for _ in range(3)]
-fwd2 = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fpn.data_ptr(), fpn.data_ptr(), bias2.data_ptr(),  # noqa
-                         bias2.data_ptr(), gb2.data_ptr(), new[0].data_ptr(), new[1].data_ptr(), new[2].data_ptr(),
-                         st_b.data_ptr(), B, L, KS, dil, st)
-fwd2()
-torch.cuda.synchronize()
-for nm, u, v in zip(("pre_n", "pre_w", "s1"), ref, new):
-    print(f"  fwd3 vs fwd {nm}: max|diff| {float((u.float() - v.float()).abs().max()):.4g}  "
-          f"max|ref| {float(u.float().abs().max()):.3g}", flush=True)
-report("conv_fwd3 (frag-streamed W)", timeit(fwd2), conv_flops, 4 * x.numel() * 2)
+for tbm in (128, 256):
+    st_b = torch.empty(B, (L + tbm - 1) // tbm, 2, device=dev)
+    fwd2 = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fpn.data_ptr(), fpn.data_ptr(), bias2.data_ptr(),  # noqa
+                             bias2.data_ptr(), gb2.data_ptr(), new[0].data_ptr(), new[1].data_ptr(),
+                             new[2].data_ptr(), st_b.data_ptr(), B, L, KS, dil, tbm, st)
+    fwd2()
+    torch.cuda.synchronize()
+    for nm, u, v in zip(("pre_n", "pre_w", "s1"), ref, new):
+        print(f"  fwd3/{tbm} vs fwd {nm}: max|diff| {float((u.float() - v.float()).abs().max()):.4g}  "
+              f"max|ref| {float(u.float().abs().max()):.3g}", flush=True)
+    report(f"conv_fwd3 tile {tbm} (frag-streamed W)", timeit(fwd2), conv_flops, 4 * x.numel() * 2)
 dref = [act() for _ in range(3)]
 dnew = [act() for _ in range(3)]
 ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
