@@ -348,14 +348,15 @@ __global__ void __launch_bounds__(256) local_head_kernel(
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
 }
 
-// MFMA version of the local head (B <= 608): one workgroup (4 waves) per position l; the h_l rows
-// pass through LDS in chunks of HC = 128 rows (twice: logits, then dWo), so the LDS holds only the
-// [B][32] logit / dz tiles at full batch size.
+// MFMA version of the local head (B <= 608): one workgroup (8 waves; the MFMA phases use waves 0-3,
+// the softmax / CE phases all 8) per position l; h_l is held in registers and passes through LDS in
+// chunks of HC = 128 rows (twice: logits, then dWo), so the LDS holds only the [B][32] logit / dz
+// tiles at full batch size.
 //   logits  Z[b][v]   = h_l[b] . Wo[v] + bo[v]       (MFMA: A = h_l rows, B = Wo rows)
 //   softmax over b, CE on the probabilities, dz      (VALU on the [B][32] logit tile, as above)
 //   dWo_l[v][c]       = sum_b dz[b][v] h_l[b][c]     (MFMA: both operands transposed LDS reads)
 //   dh[b][c]          = sum_v dz[b][v] Wo[v][c]      (MFMA, staged through LDS for 256-B row stores)
-__global__ void __launch_bounds__(256) local_head_mfma_kernel(
+__global__ void __launch_bounds__(512) local_head_mfma_kernel(
     const bf16_t* __restrict__ h, const float* __restrict__ wo, const float* __restrict__ bo,
     const long long* __restrict__ y, const float* __restrict__ wl, bf16_t* __restrict__ dh, float* __restrict__ dwo_part,
     float* __restrict__ dbo_part, float* __restrict__ loss, int B, int L, int V, float inv_bl) {
@@ -366,25 +367,36 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
   unsigned char* wos = hs + HC * 256;                         // [32][128] bf16 swz256
   unsigned char* dzb = wos + 32 * 256;                        // [Bp][32] bf16, 64-B rows
   float* zs = reinterpret_cast<float*>(dzb + Bp * 64);        // [Bp][32] fp32
-  float* red = zs + Bp * 32;                                  // [8][32]
-  float* colv = red + 8 * 32;                                 // [32] + [2][32]
+  float* red = zs + Bp * 32;                                  // [16][32]
+  float* colv = red + 16 * 32;                                // [32] + [2][32]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int l = blockIdx.x;
   // h_l rows c0 .. c0 + HC - 1 -> hs (zero beyond B)
-  auto stage_h = [&](int c0) {
-    stage_chunks(
-        HC * 16,
-        [&](int idx) {
-          const int b = c0 + (idx >> 4);
-          return b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
-                       : make_uint4(0u, 0u, 0u, 0u);
-        },
-        [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = v; });
+  // All of h_l (B <= 608 rows x 256 B) is loaded into registers once, up front (<= 5 chunks x 4 x 16 B
+  // per thread): one HBM round trip instead of one per chunk and pass, and no second read for dWo.
+  constexpr int MAXC = 5;
+  uint4 hreg[MAXC][4];
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 512 * i;
+      const int b = c * HC + (idx >> 4);
+      hreg[c][i] = b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
+                         : make_uint4(0u, 0u, 0u, 0u);
+    }
+  // chunk c (compile-time index after unrolling) -> hs
+  auto stage_h = [&](const uint4 (&hc)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = tid + 512 * i;
+      *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = hc[i];
+    }
   };
   // Wo (bf16, zero rows beyond V)
-  for (int idx = tid; idx < 32 * 16; idx += 256) {
+  for (int idx = tid; idx < 32 * 16; idx += 512) {
     const int v = idx >> 4, c8 = idx & 15;
     float e[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (v < V) {
@@ -396,12 +408,15 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
   }
   // logits, one h chunk at a time (wave w -> row tile w of the chunk)
   const float bov = r < V ? bo[r] : 0.f;
-  for (int c0 = 0; c0 < Bp; c0 += HC) {
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int c0 = c * HC;
+    if (c0 >= Bp) break;
     __syncthreads();                            // previous chunk consumed
-    stage_h(c0);
+    stage_h(hreg[c]);
     __syncthreads();
     const int rt = c0 / 32 + w;
-    if (rt < Bp / 32) {
+    if (w < HC / 32 && rt < Bp / 32) {
       f32x16_t acc = zero16();
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk)
@@ -414,115 +429,120 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
     }
   }
   __syncthreads();
-  // softmax over b for each v (8 partial columns per v)
+  // softmax over b for each v (16 partial columns per v)
   {
     const int v = tid & 31, part = tid >> 5;
     float m = -3.4e38f;
     if (v < V)
-      for (int b = part; b < B; b += 8) m = fmaxf(m, zs[b * 32 + v]);
+      for (int b = part; b < B; b += 16) m = fmaxf(m, zs[b * 32 + v]);
     red[part * 32 + v] = m;
     __syncthreads();
     if (tid < 32) {
       float mm = -3.4e38f;
-      for (int k = 0; k < 8; ++k) mm = fmaxf(mm, red[k * 32 + tid]);
+      for (int k = 0; k < 16; ++k) mm = fmaxf(mm, red[k * 32 + tid]);
       colv[32 + tid] = mm;
     }
     __syncthreads();
     float sacc = 0.f;
     if (v < V)
-      for (int b = part; b < B; b += 8) sacc += __expf(zs[b * 32 + v] - colv[32 + v]);
+      for (int b = part; b < B; b += 16) sacc += __expf(zs[b * 32 + v] - colv[32 + v]);
     red[part * 32 + v] = sacc;
     __syncthreads();
     if (tid < 32) {
       float ss = 0.f;
-      for (int k = 0; k < 8; ++k) ss += red[k * 32 + tid];
+      for (int k = 0; k < 16; ++k) ss += red[k * 32 + tid];
       colv[64 + tid] = ss > 0.f ? 1.0f / ss : 0.f;
       colv[tid] = 0.f;
     }
     __syncthreads();
   }
-  for (int i = tid; i < B * 32; i += 256) {
+  for (int i = tid; i < B * 32; i += 512) {
     const int v = i & 31;
     zs[i] = v < V ? __expf(zs[i] - colv[32 + v]) * colv[64 + v] : 0.f;
   }
   __syncthreads();
-  // CE over v on the probabilities (one thread per sample); colv[v] = sum_b G P
+  // CE over v on the probabilities, one thread per sample: se_b = sum_v exp(P[b][v]) (P is a
+  // probability in [0, 1]: no max shift needed), loss_b = log se_b - P[b][y_b]; the per-row scalars
+  // (1/se_b, w_b/(BL), y_b) go to the free h staging tile.  G[b][v] = coef_b (exp(P)/se_b - [v==y_b]).
+  float* rsv = reinterpret_cast<float*>(hs);                  // [Bp] 1/se_b
+  float* cfv = rsv + Bp;                                      // [Bp] w_b / (B L)
+  int* ybv = reinterpret_cast<int*>(cfv + Bp);                // [Bp] y_b
   float lsum = 0.f;
+  for (int b = tid; b < B; b += 512) {
+    const float* p = zs + b * 32;
+    float se = 0.f;
+#pragma unroll
+    for (int v4 = 0; v4 < 8; ++v4) {
+      const float4 q4 = *reinterpret_cast<const float4*>(p + 4 * v4);
+      const float pv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) se += (4 * v4 + e) < V ? __expf(pv[e]) : 0.f;
+    }
+    const int yv = (int)y[(size_t)b * L + l];
+    const float wgt = wl[(size_t)b * L + l];
+    lsum += wgt * (__logf(se) - p[yv]);
+    rsv[b] = 1.0f / se;
+    cfv[b] = wgt * inv_bl;
+    ybv[b] = yv;
+  }
+  __syncthreads();
+  // colv[v] = sum_b G[b][v] P[b][v]: thread (v, part) over rows part, part + 16, ...; 16 partial
+  // columns combined in a fixed order
+  const int cv_v = tid & 31, cv_part = tid >> 5;
   {
-    // per-thread G.P rows, then one wave reduction per v (no contended LDS atomics)
-    float gp[32];
-#pragma unroll
-    for (int v = 0; v < 32; ++v) gp[v] = 0.f;
-    for (int b = tid; b < B; b += 256) {
-      const float* p = zs + b * 32;
-      float pv[32];
-#pragma unroll
-      for (int v = 0; v < 32; ++v) pv[v] = p[v];
-      float mx = -3.4e38f;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) mx = v < V ? fmaxf(mx, pv[v]) : mx;
-      float se = 0.f, ev[32];
-#pragma unroll
-      for (int v = 0; v < 32; ++v) { ev[v] = v < V ? __expf(pv[v] - mx) : 0.f; se += ev[v]; }
-      const int yv = (int)y[(size_t)b * L + l];
-      const float wgt = wl[(size_t)b * L + l];
-      float py = 0.f;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) py = v == yv ? pv[v] : py;
-      lsum += wgt * (mx + __logf(se) - py);
-      const float coef = wgt * inv_bl, inv_se = 1.0f / se;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) gp[v] += coef * (ev[v] * inv_se - (v == yv ? 1.f : 0.f)) * pv[v];
-    }
-#pragma unroll
-    for (int v = 0; v < 32; ++v) {
-      if (v < V) {
-        const float sv = wave_reduce_sum(gp[v]);
-        if (lane == 0) atomicAdd(&colv[v], sv);
+    float acc = 0.f;
+    if (cv_v < V)
+      for (int b = cv_part; b < B; b += 16) {
+        const float pv = zs[b * 32 + cv_v];
+        const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
+        acc += g * pv;
       }
+    red[cv_part * 32 + cv_v] = acc;
+    __syncthreads();
+    if (tid < 32) {
+      float t = 0.f;
+      for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
+      colv[tid] = t;
+    }
+    __syncthreads();
+  }
+  // dz = P (G - colv) -> bf16 dzb for the MFMAs (zero beyond B and V) and dbo_l[v] = sum_b dz
+  {
+    float acc = 0.f;
+    const float cvv = colv[cv_v];
+    for (int b = cv_part; b < Bp; b += 16) {
+      float dz = 0.f;
+      if (b < B && cv_v < V) {
+        const float pv = zs[b * 32 + cv_v];
+        const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
+        dz = pv * (g - cvv);
+      }
+      acc += dz;
+      *reinterpret_cast<bf16_t*>(dzb + b * 64 + cv_v * 2) = f2bf(dz);
+    }
+    __syncthreads();                            // every colv / rsv read done before red is reused
+    red[cv_part * 32 + cv_v] = acc;
+    __syncthreads();
+    if (tid < V) {
+      float t = 0.f;
+      for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
+      dbo_part[(size_t)l * V + tid] = t;
     }
   }
-  __syncthreads();
-  // dz = P (G - colv)  (fp32 in zs for dbo, bf16 copy in dzb for the MFMAs)
-  for (int b = tid; b < Bp; b += 256) {
-    float* p = zs + b * 32;
-    float dzv[32];
-#pragma unroll
-    for (int v = 0; v < 32; ++v) dzv[v] = 0.f;
-    if (b < B) {
-      float pv[32], ev[32];
-#pragma unroll
-      for (int v = 0; v < 32; ++v) pv[v] = p[v];
-      float mx = -3.4e38f;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) mx = v < V ? fmaxf(mx, pv[v]) : mx;
-      float se = 0.f;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) { ev[v] = v < V ? __expf(pv[v] - mx) : 0.f; se += ev[v]; }
-      const int yv = (int)y[(size_t)b * L + l];
-      const float coef = wl[(size_t)b * L + l] * inv_bl, inv_se = 1.0f / se;
-#pragma unroll
-      for (int v = 0; v < 32; ++v) {
-        const float g = coef * (ev[v] * inv_se - (v == yv ? 1.f : 0.f));
-        dzv[v] = v < V ? pv[v] * (g - colv[v]) : 0.f;
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < 32; ++v) p[v] = dzv[v];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) *reinterpret_cast<uint4*>(dzb + b * 64 + c * 16) = packq8(dzv + 8 * c);
-  }
-  __syncthreads();
-  // dWo_l: wave w -> channel tile w;  D[v][c] = sum_b dz^T[v][b] h[b][c]  (h chunks re-staged)
+  // dWo_l: wave w -> channel tile w & 3, row half w >> 2 of each chunk (the two halves summed
+  // through LDS);  D[v][c] = sum_b dz^T[v][b] h[b][c]  (h chunks re-staged)
   {
     f32x16_t acc = zero16();
-    const int colb = w * 32 + tc;
-    for (int c0 = 0; c0 < Bp; c0 += HC) {
+    const int colb = (w & 3) * 32 + tc;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      const int c0 = c * HC;
+      if (c0 >= Bp) break;
       __syncthreads();
-      stage_h(c0);
+      stage_h(hreg[c]);
       __syncthreads();
       const int nkb = min(HC, Bp - c0) / 16;
-      for (int kb = 0; kb < nkb; ++kb) {
+      for (int kb = (w >> 2); kb < nkb; kb += 2) {
         const int ra = kb * 16 + 8 * hh + q;
         const bf16x8 fa =
             cat_tr(lds_tr(dzb, (c0 + ra) * 64 + tc * 2), lds_tr(dzb, (c0 + ra + 4) * 64 + tc * 2));
@@ -530,24 +550,29 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
         acc = mfma32(fa, fb, acc);
       }
     }
-    float* dst = dwo_part + (size_t)l * V * 128;
+    // waves 4-7 hand their half to waves 0-3 through the (free) dh staging tile
+    __syncthreads();
+    float* xch = reinterpret_cast<float*>(hs);                // [4 waves][16][64 lanes] fp32 = 16 KB
+    if (w >= 4) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int v = (i & 3) + 8 * (i >> 2) + 4 * hh;
-      if (v < V) dst[v * 128 + w * 32 + r] = acc[i];
+      for (int i = 0; i < 16; ++i) xch[((w - 4) * 16 + i) * 64 + lane] = acc[i];
     }
-  }
-  if (tid < 32 && tid < V) {
-    float a = 0.f;
-    for (int b = 0; b < B; ++b) a += zs[b * 32 + tid];
-    dbo_part[(size_t)l * V + tid] = a;
+    __syncthreads();
+    if (w < 4) {
+      float* dst = dwo_part + (size_t)l * V * 128;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int v = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        if (v < V) dst[v * 128 + w * 32 + r] = acc[i] + xch[(w * 16 + i) * 64 + lane];
+      }
+    }
   }
   // dh: D[b][c] = sum_v dz[b][v] Wo[v][c]; per chunk: wave -> row tile, all 4 channel tiles, staged
   // in hs for 256-B row stores
   for (int c0 = 0; c0 < Bp; c0 += HC) {
     __syncthreads();                            // hs free (previous chunk stored / dWo done)
     const int rt = c0 / 32 + w;
-    if (rt < Bp / 32) {
+    if (w < HC / 32 && rt < Bp / 32) {
     f32x16_t acc[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
@@ -573,7 +598,7 @@ __global__ void __launch_bounds__(256) local_head_mfma_kernel(
       }
     }
     __syncthreads();
-    for (int idx = tid; idx < HC * 16; idx += 256) {
+    for (int idx = tid; idx < HC * 16; idx += 512) {
       const int b = c0 + (idx >> 4), c8 = idx & 15;
       if (b < B)
         *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
@@ -667,9 +692,9 @@ PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, c
     attr = true;
   }
   const int Bp = (B + 31) & ~31;
-  const int lds_m = 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (8 * 32 + 96) * 4;
+  const int lds_m = 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (16 * 32 + 96) * 4;
   if (lds_m <= 163840) {
-    hipLaunchKernelGGL(local_head_mfma_kernel, dim3(L), dim3(256), lds_m, st, (const bf16_t*)h, wo, bo,
+    hipLaunchKernelGGL(local_head_mfma_kernel, dim3(L), dim3(512), lds_m, st, (const bf16_t*)h, wo, bo,
                        (const long long*)y, wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V,
                        1.0f / ((float)B * (float)L));
     return pbx_launch_status();
