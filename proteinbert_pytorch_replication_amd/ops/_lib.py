@@ -13,7 +13,11 @@ from typing import Optional
 
 import torch
 
-from .build import HIP_LIB, HOST_LIB
+from .build import HIP_LIB as _BUILT_HIP_LIB, HOST_LIB
+
+# PBX_HIP_LIB: load an alternative build of the kernel library (A/B comparisons of kernel variants
+# inside one process launch on the same GPU); the in-tree build otherwise
+HIP_LIB = os.environ.get("PBX_HIP_LIB") or _BUILT_HIP_LIB
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

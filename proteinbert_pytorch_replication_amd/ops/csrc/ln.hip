@@ -167,9 +167,16 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
     const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
 #pragma unroll
+    for (int e = 0; e < 8; ++e) pre[e] = yv[e] + bb[e];
+    f32x2 gg[4];
+    {
+      const f32x2 xi[4] = {(f32x2){pre[0], pre[1]}, (f32x2){pre[2], pre[3]}, (f32x2){pre[4], pre[5]},
+                           (f32x2){pre[6], pre[7]}};
+      gelu2_fast_n<4, false>(xi, gg);
+    }
+#pragma unroll
     for (int e = 0; e < 8; ++e) {
-      pre[e] = yv[e] + bb[e];
-      o[e] = okl ? bfround(h1[e] + gelu_f(pre[e])) : 0.f;
+      o[e] = okl ? bfround(h1[e] + ((e & 1) ? gg[e >> 1].y : gg[e >> 1].x)) : 0.f;
       lsum += o[e];
     }
     if (okl) {
@@ -518,13 +525,25 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     unpack8(n_s2, sv2);
     unpack8(n_pr, pr);
     unpack8(n_s1, sv1);
+    float gp[8];
+    {
+      const f32x2 xi[4] = {(f32x2){pr[0], pr[1]}, (f32x2){pr[2], pr[3]}, (f32x2){pr[4], pr[5]},
+                           (f32x2){pr[6], pr[7]}};
+      f32x2 go[4];
+      gelu2_fast_n<4, true>(xi, go);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        gp[2 * e] = go[e].x;
+        gp[2 * e + 1] = go[e].y;
+      }
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xh2 = (sv2[e] - mean2) * rstd2;
       adg2[e] += okc ? dh[e] * xh2 : 0.f;
       adb2[e] += okc ? dh[e] : 0.f;
       ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
-      dp[e] = ds2[e] * gelu_grad_f(pr[e]);
+      dp[e] = ds2[e] * gp[e];
       xh1[e] = (sv1[e] - mean1) * rstd1;
       hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
     }
