@@ -20,6 +20,7 @@
 // Backward data path in the same structure; the weight gradients dW = dU^T X (K = B rows) are
 // left to three library GEMMs the caller issues off the critical path.
 #include "mfma.h"
+#include <stdlib.h>
 
 using namespace pbx;
 typedef unsigned short bf16_t;
@@ -27,7 +28,6 @@ typedef unsigned short bf16_t;
 namespace {
 typedef __attribute__((ext_vector_type(4))) float f4_t;
 constexpr int RB = 16;       // rows per workgroup
-constexpr int NWV = 8;       // waves per workgroup
 constexpr int PF = 4;        // B-fragment prefetch depth (k-steps in flight)
 
 __device__ __forceinline__ f4_t mfma16(const bf16x8& a, const bf16x8& b, const f4_t& c) {
@@ -70,8 +70,8 @@ __device__ __forceinline__ void gemm_rows(f4_t* acc, const unsigned char* at, in
 }
 
 // per-row sums of v[t][i] (row 4q + i) over the workgroup's columns: lanes of one q share rows;
-// red: [NWV][RB] floats.  Returns the 4 row totals of this lane's rows.
-template <int NT>
+// red: [NW][RB] floats.  Returns the 4 row totals of this lane's rows.
+template <int NT, int NW>
 __device__ __forceinline__ void row_sums(const float (*v)[4], float* red, float* out, int lane, int w) {
   float s[4];
 #pragma unroll
@@ -94,7 +94,7 @@ __device__ __forceinline__ void row_sums(const float (*v)[4], float* red, float*
   for (int i = 0; i < 4; ++i) {
     float a = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < NWV; ++ww) a += red[ww * RB + 4 * q + i];
+    for (int ww = 0; ww < NW; ++ww) a += red[ww * RB + 4 * q + i];
     out[i] = a;
   }
 }
@@ -115,9 +115,10 @@ __device__ __forceinline__ void col_atomic(const float (*v)[4], const bool* rok,
 }
 
 // ------------------------------------------------------------------------------------------------
-// forward.  NT = G / 128 column tiles per wave, NT3 = NGL / 128 (0: last block, no gb).
-template <int NT, int NT3>
-__global__ void __launch_bounds__(512) glob_fwd_kernel(
+// forward.  NW waves of NT column tiles each (G = 16 NT NW); NGL = 0 (last block, no gb) or 128
+// (waves 0 .. NGL/16 - 1 compute one gb column tile each).
+template <int NT, int NW, int NGL>
+__global__ void __launch_bounds__(NW * 64) glob_fwd_kernel(
     const float* __restrict__ g, const bf16_t* __restrict__ g_bf, const float* __restrict__ vpart, int TV,
     const float* __restrict__ wp, int K, const bf16x8* __restrict__ f1, const float* __restrict__ b1,
     const float* __restrict__ n1w, const float* __restrict__ n1b, const bf16x8* __restrict__ f2,
@@ -126,9 +127,9 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
     float* __restrict__ r1, float* __restrict__ vsum, bf16_t* __restrict__ g1_bf, float* __restrict__ pre2,
     float* __restrict__ xh2, float* __restrict__ r2, float* __restrict__ g2, bf16_t* __restrict__ g2_bf,
     float* __restrict__ pregl, float* __restrict__ gb, int B, float eps) {
-  constexpr int G = NT * 128, NGL = NT3 * 128;
+  constexpr int G = NT * 16 * NW, NT3 = NGL > 0 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) unsigned char at[RB * G * 2];
-  __shared__ float red[NWV * RB];
+  __shared__ float red[NW * RB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, q = lane >> 4;
   const int row0 = blockIdx.x * RB;
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
   }
   const int col0 = w * NT * 16;
   // A tile <- g_bf rows
-  for (int idx = tid; idx < RB * G / 8; idx += 512) {
+  for (int idx = tid; idx < RB * G / 8; idx += NW * 64) {
     const int row = idx / (G / 8), ch = idx % (G / 8);
     const int gr = min(row0 + row, B - 1);
     *reinterpret_cast<uint4*>(at + atile(row, ch, G)) =
@@ -190,7 +191,7 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
       }
     }
     float mean[4], var[4];
-    row_sums<NT>(z, red, mean, lane, w);
+    row_sums<NT, NW>(z, red, mean, lane, w);
 #pragma unroll
     for (int i = 0; i < 4; ++i) mean[i] *= 1.f / (float)G;
     float d2[NT][4];
@@ -198,7 +199,7 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) d2[t][i] = (z[t][i] - mean[i]) * (z[t][i] - mean[i]);
-    row_sums<NT>(d2, red, var, lane, w);
+    row_sums<NT, NW>(d2, red, var, lane, w);
     float rs[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) rs[i] = rsqrtf(var[i] * (1.f / (float)G) + eps);
@@ -259,6 +260,7 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
   }
   // ---- gb = GELU(g2 Wgl^T + bgl) (the next block's global->local vector) ----
   if constexpr (NT3 > 0) {
+    if (w >= NGL / 16) return;                    // (no barrier below)
     f4_t acc[NT3];
 #pragma unroll
     for (int t = 0; t < NT3; ++t) acc[t] = (f4_t){0.f, 0.f, 0.f, 0.f};
@@ -285,8 +287,8 @@ __global__ void __launch_bounds__(512) glob_fwd_kernel(
 // attention partial-sum gradient, identical for every tile), du1/du2/dugl (bf16, the weight
 // gradient GEMM operands), and column-sum gradients accumulated with one atomic per column and
 // workgroup: db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl, dwp.
-template <int NT, int NT3>
-__global__ void __launch_bounds__(512) glob_bwd_kernel(
+template <int NT, int NW, int NGL>
+__global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
     const float* __restrict__ dg2_in, const float* __restrict__ dgb, const float* __restrict__ pregl,
     const bf16x8* __restrict__ fglT, const float* __restrict__ xh2, const float* __restrict__ r2,
     const float* __restrict__ n2w, const float* __restrict__ pre2, const bf16x8* __restrict__ f2T,
@@ -296,9 +298,9 @@ __global__ void __launch_bounds__(512) glob_bwd_kernel(
     bf16_t* __restrict__ du2, bf16_t* __restrict__ dugl, float* __restrict__ db1, float* __restrict__ dn1w,
     float* __restrict__ dn1b, float* __restrict__ db2, float* __restrict__ dn2w, float* __restrict__ dn2b,
     float* __restrict__ dbgl, float* __restrict__ dwp, int B) {
-  constexpr int G = NT * 128, NGL = NT3 * 128;
+  constexpr int G = NT * 16 * NW, NT3 = NGL > 0 ? 1 : 0;
   __shared__ __attribute__((aligned(16))) unsigned char at[RB * G * 2];
-  __shared__ float red[NWV * RB];
+  __shared__ float red[NW * RB];
   __shared__ float dsum[NT3 > 0 ? RB * NGL : 1];   // fp32 dugl for the bias-gradient column sums
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int c16 = lane & 15, q = lane >> 4;
@@ -319,7 +321,7 @@ __global__ void __launch_bounds__(512) glob_bwd_kernel(
 
   // ---- gb = GELU(pregl): dugl = dgb * GELU'(pregl) ; dg2 += dugl Wgl ----
   if constexpr (NT3 > 0) {
-    for (int idx = tid; idx < RB * NGL; idx += 512) {
+    for (int idx = tid; idx < RB * NGL; idx += NW * 64) {
       const int row = idx / NGL, c = idx % NGL;
       const int gr = min(row0 + row, B - 1);
       const bool ok = row0 + row < B;
@@ -330,7 +332,7 @@ __global__ void __launch_bounds__(512) glob_bwd_kernel(
       if (ok) dugl[(size_t)gr * NGL + c] = db;
     }
     __syncthreads();
-    for (int c = tid; c < NGL; c += 512) {        // dbgl: column sums over the rows
+    for (int c = tid; c < NGL; c += NW * 64) {    // dbgl: column sums over the rows
       float a = 0.f;
       for (int row = 0; row < RB; ++row) a += dsum[row * NGL + c];
       atomicAdd(dbgl + c, a);
@@ -369,8 +371,8 @@ __global__ void __launch_bounds__(512) glob_bwd_kernel(
       for (int i = 0; i < 4; ++i) tmp[t][i] = dyv[t][i];
     col_atomic<NT>(tmp, rok, dbet, col0, lane);
     float m1[4], m2[4], rs[4];
-    row_sums<NT>(dxh, red, m1, lane, w);
-    row_sums<NT>(dxx, red, m2, lane, w);
+    row_sums<NT, NW>(dxh, red, m1, lane, w);
+    row_sums<NT, NW>(dxx, red, m2, lane, w);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       m1[i] *= 1.f / (float)G;
@@ -429,7 +431,7 @@ __global__ void __launch_bounds__(512) glob_bwd_kernel(
     if (tid < K) {
       float a = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < NWV; ++ww) a += red[ww];
+      for (int ww = 0; ww < NW; ++ww) a += red[ww];
       atomicAdd(dwp + tid, a / (float)K);
     }
     gemm_rows<NT>(acc, at, G, f1T, w * NT, lane);
@@ -459,9 +461,9 @@ __global__ void __launch_bounds__(256) pack_glob_frags_kernel(const float* __res
   }
 }
 
-template <int NT, int NT3>
+template <int NT, int NW, int NGL>
 void launch_fwd(int B, const void* const* p, const int* iv, float eps, hipStream_t st) {
-  hipLaunchKernelGGL((glob_fwd_kernel<NT, NT3>), dim3((B + RB - 1) / RB), dim3(512), 0, st, (const float*)p[0],
+  hipLaunchKernelGGL((glob_fwd_kernel<NT, NW, NGL>), dim3((B + RB - 1) / RB), dim3(NW * 64), 0, st, (const float*)p[0],
                      (const bf16_t*)p[1], (const float*)p[2], iv[0], (const float*)p[3], iv[1],
                      (const bf16x8*)p[4], (const float*)p[5], (const float*)p[6], (const float*)p[7],
                      (const bf16x8*)p[8], (const float*)p[9], (const float*)p[10], (const float*)p[11],
@@ -470,15 +472,21 @@ void launch_fwd(int B, const void* const* p, const int* iv, float eps, hipStream
                      (bf16_t*)p[23], (float*)p[24], (float*)p[25], B, eps);
 }
 
-template <int NT, int NT3>
+template <int NT, int NW, int NGL>
 void launch_bwd(int B, const void* const* p, int K, hipStream_t st) {
-  hipLaunchKernelGGL((glob_bwd_kernel<NT, NT3>), dim3((B + RB - 1) / RB), dim3(512), 0, st, (const float*)p[0],
+  hipLaunchKernelGGL((glob_bwd_kernel<NT, NW, NGL>), dim3((B + RB - 1) / RB), dim3(NW * 64), 0, st, (const float*)p[0],
                      (const float*)p[1], (const float*)p[2], (const bf16x8*)p[3], (const float*)p[4],
                      (const float*)p[5], (const float*)p[6], (const float*)p[7], (const bf16x8*)p[8],
                      (const float*)p[9], (const float*)p[10], (const float*)p[11], (const float*)p[12],
                      (const float*)p[13], (const float*)p[14], K, (const bf16x8*)p[15], (float*)p[16],
                      (float*)p[17], (bf16_t*)p[18], (bf16_t*)p[19], (bf16_t*)p[20], (float*)p[21], (float*)p[22],
                      (float*)p[23], (float*)p[24], (float*)p[25], (float*)p[26], (float*)p[27], (float*)p[28], B);
+}
+// forward waves per workgroup: 16 (half the column tiles per wave: shorter dependent chains per
+// row block) or 8; PBX_GLOB_WAVES overrides
+int glob_waves() {
+  static const int wv = getenv("PBX_GLOB_WAVES") ? atoi(getenv("PBX_GLOB_WAVES")) : 16;
+  return wv;
 }
 }  // namespace
 
@@ -492,8 +500,13 @@ PBX_EXPORT int pbx_glob_supported(int G, int NGL) {
 PBX_EXPORT int pbx_glob_fwd(const void* const* p, int B, int G, int NGL, int TV, int K, float eps, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1) return (int)hipErrorInvalidValue;
   const int iv[2] = {TV, K};
-  if (G == 512) (NGL ? launch_fwd<4, 1> : launch_fwd<4, 0>)(B, p, iv, eps, st);
-  else (NGL ? launch_fwd<2, 1> : launch_fwd<2, 0>)(B, p, iv, eps, st);
+  if (glob_waves() == 16) {
+    if (G == 512) (NGL ? launch_fwd<2, 16, 128> : launch_fwd<2, 16, 0>)(B, p, iv, eps, st);
+    else (NGL ? launch_fwd<1, 16, 128> : launch_fwd<1, 16, 0>)(B, p, iv, eps, st);
+  } else {
+    if (G == 512) (NGL ? launch_fwd<4, 8, 128> : launch_fwd<4, 8, 0>)(B, p, iv, eps, st);
+    else (NGL ? launch_fwd<2, 8, 128> : launch_fwd<2, 8, 0>)(B, p, iv, eps, st);
+  }
   return pbx_launch_status();
 }
 
@@ -501,8 +514,9 @@ PBX_EXPORT int pbx_glob_fwd(const void* const* p, int B, int G, int NGL, int TV,
 //    db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl, dwp   (29 pointers)
 PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1 || K > 512) return (int)hipErrorInvalidValue;
-  if (G == 512) (NGL ? launch_bwd<4, 1> : launch_bwd<4, 0>)(B, p, K, st);
-  else (NGL ? launch_bwd<2, 1> : launch_bwd<2, 0>)(B, p, K, st);
+  // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves)
+  if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, st);
+  else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, st);
   return pbx_launch_status();
 }
 
