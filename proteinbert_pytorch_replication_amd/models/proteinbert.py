@@ -136,8 +136,16 @@ class GlobalAttention(nn.Module):
         return v.float().sum(dim=1) * scale
 
     def forward_paper(self, h: torch.Tensor, g: torch.Tensor,
-                      mask: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """Per-head single query from the global track, softmax over positions."""
+                      mask: Optional[torch.Tensor] = None, use_kernel: bool = True) -> torch.Tensor:
+        """Per-head single query from the global track, softmax over positions.
+
+        bf16 on a GPU runs the split-L HIP core (``ops/paper_attention.py``); ``use_kernel=False``
+        (or any other dtype/device) is the torch oracle below.
+        """
+        if use_kernel:
+            from ..ops import paper_attention as pa
+            if pa.kernel_supported(h, self.key_dim, self.value_dim):
+                return pa.paper_attention(h, g, self.Wq, self.Wk, self.Wv, mask)
         q = torch.tanh(torch.einsum("bg,hgk->bhk", g, self.Wq.to(g.dtype)))            # [B,H,K]
         k = torch.tanh(torch.einsum("blc,hck->bhlk", h, self.Wk.to(h.dtype)))          # [B,H,L,K]
         v = _gelu(torch.einsum("blc,hcv->bhlv", h, self.Wv.to(h.dtype)))               # [B,H,L,vd]
