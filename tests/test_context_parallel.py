@@ -1,0 +1,89 @@
+"""Context (sequence) parallelism on CPU (gloo): the L-sharded forward/backward over 3 ranks
+reproduces the single-device loss, output slices and parameter gradients, in both attention
+semantics (parallel/context_parallel.py; SURVEY §2.4 SP row, §5.7)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+CFG = dict(sequences_length=96, num_annotations=40, local_dim=16, global_dim=32, key_dim=8,
+           num_heads=4, num_blocks=2)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, semantics, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.models import ProteinBERT
+    from proteinbert_pytorch_replication_amd.parallel.context_parallel import (
+        ContextParallelProteinBERT, all_reduce_grads, cp_pretrain_loss)
+    from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.manual_seed(0)
+    m = ProteinBERT(backend="torch", semantics=semantics, **CFG)
+    X, Y, W = SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=7,
+                                use_kernel=False).next_batch()
+    # single-device oracle (identical on every rank)
+    pl, pg = m(X)
+    ref_loss = pretrain_loss_torch(pl, pg, Y, W, semantics=semantics)
+    ref_loss.backward()
+    ref_grads = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    for b in m.proteinBERT_blocks:
+        for t in (b.global_attention_layer.Wq, b.global_attention_layer.Wk, b.global_attention_layer.Wv):
+            t.grad = None
+    # context-parallel
+    cp = ContextParallelProteinBERT(m)
+    pl_cp, pg_cp = cp(cp.shard(X["local"]), X["global"])
+    loss = cp_pretrain_loss(pl_cp, pg_cp, cp.shard(Y["local"]), cp.shard(W["local"]), Y["global"], W["global"],
+                            CFG["sequences_length"], world, semantics)
+    loss.backward()
+    tot = loss.detach().clone()
+    dist.all_reduce(tot)
+    params = [p for p in m.parameters()]
+    all_reduce_grads(params)
+    errs = {"loss": (tot - ref_loss.detach()).abs().item(),
+            "probs_l": (pl_cp - cp.shard(pl.detach())).abs().max().item(),
+            "probs_g": (pg_cp - pg.detach()).abs().max().item()}
+    gmax = 0.0
+    for n, p in m.named_parameters():
+        if n in ref_grads:
+            scale = max(ref_grads[n].abs().max().item(), 1e-4)   # absolute floor for ~1e-6 grads
+            gmax = max(gmax, (p.grad - ref_grads[n]).abs().max().item() / scale)
+    errs["grad_rel"] = gmax
+    errs["heads_checked"] = any(n.endswith(".Wv") for n in ref_grads)   # registered: grad_rel covers them
+    torch.save(errs, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("semantics", ["reference", "paper"])
+def test_context_parallel_matches_single_device(tmp_path, semantics):
+    world = 3
+    mp.start_processes(_worker, args=(world, _free_port(), semantics, str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        e = torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True)
+        assert e["loss"] < 1e-5, e
+        assert e["probs_l"] < 1e-5, e
+        assert e["probs_g"] < 1e-5, e
+        assert e["grad_rel"] < 1e-4, e
+        if semantics == "paper":
+            assert e["heads_checked"], e
+
+
+def test_halo_exchange_rejects_short_shard():
+    from proteinbert_pytorch_replication_amd.parallel.context_parallel import halo_exchange
+    with pytest.raises(ValueError):
+        halo_exchange(torch.zeros(1, 8, 4), 20)
