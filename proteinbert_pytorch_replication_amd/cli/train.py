@@ -66,6 +66,7 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     ap.add_argument("--async-checkpoint", action="store_true")
     ap.add_argument("--profile-steps", default=None, help="START[:COUNT] steps traced with torch.profiler")
     ap.add_argument("--profile-dir", default=None, help="trace output directory (default: save path)")
+    ap.add_argument("--zero", action="store_true", help="ZeRO-1: shard the Adam moments over the DP ranks")
     a = ap.parse_args(argv)
     cfg = _cfg(a)
     logging.basicConfig(format="%(asctime)s [%(levelname)s]: %(message)s", level=logging.INFO)
@@ -104,7 +105,8 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
                    optim_scheduler_patience=cfg.optim.plateau_patience, warmup_duration=cfg.optim.warmup_duration,
                    device=dev, log_every=a.log_every, bucket_mb=cfg.dist.bucket_mb, compute_dtype=cfg.kernel.dtype,
                    grad_clip=cfg.optim.grad_clip, async_checkpoint=a.async_checkpoint, metrics_path=a.metrics,
-                   resume=a.resume, profile_steps=a.profile_steps, profile_dir=a.profile_dir)
+                   resume=a.resume, profile_steps=a.profile_steps, profile_dir=a.profile_dir,
+                   zero_optimizer=a.zero)
     if info.is_main:
         print(json.dumps({"final_loss": res["train_loss"][-1] if res["train_loss"] else None,
                           "iterations": len(res["train_loss"]), "final_model": res.get("final_model_path")}))

@@ -1,5 +1,6 @@
 """Parallelism over RCCL/xGMI: process-group bootstrap, bucketed all-reduce, sharded sampling,
-and context (sequence) parallelism over the residue axis (``context_parallel``).
+ZeRO-1 sharded Adam (``zero``) and context (sequence) parallelism over the residue axis
+(``context_parallel``).
 
 Tensor/pipeline/expert parallelism are not provided: the reference has none and
 the 16.8M-parameter model fits one MI355X many times over.
@@ -8,9 +9,11 @@ from .dist import (DistInfo, init_distributed, get_info, is_main, barrier, all_r
                    broadcast_module, destroy)
 from .ddp import BucketedAllReduce
 from .sampler import ShardedSampler
+from .zero import ZeroFusedAdam
 from .context_parallel import (ContextParallelProteinBERT, all_reduce_grads, cp_pretrain_loss, halo_exchange,
                                make_cp_groups)
 
 __all__ = ["DistInfo", "init_distributed", "get_info", "is_main", "barrier", "all_reduce_max",
            "all_reduce_mean_", "broadcast_module", "destroy", "BucketedAllReduce", "ShardedSampler",
-           "ContextParallelProteinBERT", "all_reduce_grads", "cp_pretrain_loss", "halo_exchange", "make_cp_groups"]
+           "ContextParallelProteinBERT", "all_reduce_grads", "cp_pretrain_loss", "halo_exchange", "make_cp_groups",
+           "ZeroFusedAdam"]

@@ -70,7 +70,7 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
              log_every: int = 1, bucket_mb: float = 8.0, compute_dtype="auto", grad_clip: Optional[float] = None,
              async_checkpoint: bool = False, metrics_path: Optional[str] = None, resume: str = "none",
              fuse_optimizer: bool = True, final_save: bool = True, profile_steps: Optional[str] = None,
-             profile_dir: Optional[str] = None) -> Dict[str, Any]:
+             profile_dir: Optional[str] = None, zero_optimizer: bool = False) -> Dict[str, Any]:
     info = pdist.init_distributed()
     if device is None:
         device = info.device
@@ -82,10 +82,23 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
 
     ddp = None
     if info.distributed:
+        from ..parallel.zero import ZeroFusedAdam
         if not isinstance(optimizer, FusedAdam):
             raise ValueError("data-parallel pretrain needs FusedAdam (flat gradient arena)")
-        ddp = BucketedAllReduce(optimizer.arena, bucket_mb=bucket_mb)
-        ddp.broadcast_parameters(model)
+        if zero_optimizer and not isinstance(optimizer, ZeroFusedAdam):
+            # ZeRO-1: Adam moments sharded over the DP ranks (parallel/zero.py); reduce-scatter at step()
+            g = optimizer.param_groups[0]
+            zopt = ZeroFusedAdam(optimizer.arena, lr=g["lr"], betas=g["betas"], eps=g["eps"],
+                                 weight_decay=g["weight_decay"])
+            if optimizer.step_count:
+                zopt.load_state_dict(optimizer.state_dict())
+            optimizer = zopt
+            results["optimizer"] = optimizer
+        if isinstance(optimizer, ZeroFusedAdam):
+            pdist.broadcast_module(model)
+        else:
+            ddp = BucketedAllReduce(optimizer.arena, bucket_mb=bucket_mb)
+            ddp.broadcast_parameters(model)
 
     scheduler = WarmupThenPlateau(optimizer, warmup_duration=warmup_duration, patience=optim_scheduler_patience)
     step_fn = PretrainStep(model, optimizer, ddp, local_loss_fn, global_loss_fn, compute_dtype, grad_clip)

@@ -87,3 +87,50 @@ def test_halo_exchange_rejects_short_shard():
     from proteinbert_pytorch_replication_amd.parallel.context_parallel import halo_exchange
     with pytest.raises(ValueError):
         halo_exchange(torch.zeros(1, 8, 4), 20)
+
+
+def _hybrid_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.models import ProteinBERT
+    from proteinbert_pytorch_replication_amd.parallel.context_parallel import (
+        ContextParallelProteinBERT, all_reduce_grads, cp_pretrain_loss, make_cp_groups)
+    from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cp_size = 2
+    cp_group, dp_group = make_cp_groups(cp_size)
+    cfg = dict(CFG, sequences_length=64)
+    torch.manual_seed(0)
+    m = ProteinBERT(backend="torch", **cfg)
+    batches = [SyntheticUniRefGO(64, cfg["num_annotations"], 2, "cpu", seed=20 + i, use_kernel=False).next_batch()
+               for i in range(world // cp_size)]
+    # oracle: DP mean of the per-batch single-device gradients
+    for X, Y, W in batches:
+        pl, pg = m(X)
+        (pretrain_loss_torch(pl, pg, Y, W) / len(batches)).backward()
+    ref = {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    cp = ContextParallelProteinBERT(m, cp_group)
+    X, Y, W = batches[rank // cp_size]
+    pl, pg = cp(cp.shard(X["local"]), X["global"])
+    cp_pretrain_loss(pl, pg, cp.shard(Y["local"]), cp.shard(W["local"]), Y["global"], W["global"], 64,
+                     cp_size).backward()
+    params = list(m.parameters())
+    all_reduce_grads(params, cp_group)
+    all_reduce_grads(params, dp_group, average_over=world // cp_size)
+    err = max((p.grad - ref[n]).abs().max().item() / max(ref[n].abs().max().item(), 1e-4)
+              for n, p in m.named_parameters() if n in ref)
+    torch.save({"err": err}, os.path.join(out_dir, f"h{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def test_cp_x_dp_groups_match_dp_mean(tmp_path):
+    world = 4
+    mp.start_processes(_hybrid_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        e = torch.load(os.path.join(tmp_path, f"h{r}.pt"), weights_only=True)
+        assert e["err"] < 1e-4, e

@@ -84,7 +84,7 @@ def test_dp_bucketed_allreduce_equals_averaged_gradients(tmp_path):
         torch.testing.assert_close(r0[k], v, rtol=1e-4, atol=2e-5, msg=k)
 
 
-def _pretrain_worker(rank, world, port, save):
+def _pretrain_worker(rank, world, port, save, zero=False):
     _env(rank, world, port)
     torch.set_num_threads(1)
     from proteinbert_pytorch_replication_amd.train.pretrain import pretrain
@@ -92,17 +92,24 @@ def _pretrain_worker(rank, world, port, save):
     m = ProteinBERT(backend="torch", **CFG)
     gen = SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=rank, use_kernel=False)
     pretrain(m, gen, torch.optim.Adam(m.parameters(), lr=1e-3), max_batch_iterations=5, save_path=save,
-             nb_iterations_checkpoint=2, warmup_duration=2, device="cpu")
+             nb_iterations_checkpoint=2, warmup_duration=2, device="cpu", zero_optimizer=zero)
 
 
-def test_dp_pretrain_rank0_checkpoints(tmp_path):
-    mp.start_processes(_pretrain_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn",
-                       join=True)
+@pytest.mark.parametrize("zero", [False, True])
+def test_dp_pretrain_rank0_checkpoints(tmp_path, zero):
+    mp.start_processes(_pretrain_worker, args=(2, _free_port(), str(tmp_path), zero), nprocs=2,
+                       start_method="spawn", join=True)
     files = sorted(os.listdir(tmp_path))
     assert "proteinbert_pretraining_checkpoint_2.pt" in files and "proteinbert_pretraining_checkpoint_4.pt" in files
     assert len([f for f in files if f.startswith("proteinbert_pretrained_model_")]) == 1
     blob = torch.load(tmp_path / "proteinbert_pretraining_checkpoint_4.pt", weights_only=False)
     assert blob["extra_state"]["world_size"] == 2
+    # ZeRO-1 checkpoints hold the gathered (full-size) moments, same format as the all-reduce path
+    m = ProteinBERT(backend="torch", **CFG)
+    shapes = [p.shape for p in m.parameters()]
+    st = blob["optimizer_state_dict"]["state"]
+    assert len(st) == len(shapes)
+    assert sorted(tuple(v["exp_avg"].shape) for v in st.values()) == sorted(tuple(s) for s in shapes)
 
 
 SCRIPT = r'''
