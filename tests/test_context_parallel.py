@@ -134,3 +134,34 @@ def test_cp_x_dp_groups_match_dp_mean(tmp_path):
     for r in range(world):
         e = torch.load(os.path.join(tmp_path, f"h{r}.pt"), weights_only=True)
         assert e["err"] < 1e-4, e
+
+
+@pytest.mark.gpu
+def test_context_parallel_gpu_rccl_long_sequence():
+    """1-rank RCCL group on the GPU at L=4096 (BASELINE cfg 4 length), bf16 activations: the CP
+    forward (halo path with zero padding, all-reduced LN / attention pool) equals the single-shard
+    torch encoder and the backward runs."""
+    import datetime
+    import torch.distributed as dist
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.models import ProteinBERT
+    from proteinbert_pytorch_replication_amd.parallel.context_parallel import ContextParallelProteinBERT
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_free_port()}", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0))
+    try:
+        torch.manual_seed(0)
+        m = ProteinBERT(sequences_length=4096, num_annotations=8943, local_dim=128, global_dim=512, key_dim=64,
+                        num_heads=4, num_blocks=2, device="cuda", backend="torch")
+        X, _, _ = SyntheticUniRefGO(4096, 8943, 2, "cuda", seed=3).next_batch()
+        cp = ContextParallelProteinBERT(m, compute_dtype=torch.bfloat16)
+        pl, pg = cp(cp.shard(X["local"]), X["global"])
+        h, g = m.encode_torch(X["local"], X["global"], compute_dtype=torch.bfloat16)
+        rl, rg = m.heads_torch(h, g)
+        # bf16 activations: the two LN formulations round differently, so bound max and mean error
+        assert float((pl - rl).abs().max()) < 5e-2 and float((pl - rl).abs().mean()) < 5e-3
+        assert float((pg - rg).abs().max()) < 5e-2 and float((pg - rg).abs().mean()) < 5e-3
+        (pl.float().square().mean() + pg.mean()).backward()
+        torch.cuda.synchronize()
+        assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+    finally:
+        dist.destroy_process_group()
