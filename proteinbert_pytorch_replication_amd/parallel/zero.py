@@ -48,6 +48,8 @@ class ZeroFusedAdam(FusedAdam):
         self._ppad = torch.zeros(self.shard * self.world, dtype=torch.float32, device=dev)
         self.grad_scale = 1.0 / self.world
         self._native = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+        self._clip_pending: Optional[float] = None
+        self._last_norm = torch.zeros((), dtype=torch.float32, device=dev)
 
     # -- collectives ---------------------------------------------------------------------------
     def _reduce_scatter(self) -> None:
@@ -84,6 +86,8 @@ class ZeroFusedAdam(FusedAdam):
         if not a.grads_attached():
             a.attach_grads()
         self._reduce_scatter()
+        if self._clip_pending is not None:
+            self._apply_clip()
         n = self.hi - self.lo
         if n > 0:
             p = a.data[self.lo:self.hi]
@@ -117,8 +121,24 @@ class ZeroFusedAdam(FusedAdam):
 
     @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
-        raise NotImplementedError("ZeroFusedAdam: clip after the reduce-scatter is not wired; use FusedAdam + "
-                                  "BucketedAllReduce for clipped fine-tuning")
+        """Deferred global-norm clip: the reduced gradient only exists after ``step()``'s
+        reduce-scatter, so the clip is applied there (norm of the mean gradient = sqrt of the
+        all-reduced shard sums of squares; same ``max_norm / (norm + 1e-6)`` rule as FusedAdam).
+        Returns a 0-dim tensor that ``step()`` fills with the pre-clip norm."""
+        self._clip_pending = float(max_norm)
+        return self._last_norm
+
+    def _apply_clip(self) -> None:
+        n = self.hi - self.lo
+        g = self._gshard[:n] * self.grad_scale
+        sumsq = (g * g).sum().reshape(1) if n > 0 else self._gshard.new_zeros(1)
+        if self.world > 1:
+            dist.all_reduce(sumsq, group=self.pg)
+        norm = sumsq.sqrt()
+        self._last_norm.copy_(norm[0])
+        coef = torch.clamp(self._clip_pending / (norm + 1e-6), max=1.0)
+        self._gshard.mul_(coef)
+        self._clip_pending = None
 
     # -- checkpoints: gather the full moments so the format is torch.optim.Adam's -------------------
     def _full(self, t: torch.Tensor) -> torch.Tensor:

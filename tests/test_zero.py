@@ -20,7 +20,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, clip=None):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(port))
     torch.set_num_threads(1)
@@ -38,10 +38,10 @@ def _worker(rank, world, port, out_dir):
     mb = ProteinBERT(backend="torch", **CFG)
     oa = FusedAdam(ma.parameters(), lr=1e-2)
     ddp = BucketedAllReduce(oa.arena, bucket_mb=0.01)
-    sa = PretrainStep(ma, oa, ddp)
+    sa = PretrainStep(ma, oa, ddp, grad_clip=clip)
     ob = ZeroFusedAdam(mb.parameters(), lr=1e-2)
     assert ob.exp_avg.numel() * world <= oa.exp_avg.numel() + 64 * world
-    sb = PretrainStep(mb, ob)
+    sb = PretrainStep(mb, ob, grad_clip=clip)
     gen = SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=50 + rank,
                             use_kernel=False)
     for _ in range(3):
@@ -60,13 +60,16 @@ def _worker(rank, world, port, out_dir):
     pdist.destroy()
 
 
-def test_zero1_matches_allreduce_adam(tmp_path):
+@pytest.mark.parametrize("clip", [None, 0.05])
+def test_zero1_matches_allreduce_adam(tmp_path, clip):
     world = 2
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, start_method="spawn",
-                       join=True)
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), clip), nprocs=world,
+                       start_method="spawn", join=True)
     for r in range(world):
         e = torch.load(os.path.join(tmp_path, f"r{r}.pt"), weights_only=True)
-        assert e["perr"] < 1e-6, e
+        # with clipping the two paths sum the squared norm in different orders; Adam's m/sqrt(v)
+        # amplifies that rounding for near-zero gradient entries (lr=1e-2 bounds a step at 1e-2)
+        assert e["perr"] < (1e-6 if clip is None else 1e-3), e
         assert e["serr"] < 1e-6, e
         assert e["rt"] == 0.0, e
         assert e["steps"] == 3, e
@@ -89,12 +92,15 @@ def test_zero1_gpu_rccl_matches_fused_adam():
         pb = [torch.nn.Parameter(p.detach().clone()) for p in pa]
         oa, ob = FusedAdam(pa, lr=1e-3), ZeroFusedAdam(pb, lr=1e-3)
         assert ob._native
-        for _ in range(3):
+        for i in range(3):
             g = torch.randn(oa.arena.numel, device="cuda")
             oa.arena.grad.copy_(g)
             ob.arena.grad.copy_(g)
+            if i == 2:      # HIP grad-norm clip kernel vs the deferred shard clip
+                na, nb = oa.clip_grad_norm_(100.0), ob.clip_grad_norm_(100.0)
             oa.step()
             ob.step()
+        assert abs(float(na) - float(nb)) < 1e-3 * float(na)
         torch.cuda.synchronize()
         assert float((oa.arena.data - ob.arena.data).abs().max()) < 1e-6
         assert float((oa.exp_avg_sq - ob.exp_avg_sq[:oa.arena.numel]).abs().max()) < 1e-6
