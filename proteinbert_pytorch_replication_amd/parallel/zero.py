@@ -86,6 +86,16 @@ class ZeroFusedAdam(FusedAdam):
         if not a.grads_attached():
             a.attach_grads()
         self._reduce_scatter()
+        if self.skip_flag is not None:
+            # the caller's flag came from this rank's LOCAL (un-reduced) gradient; a non-finite
+            # value on any rank lands in some rank's reduced shard, so decide from the shards and
+            # agree over the group (MAX) - every rank skips together, no NaN reaches the all-gather
+            n = self.hi - self.lo
+            bad = (~torch.isfinite(self._gshard[:n].sum())).to(torch.int32).reshape(1) if n > 0 \
+                else torch.zeros(1, dtype=torch.int32, device=self._gshard.device)
+            if self.world > 1:
+                dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=self.pg)
+            self.skip_flag = bad
         if self._clip_pending is not None:
             self._apply_clip()
         n = self.hi - self.lo

@@ -125,9 +125,12 @@ class FusedAdam(torch.optim.Optimizer):
             ws = torch.empty(1025, dtype=torch.float32, device=a.grad.device)
             _lib.call("pbx_sumsq_flat", a.grad.data_ptr(), a.numel, ws.data_ptr(), ws[1024:].data_ptr(),
                       _lib.stream_ptr(a.grad.device))
+            # sumsq of the (grad_scale-scaled) mean gradient: the clip coefficient max_norm / norm
+            # is scale-invariant once both sides refer to the same gradient, so the raw threshold
+            # is passed (the coefficient multiplies the unscaled SUM gradient in place)
             sumsq = ws[1024:] * (self.grad_scale ** 2)
             _lib.call("pbx_clip_scale_flat", a.grad.data_ptr(), a.numel, sumsq.data_ptr(),
-                      float(max_norm / self.grad_scale), _lib.stream_ptr(a.grad.device))
+                      float(max_norm), _lib.stream_ptr(a.grad.device))
             return sumsq.sqrt()[0]
         norm = (a.grad * self.grad_scale).norm()
         c = max_norm / (norm + 1e-6)

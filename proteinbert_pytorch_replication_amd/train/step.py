@@ -75,7 +75,9 @@ class PretrainStep:
             else:
                 torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.grad_clip)
         if self.fused and self.skip_nonfinite:
-            # all-reduced grads: every rank takes the same decision, no host sync
+            # all-reduced grads (bucketed DP): every rank takes the same decision, no host sync.
+            # ZeroFusedAdam reduces inside step() and replaces this local flag by a group-wide
+            # decision over the reduced shards (parallel/zero.py)
             opt.skip_flag = (~torch.isfinite(opt.arena.grad.sum())).to(torch.int32).reshape(1)
         opt.step()
         return loss.detach()

@@ -58,6 +58,33 @@ def test_clip_grad_norm_gpu():
     torch.testing.assert_close(p.grad.norm(), torch.tensor(1.0, device="cuda"), rtol=1e-3, atol=1e-3)
 
 
+@pytest.mark.parametrize("grad_scale", [0.5, 0.125])
+def test_clip_grad_norm_gpu_grad_scale(grad_scale):
+    """Under DP the arena holds the SUM gradient and grad_scale=1/world turns it into the mean: the
+    HIP clip must match the CPU branch and torch's clip_grad_norm_ applied to grad*grad_scale."""
+    torch.manual_seed(1)
+    g0 = torch.randn(7001) * 3.0
+    p = torch.nn.Parameter(torch.zeros(7001, device="cuda"))
+    fa = FusedAdam([p], lr=0.1)
+    fa.grad_scale = grad_scale
+    p.grad.copy_(g0.cuda())
+    norm = fa.clip_grad_norm_(1.0)
+    # CPU branch of the same optimizer
+    q = torch.nn.Parameter(torch.zeros(7001))
+    fc = FusedAdam([q], lr=0.1, bf16_shadow=False)
+    fc.grad_scale = grad_scale
+    q.grad.copy_(g0)
+    norm_c = fc.clip_grad_norm_(1.0)
+    # torch oracle on the mean gradient
+    r = torch.nn.Parameter(torch.zeros(7001))
+    r.grad = g0 * grad_scale
+    norm_t = torch.nn.utils.clip_grad_norm_([r], 1.0)
+    torch.testing.assert_close(norm.cpu(), norm_t, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(torch.as_tensor(norm_c).float(), norm_t, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close((p.grad * grad_scale).cpu(), r.grad, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(p.grad.cpu(), q.grad, rtol=1e-4, atol=1e-6)
+
+
 def test_synth_and_corrupt_kernels():
     from proteinbert_pytorch_replication_amd.ops.corrupt import synth_batch, corrupt_batch
     B, L, A = 512, 128, 2000

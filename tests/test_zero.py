@@ -75,6 +75,48 @@ def test_zero1_matches_allreduce_adam(tmp_path, clip):
         assert e["steps"] == 3, e
 
 
+def _inf_worker(rank, world, port, out_dir):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    import torch.distributed as dist
+    from proteinbert_pytorch_replication_amd.models import ProteinBERT
+    from proteinbert_pytorch_replication_amd.parallel import dist as pdist
+    from proteinbert_pytorch_replication_amd.parallel.zero import ZeroFusedAdam
+    pdist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    m = ProteinBERT(backend="torch", **CFG)
+    o = ZeroFusedAdam(m.parameters(), lr=1e-2)
+    before = o.arena.data.clone()
+    g = torch.Generator().manual_seed(rank)
+    o.arena.grad.copy_(torch.randn(o.arena.numel, generator=g))
+    if rank == 1:
+        # a non-finite LOCAL gradient on one rank only, inside rank 0's shard of the arena
+        o.arena.grad[3] = float("inf")
+    # PretrainStep's flag from the local gradient: only rank 1 sees the Inf
+    o.skip_flag = (~torch.isfinite(o.arena.grad.sum())).to(torch.int32).reshape(1)
+    o.step()
+    finite = bool(torch.isfinite(o.arena.data).all())
+    unchanged = bool(torch.equal(o.arena.data, before))
+    parts = [torch.zeros_like(o.arena.data) for _ in range(world)]
+    dist.all_gather(parts, o.arena.data)
+    same = all(torch.equal(parts[0], p) for p in parts)
+    torch.save({"finite": finite, "unchanged": unchanged, "same": same, "flag": int(o.skip_flag.item())},
+               os.path.join(out_dir, f"inf{rank}.pt"))
+    pdist.destroy()
+
+
+def test_zero1_nonfinite_on_one_rank_skips_everywhere(tmp_path):
+    """An Inf in ONE rank's local gradient: every rank skips the update (group-wide flag over the
+    reduced shards), so parameters stay finite, unchanged and identical on all ranks."""
+    world = 2
+    mp.start_processes(_inf_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       start_method="spawn", join=True)
+    for r in range(world):
+        e = torch.load(os.path.join(tmp_path, f"inf{r}.pt"), weights_only=True)
+        assert e == {"finite": True, "unchanged": True, "same": True, "flag": 1}, (r, e)
+
+
 @pytest.mark.gpu
 def test_zero1_gpu_rccl_matches_fused_adam():
     """1-rank RCCL group on the GPU: reduce_scatter_tensor / all_gather_into_tensor + the HIP Adam
