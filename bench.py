@@ -59,7 +59,7 @@ def parse():
                          "measure faster since the conv weight gradients overlap on a second stream)")
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--semantics", default="reference", choices=["reference", "paper"],
-                    help="paper: published attention/LN/softmax (eager blocks + HIP paper-attention core)")
+                    help="paper: published attention/LN/softmax (per-position LayerNorm, softmax over positions)")
     return ap.parse_args()
 
 
@@ -78,7 +78,7 @@ def main():
     model = ProteinBERT(sequences_length=L, num_annotations=mcfg.num_annotations, local_dim=mcfg.local_dim,
                         global_dim=mcfg.global_dim, key_dim=mcfg.key_dim, num_heads=mcfg.num_heads,
                         num_blocks=mcfg.num_blocks, device=dev,
-                        backend=backend if a.semantics == "reference" else "torch", semantics=a.semantics)
+                        backend=backend, semantics=a.semantics)
     if a.mode == "finetune":
         return finetune_bench(a, info, model, L, B, mcfg)
     opt = FusedAdam(model.parameters(), lr=2e-4)
@@ -146,7 +146,7 @@ def main():
                                    f"d_global={mcfg.global_dim}, key_dim={mcfg.key_dim}, heads={mcfg.num_heads}, "
                                    f"annotations={mcfg.num_annotations}, semantics={a.semantics}",
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
-                          "impl": a.impl if a.semantics == "reference" else "torch+hip_paper_attn", "hip_graph": graphed},
+                          "impl": a.impl, "hip_graph": graphed},
                "final_loss": round(final_loss, 5)}
         print(json.dumps(out), flush=True)
     pdist.destroy()

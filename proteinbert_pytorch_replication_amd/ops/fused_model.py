@@ -14,6 +14,7 @@ import torch.nn.functional as F
 
 from .global_track import FusedGlobalBlockFn, GlobalBlockFn, HeadsLossFn, InputLayerFn, glob_fused_ok, pack_batch
 from .local_track import CH, EmbedFn, conv_images, local_block
+from .paper_track import PaperHeadsLossFn, paper_local_block, unit_attention_weight
 
 
 def hip_supported(model) -> Tuple[bool, str]:
@@ -24,8 +25,6 @@ def hip_supported(model) -> Tuple[bool, str]:
         return False, f"conv_kernel_size={cfg['conv_kernel_size']} (HIP kernels are specialised for 9)"
     if cfg["vocab_size"] > 32:
         return False, "vocab_size > 32"
-    if cfg["semantics"] != "reference":
-        return False, "paper semantics run on the eager path"
     if (cfg["global_dim"] % 32) != 0:
         return False, "global_dim must be a multiple of 32"
     return True, ""
@@ -47,6 +46,8 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     # g0 and block 0's global->local vector; every GlobalBlockFn then produces the next block's gb
     g, g_bf, gb = InputLayerFn.apply(annotations, lin.weight, lin.bias, gl0.weight, gl0.bias)
     h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
+    paper = model.semantics == "paper"
+    mask = (tokens != 0).contiguous() if paper else None
     # every weight image the fused kernels read this step, built by one launch
     items, conv_imgs, glob_imgs = [], [], []
     for i, blk in enumerate(blocks):
@@ -70,13 +71,22 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
             glob_imgs.append(None)
     pack_batch(items)
     for i, blk in enumerate(blocks):
-        h, vpart = local_block(h, gb, blk, conv_imgs[i])
         att = blk.global_attention_layer
+        if paper:
+            # per-position LayerNorm local track, then attention over positions (split-L HIP core);
+            # its [B, G] output enters the global track unscaled (W_parameter unused, as in the oracle)
+            h_in = h
+            h = paper_local_block(h_in, gb, blk, conv_imgs[i])
+            vpart = att.forward_paper(h, g, mask).unsqueeze(1)
+            wp = unit_attention_weight(att.key_dim, h.device)
+        else:
+            h, vpart = local_block(h, gb, blk, conv_imgs[i])
+            wp = att.W_parameter
         nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
         l1, l2 = blk.global_linear_layer_1[0], blk.global_linear_layer_2[0]
         n1, n2 = blk.global_norm_1, blk.global_norm_2
         args = (g, g_bf, vpart, l1.weight, l1.bias, n1.weight, n1.bias, l2.weight, l2.bias, n2.weight, n2.bias,
-                att.W_parameter, None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
+                wp, None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
         if glob_imgs[i] is not None:
             g, g_bf, gb = FusedGlobalBlockFn.apply(*args, glob_imgs[i])
         else:
@@ -96,7 +106,8 @@ def fused_pretrain_loss(model, X: Dict[str, torch.Tensor], Y: Dict[str, torch.Te
     """Reference loss (utils.py:293-294) through the fused heads: one HIP pass per head."""
     h, g, g_bf = fused_encode(model, X["local"], X["global"], return_bf16=True)
     lo, go = model.pretraining_local_output[0], model.pretraining_global_output[0]
-    total, parts = HeadsLossFn.apply(h, g, g_bf, lo.weight, lo.bias, go.weight, go.bias, Y["local"], Y["global"],
+    fn = PaperHeadsLossFn if model.semantics == "paper" else HeadsLossFn
+    total, parts = fn.apply(h, g, g_bf, lo.weight, lo.bias, go.weight, go.bias, Y["local"], Y["global"],
                                      W["local"], W["global"])
     if return_parts:
         return total, parts[0], parts[1]

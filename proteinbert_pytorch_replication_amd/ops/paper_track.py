@@ -1,0 +1,192 @@
+"""Paper-semantics block pieces on MI355X: fused local track (``csrc/paper_local.hip`` + the
+semantics-independent conv kernels) and the row-softmax local head loss.
+
+``semantics="paper"`` is the published ProteinBERT (per-position LayerNorm over channels with a
+``[C]`` affine, attention softmax over positions, local softmax over the vocabulary); reference
+``ProteinBERT/modules.py:148-164,212-217`` normalises over ``(L, C)`` instead.
+One :class:`PaperLocalBlockFn` is::
+
+    s1 = x + GELU(conv_d1(x)) + GELU(conv_d5(x)) + gb        (conv_fwd3, shared with reference semantics)
+    h1 = LN_C(s1); s2 = h1 + GELU(h1 Wl^T + bl); h2 = LN_C(s2)  (pbx_pc_ln_linear_fwd: 1 launch)
+
+and its backward is one LayerNorm/MLP launch (recomputing h1 / the MLP pre-activation from s1) plus
+the conv data / weight gradient kernels.  The attention of the block runs on ``h2`` through
+:mod:`.paper_attention` (split-L HIP core), the global track through the fused global-track kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib, streams
+from ..train.arena import notify_grads_ready
+from .global_track import BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, mm32, addmm_into
+from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, pack_conv, _grad_dst, _wgrad
+
+_P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
+_lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+_lib.register("pbx_pc_ln_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
+                                       _I, _I, _P])
+
+LN_EPS = 1e-5
+TR = 32          # positions per work item of the paper LayerNorm kernels
+
+
+class PaperLocalBlockFn(torch.autograd.Function):
+    """Fused local track of one block, paper semantics (per-position LayerNorm(C))."""
+
+    @staticmethod
+    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, dil: int, packed=None):
+        params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
+        B, L, C = x.shape
+        assert C == CH and x.dtype == BF16 and x.is_contiguous()
+        assert g1.shape == (CH,), "paper semantics: LayerNorm affine is [C]"
+        KS = wn.shape[2]
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        BM1 = conv_tile(L)
+        T1 = (L + BM1 - 1) // BM1
+        if packed is not None:
+            wpn, wtn, wpw, wtw = packed
+        else:
+            wpn, wtn = pack_conv(wn)
+            wpw, wtw = pack_conv(ww)
+        wl_b = bf16_of(wl)
+        gb = gb.detach().float().contiguous()
+        pre_n, pre_w, s1 = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+        st1 = torch.empty((B, T1, 2), dtype=F32, device=dev)       # whole-sequence partials (unused here)
+        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
+        h2 = torch.empty_like(x)
+        stats = torch.empty((B * L, 4), dtype=F32, device=dev)
+        _lib.call("pbx_pc_ln_linear_fwd", s1.data_ptr(), g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(),
+                  bl.data_ptr(), g2.data_ptr(), be2.data_ptr(), h2.data_ptr(), stats.data_ptr(), B, L, LN_EPS, stream)
+        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b)
+        ctx.meta = (B, L, KS, dil, BM1)
+        ctx.params = params
+        ctx.set_materialize_grads(False)
+        return h2
+
+    @staticmethod
+    def backward(ctx, dh2):
+        x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b = ctx.saved_tensors
+        B, L, KS, dil, BM1 = ctx.meta
+        dev = x.device
+        stream = _lib.stream_ptr(dev)
+        params = ctx.params
+        wn, bn, ww, bw, g1, be1, wl, bl, g2, be2 = params
+        dsts = [_grad_dst(p, p.shape) for p in params]
+        (dwn, _), (dbn, _), (dww, _), (dbw, _), (dg1, _), (dbe1, _), (dwl, _), (dbl, _), (dg2, _), (dbe2, _) = dsts
+        dh2 = None if dh2 is None else dh2.to(BF16).contiguous()
+        ds1 = torch.empty_like(x)
+        T = (L + TR - 1) // TR
+        dgbp = torch.empty((B, T, CH), dtype=F32, device=dev)
+        _lib.call("pbx_pc_ln_linear_bwd", _lib.ptr(dh2), None, s1.data_ptr(), stats.data_ptr(), g1.data_ptr(),
+                  be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(), dgbp.data_ptr(),
+                  dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
+                  B, L, stream)
+        dgb = dgbp.sum(dim=1)
+        if streams.GLOBAL_ENABLED:
+            streams.fork(dev, "global")
+        dx, dpn, dpw = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
+        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
+        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
+            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
+                           keep=[dpn, dpw, x], name="wgrad")
+        else:
+            _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
+        direct = [p for p, (_, d) in zip(params, dsts) if d]
+        if direct:
+            notify_grads_ready(direct)
+        pgrads = [None if d else g for (g, d) in dsts]
+        return (dx, dgb, *pgrads, None, None)
+
+
+def paper_local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> torch.Tensor:
+    nc = blk.local_narrow_conv_layer[0]
+    wc = blk.local_wide_conv_layer[0]
+    return PaperLocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
+                                   blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
+                                   blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
+                                   blk.wide_conv_dilation, packed)
+
+
+_ONES = {}
+
+
+def unit_attention_weight(K: int, device) -> torch.Tensor:
+    """Constant ``[K]`` ones: the fused global-track kernels scale the attention input by
+    ``sum(W_parameter) / K`` (reference semantics); in paper semantics the attention output enters
+    the global track unscaled and ``W_parameter`` is unused (as in ``GlobalAttention.forward_paper``)."""
+    key = (K, str(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.ones(K, dtype=F32, device=device)
+        _ONES[key] = t
+    return t
+
+
+class PaperHeadsLossFn(torch.autograd.Function):
+    """Both heads + the paper-semantics loss: local head softmax over the vocabulary (NLL of the
+    target residue, weighted, mean over B*L), GO head sigmoid + BCE (the reference's, ``utils.py:294``).
+    Gradients are produced in the forward pass (the loss is terminal)."""
+
+    @staticmethod
+    def forward(ctx, h, g2, g2_bf, wo, bo, wa, ba, y_l, y_g, w_l, w_g):
+        dev = h.device
+        st = _lib.stream_ptr(dev)
+        B, L, C = h.shape
+        V = wo.shape[0]
+        A = wa.shape[0]
+        loss = torch.zeros(2, dtype=F32, device=dev)
+        hb = h.reshape(B * L, C)
+        logits = torch.addmm(bo.float(), hb, bf16_of(wo).t(), out_dtype=F32)       # [R, V] fp32
+        lse = torch.logsumexp(logits, dim=1)
+        y = y_l.reshape(-1)
+        wl = w_l.reshape(-1).float()
+        nll = lse - logits.gather(1, y.unsqueeze(1)).squeeze(1)
+        inv = 1.0 / float(B * L)
+        loss[0] = (nll * wl).sum() * inv
+        dlog = torch.softmax(logits, dim=1)
+        dlog.scatter_add_(1, y.unsqueeze(1), torch.full_like(wl, -1.0).unsqueeze(1))
+        dlog.mul_((wl * inv).unsqueeze(1))
+        dlog_bf = dlog.to(BF16)
+        dh = torch.mm(dlog_bf, bf16_of(wo)).view(B, L, C)                             # bf16
+        dwo = mm32(dlog_bf.t(), hb)
+        dbo = dlog.sum(dim=0)
+        z = mm32(g2_bf, bf16_of(wa).t())
+        dz = torch.empty((B, A), dtype=BF16, device=dev)
+        dba = torch.zeros(A, dtype=F32, device=dev)
+        if w_g.dim() == 2 and w_g.stride(1) == 0:
+            wg, wsr, wsc = w_g[:, 0].float().contiguous(), 1, 0
+        else:
+            wg = w_g.float().expand(B, A).contiguous()
+            wsr, wsc = A, 1
+        _lib.call("pbx_go_head", z.data_ptr(), ba.data_ptr(), y_g.float().contiguous().data_ptr(), wg.data_ptr(),
+                  wsr, wsc, dz.data_ptr(), dba.data_ptr(), loss[1:].data_ptr(), B, A, st)
+        ctx.save_for_backward(dh, dwo, dbo, dz, dba, g2_bf)
+        ctx.params = (wo, bo, wa, ba)
+        ctx.mark_non_differentiable(loss)
+        ctx.set_materialize_grads(False)
+        return loss.sum(), loss
+
+    @staticmethod
+    def backward(ctx, dtotal, _dparts):
+        dh, dwo, dbo, dz, dba, g2_bf = ctx.saved_tensors
+        wo, bo, wa, ba = ctx.params
+        if dtotal is None:
+            return (None,) * 11
+        gr = _Grads([wo, bo, wa, ba])
+        dwo_d, dbo_d, dwa_d, dba_d = gr.dst
+        if _UNIT_LOSS_GRAD[0]:
+            s = None
+            dz_s, dh_s = dz, dh
+        else:
+            s = dtotal.reshape(()).to(F32)
+            dz_s, dh_s = (dz.float() * s).to(dz.dtype), (dh.float() * s).to(dh.dtype)
+        dwo_d.add_(dwo if s is None else dwo * s)
+        dbo_d.add_(dbo if s is None else dbo * s)
+        dba_d.add_(dba if s is None else dba * s)
+        dg2 = mm32(dz_s, bf16_of(wa))
+        addmm_into(dwa_d, dz_s.t(), g2_bf)
+        return (dh_s, dg2, None, *gr.finish(), None, None, None, None)

@@ -1,0 +1,122 @@
+"""GPU numerics: paper-semantics fused local track (csrc/paper_local.hip + the conv kernels) and the
+paper-semantics fused model step vs plain PyTorch fp32 references of the same math.
+
+Paper semantics = the published ProteinBERT: LayerNorm over channels per position ([C] affine),
+attention softmax over positions, local softmax over the vocabulary (reference modules.py:148-164
+uses LayerNorm((L, C)) instead).  Odd lengths exercise the masked last tile.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from proteinbert_pytorch_replication_amd.models import ProteinBERT
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def make_block(L, seed=0):
+    torch.manual_seed(seed)
+    m = ProteinBERT(sequences_length=L, num_annotations=64, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
+                    num_blocks=1, device="cuda", backend="hip", semantics="paper")
+    blk = m.proteinBERT_blocks[0]
+    with torch.no_grad():
+        for ln in (blk.local_norm_1, blk.local_norm_2):
+            ln.weight.normal_(1.0, 0.2)
+            ln.bias.normal_(0.0, 0.2)
+        blk.local_linear_layer[0].bias.normal_(0.0, 0.2)
+    return m, blk
+
+
+def torch_local(x, gb, blk):
+    nc, wc = blk.local_narrow_conv_layer[0], blk.local_wide_conv_layer[0]
+    xt = x.transpose(1, 2)
+    n = F.gelu(F.conv1d(xt, nc.weight, nc.bias, padding="same", dilation=1)).transpose(1, 2)
+    w = F.gelu(F.conv1d(xt, wc.weight, wc.bias, padding="same", dilation=blk.wide_conv_dilation)).transpose(1, 2)
+    s1 = x + n + w + gb.unsqueeze(1)
+    h1 = F.layer_norm(s1, (128,), blk.local_norm_1.weight, blk.local_norm_1.bias)
+    lin = blk.local_linear_layer[0]
+    s2 = h1 + F.gelu(F.linear(h1, lin.weight, lin.bias))
+    return F.layer_norm(s2, (128,), blk.local_norm_2.weight, blk.local_norm_2.bias)
+
+
+def _params(blk):
+    return [blk.local_narrow_conv_layer[0].weight, blk.local_narrow_conv_layer[0].bias,
+            blk.local_wide_conv_layer[0].weight, blk.local_wide_conv_layer[0].bias,
+            blk.local_norm_1.weight, blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
+            blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias]
+
+
+@pytest.mark.parametrize("L,B", [(512, 3), (200, 2), (77, 5), (1024, 2)])
+def test_paper_local_block_forward(L, B):
+    from proteinbert_pytorch_replication_amd.ops.paper_track import paper_local_block
+    m, blk = make_block(L)
+    x = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
+    gb = torch.randn(B, 128, device="cuda") * 0.5
+    with torch.no_grad():
+        h2 = paper_local_block(x, gb, blk)
+        ref = torch_local(x.float(), gb, blk)
+    torch.cuda.synchronize()
+    assert rel(h2, ref) < 1.5e-2
+
+
+@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (77, 4)])
+def test_paper_local_block_backward(L, B):
+    from proteinbert_pytorch_replication_amd.ops.paper_track import paper_local_block
+    m, blk = make_block(L, seed=1)
+    x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
+    gb0 = torch.randn(B, 128, device="cuda") * 0.5
+    dh = torch.randn(B, L, 128, device="cuda")
+    params = _params(blk)
+    x = x0.clone().requires_grad_(True)
+    gb = gb0.clone().requires_grad_(True)
+    h2 = paper_local_block(x, gb, blk)
+    got = torch.autograd.grad((h2.float() * dh).sum(), [x, gb] + params)
+    xr = x0.float().clone().requires_grad_(True)
+    gbr = gb0.clone().requires_grad_(True)
+    ref = torch.autograd.grad((torch_local(xr, gbr, blk) * dh).sum(), [xr, gbr] + params)
+    torch.cuda.synchronize()
+    names = ["x", "gb", "wn", "bn", "ww", "bw", "g1", "be1", "wl", "bl", "g2", "be2"]
+    for n, a, b in zip(names, got, ref):
+        e = rel(a, b)
+        assert e < 3e-2, f"{n}: rel err {e:.3e}"
+
+
+def test_paper_model_fused_loss_and_grads_vs_torch():
+    """Whole paper-semantics model (2 blocks) through the fused HIP path vs the fp32 torch oracle."""
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss, hip_supported
+    from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
+    torch.manual_seed(0)
+    L, A = 256, 1024
+    m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
+                    num_blocks=2, device="cuda", backend="hip", semantics="paper")
+    assert hip_supported(m)[0]
+    with torch.no_grad():   # O(1) attention weights so the softmax over positions is not one-hot
+        for blk in m.proteinBERT_blocks:
+            att = blk.global_attention_layer
+            att.Wq.mul_(0.05)
+            att.Wk.mul_(0.05)
+            att.Wv.mul_(0.1)
+    X, Y, W = SyntheticUniRefGO(L, A, 6, "cuda", seed=3).next_batch()
+    loss = fused_pretrain_loss(m, X, Y, W)
+    loss.backward()
+    got = {n: p.grad.detach().clone() for n, p in m.named_parameters() if p.grad is not None}
+    m.zero_grad(set_to_none=True)
+    h, g = m.encode_torch(X["local"], X["global"], torch.float32)
+    pl, pg = m.heads_torch(h, g)
+    lref = pretrain_loss_torch(pl, pg, Y, {k: v.float() for k, v in W.items()}, semantics="paper")
+    lref.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - lref.item()) < 5e-3 * abs(lref.item()), (loss.item(), lref.item())
+    norms = {n: p.grad.norm().item() for n, p in m.named_parameters() if p.grad is not None}
+    scale = sorted(norms.values())[len(norms) // 2]
+    assert set(got) >= {n for n in norms if norms[n] > 0}
+    for n in norms:
+        err = (got[n].float() - m.get_parameter(n).grad.float()).norm().item()
+        print(f"{n:60s} |g|={norms[n]:.3e} err={err:.3e}")
+        assert err < 6e-2 * norms[n] + 1e-4 * scale, f"{n}: err {err:.3e} vs |g| {norms[n]:.3e}"
