@@ -14,7 +14,7 @@ import torch.nn.functional as F
 
 from .global_track import FusedGlobalBlockFn, GlobalBlockFn, HeadsLossFn, InputLayerFn, glob_fused_ok, pack_batch
 from .local_track import CH, EmbedFn, conv_images, local_block
-from .paper_track import PaperHeadsLossFn, paper_local_block, unit_attention_weight
+from .paper_track import PaperHeadsLossFn, paper_block, unit_attention_weight
 
 
 def hip_supported(model) -> Tuple[bool, str]:
@@ -75,9 +75,8 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         if paper:
             # per-position LayerNorm local track, then attention over positions (split-L HIP core);
             # its [B, G] output enters the global track unscaled (W_parameter unused, as in the oracle)
-            h_in = h
-            h = paper_local_block(h_in, gb, blk, conv_imgs[i])
-            vpart = att.forward_paper(h, g, mask).unsqueeze(1)
+            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i])
+            vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:
             h, vpart = local_block(h, gb, blk, conv_imgs[i])

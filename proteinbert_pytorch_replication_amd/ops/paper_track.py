@@ -4,18 +4,21 @@ semantics-independent conv kernels) and the row-softmax local head loss.
 ``semantics="paper"`` is the published ProteinBERT (per-position LayerNorm over channels with a
 ``[C]`` affine, attention softmax over positions, local softmax over the vocabulary); reference
 ``ProteinBERT/modules.py:148-164,212-217`` normalises over ``(L, C)`` instead.
-One :class:`PaperLocalBlockFn` is::
+One :class:`PaperBlockFn` is::
 
     s1 = x + GELU(conv_d1(x)) + GELU(conv_d5(x)) + gb        (conv_fwd3, shared with reference semantics)
     h1 = LN_C(s1); s2 = h1 + GELU(h1 Wl^T + bl); h2 = LN_C(s2)  (pbx_pc_ln_linear_fwd: 1 launch)
 
-and its backward is one LayerNorm/MLP launch (recomputing h1 / the MLP pre-activation from s1) plus
-the conv data / weight gradient kernels.  The attention of the block runs on ``h2`` through
-:mod:`.paper_attention` (split-L HIP core), the global track through the fused global-track kernels.
+    o  = attention(h2, g) over positions                       (K/V GEMM + split-L HIP core)
+
+and its backward is the attention core + two GEMMs, one LayerNorm/MLP launch (recomputing h1 / the
+MLP pre-activation from s1, both h2 gradients as inputs) and the conv data / weight gradient
+kernels.  The global track runs through the fused global-track kernels.
 """
 from __future__ import annotations
 
 import ctypes
+import math
 
 import torch
 
@@ -33,15 +36,37 @@ LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
 
 
-class PaperLocalBlockFn(torch.autograd.Function):
-    """Fused local track of one block, paper semantics (per-position LayerNorm(C))."""
+def _split_k_chunks(R: int, cap: int = 64) -> int:
+    """Number of row chunks for the split-K weight-gradient GEMMs (K = B*L rows): the library GEMM
+    of a [128, R] x [R, 768] product has 12 output tiles, i.e. 12 busy CUs; chunked bmm gives
+    chunks x 12 tiles and the chunk partials are summed in fp32."""
+    for c in range(cap, 0, -1):
+        if R % c == 0:
+            return c
+    return 1
+
+
+class PaperBlockFn(torch.autograd.Function):
+    """Fused local track + local->global attention of one block, paper semantics.
+
+    Outputs ``h2`` (the block's local output, bf16 ``[B, L, 128]``) and ``o`` (the attention output,
+    fp32 ``[B, H*VD]``, consumed unscaled by the global track).  The attention is the published one:
+    ``q = tanh(g Wq) / sqrt(K)``, ``pre = h2 [Wk | Wv]`` (one library GEMM), then the split-L HIP core
+    (``csrc/paper_attn.hip``: tanh keys, GELU values, pad-masked softmax over positions).  In the
+    backward both gradients of ``h2`` (from the next block and from the attention projection) enter
+    the LayerNorm/MLP kernel as two inputs, so they are never summed in a separate pass.
+    """
 
     @staticmethod
-    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, dil: int, packed=None):
-        params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
+    def forward(ctx, x, gb, g, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv, mask, dil: int, packed=None):
+        from .paper_attention import KEY_DIM, VALUE_DIM, _nsplit
+        params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv)
         B, L, C = x.shape
         assert C == CH and x.dtype == BF16 and x.is_contiguous()
         assert g1.shape == (CH,), "paper semantics: LayerNorm affine is [C]"
+        H, _, K = Wk.shape
+        VD = Wv.shape[2]
+        assert K == KEY_DIM and VD == VALUE_DIM
         KS = wn.shape[2]
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -61,30 +86,64 @@ class PaperLocalBlockFn(torch.autograd.Function):
         stats = torch.empty((B * L, 4), dtype=F32, device=dev)
         _lib.call("pbx_pc_ln_linear_fwd", s1.data_ptr(), g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(),
                   bl.data_ptr(), g2.data_ptr(), be2.data_ptr(), h2.data_ptr(), stats.data_ptr(), B, L, LN_EPS, stream)
-        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b)
-        ctx.meta = (B, L, KS, dil, BM1)
+        # attention: q from the global track, K/V projection as one library GEMM, split-L core
+        gf = g.detach().float()
+        q = torch.tanh(torch.einsum("bg,hgk->bhk", gf, Wq.detach().float()))             # [B, H, K]
+        qs = (q * (1.0 / math.sqrt(K))).contiguous()
+        wcat = torch.cat([Wk.detach().permute(1, 0, 2).reshape(C, H * K),
+                          Wv.detach().permute(1, 0, 2).reshape(C, H * VD)], dim=1).to(BF16)   # [C, H*(K+VD)]
+        pre = torch.mm(h2.view(B * L, C), wcat)                                           # [R, N] bf16
+        ns = _nsplit(B, H, L)
+        part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
+        o = torch.empty(B, H * VD, device=dev, dtype=F32)
+        lse = torch.empty(B * H, device=dev, dtype=F32)
+        mk = None if mask is None else mask.contiguous()
+        _lib.call("pbx_paper_attn_fwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), part.data_ptr(),
+                  o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
+        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wcat, pre, mk, o, lse, h2)
+        ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
         ctx.set_materialize_grads(False)
-        return h2
+        return h2, o
 
     @staticmethod
-    def backward(ctx, dh2):
-        x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b = ctx.saved_tensors
-        B, L, KS, dil, BM1 = ctx.meta
+    def backward(ctx, dh2, do):
+        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wcat, pre, mk, o, lse, h2) = ctx.saved_tensors
+        B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
         params = ctx.params
-        wn, bn, ww, bw, g1, be1, wl, bl, g2, be2 = params
+        wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv = params
         dsts = [_grad_dst(p, p.shape) for p in params]
-        (dwn, _), (dbn, _), (dww, _), (dbw, _), (dg1, _), (dbe1, _), (dwl, _), (dbl, _), (dg2, _), (dbe2, _) = dsts
+        (dwn, _), (dbn, _), (dww, _), (dbw, _), (dg1, _), (dbe1, _), (dwl, _), (dbl, _), (dg2, _), (dbe2, _) = dsts[:10]
+        (dWq, _), (dWk, _), (dWv, _) = dsts[10:]
+        R, C = B * L, CH
         dh2 = None if dh2 is None else dh2.to(BF16).contiguous()
+        dg = None
+        dh2_att = None
+        if do is not None:
+            dO = do.float().contiguous()
+            dpre = torch.empty_like(pre)
+            dq_part = torch.empty(B * H, ns, K, device=dev, dtype=F32)
+            _lib.call("pbx_paper_attn_bwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), lse.data_ptr(),
+                      o.data_ptr(), dO.data_ptr(), dpre.data_ptr(), dq_part.data_ptr(), B, L, H, K, VD, ns, stream)
+            dqs = dq_part.sum(dim=1).view(B, H, K)
+            dh2_att = torch.mm(dpre, wcat.t())                                             # [R, C] bf16
+            nc = _split_k_chunks(R)
+            dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
+                              out_dtype=F32).sum(dim=0)                                   # [C, N] fp32
+            dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
+            dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
+            dqpre = dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)                              # [B, H, K]
+            dWq.add_(torch.einsum("bg,bhk->hgk", gf, dqpre))
+            dg = torch.einsum("bhk,hgk->bg", dqpre, Wq.detach().float())
         ds1 = torch.empty_like(x)
         T = (L + TR - 1) // TR
         dgbp = torch.empty((B, T, CH), dtype=F32, device=dev)
-        _lib.call("pbx_pc_ln_linear_bwd", _lib.ptr(dh2), None, s1.data_ptr(), stats.data_ptr(), g1.data_ptr(),
-                  be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(), dgbp.data_ptr(),
-                  dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  B, L, stream)
+        _lib.call("pbx_pc_ln_linear_bwd", _lib.ptr(dh2), _lib.ptr(dh2_att), s1.data_ptr(), stats.data_ptr(),
+                  g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(),
+                  dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
+                  dbl.data_ptr(), B, L, stream)
         dgb = dgbp.sum(dim=1)
         if streams.GLOBAL_ENABLED:
             streams.fork(dev, "global")
@@ -98,17 +157,27 @@ class PaperLocalBlockFn(torch.autograd.Function):
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)
-        pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None)
+        pgrads = [None if d else gr for (gr, d) in dsts]
+        return (dx, dgb, dg, *pgrads, None, None, None)
+
+
+def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None):
+    """``(h2, o)`` of one paper-semantics block's local track + attention (fused HIP path)."""
+    nc = blk.local_narrow_conv_layer[0]
+    wc = blk.local_wide_conv_layer[0]
+    att = blk.global_attention_layer
+    return PaperBlockFn.apply(x, gb, g, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
+                              blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
+                              blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
+                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed)
 
 
 def paper_local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> torch.Tensor:
-    nc = blk.local_narrow_conv_layer[0]
-    wc = blk.local_wide_conv_layer[0]
-    return PaperLocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
-                                   blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
-                                   blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
-                                   blk.wide_conv_dilation, packed)
+    """Local track only (``h2``); the attention output is dropped (tests / encoders without the
+    global track's consumer)."""
+    g = torch.zeros((x.shape[0], blk.global_dim), dtype=F32, device=x.device)
+    h2, _ = paper_block(x, gb, g, blk, None, packed)
+    return h2
 
 
 _ONES = {}
