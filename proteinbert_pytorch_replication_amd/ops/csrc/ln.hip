@@ -31,6 +31,19 @@ __device__ __forceinline__ void load_f4(const float* p, float* v) {
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
 }
 
+// One 1-KiB global->LDS DMA wave instruction (lane i's 16 source bytes land at lds_base + 16 i), as
+// inline asm so hipcc does not make later ds_reads wait for it (see wgrad.hip); it retires in vmcnt
+// order with the wave's other vector-memory operations.
+__device__ __forceinline__ void glds16_ln(const void* src, unsigned char* lds_base) {
+  const unsigned dst = __builtin_amdgcn_readfirstlane(
+      (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_base);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(dst)
+               : "memory");
+}
+
 // stage a [rows x 128] bf16 weight matrix into a swz256 LDS image (whole workgroup)
 __device__ __forceinline__ void stage_weight(unsigned char* dst, const bf16_t* __restrict__ w, int rows) {
   stage_chunks(
@@ -441,6 +454,283 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Attention pool with the GELU derivative stored by the forward (v2).
+//
+// The backward of the pool needs GELU'(h2 Wv) at every (position, value column): the v1 backward
+// recomputes the [32 x 512] projection per tile (128 MFMAs) and evaluates GELU' (2 transcendentals
+// per element) just to multiply it by dv.  Here the forward evaluates GELU and GELU' from ONE shared
+// erf/exp core, column-sums GELU as before and writes GELU' as bf16 in the exact per-lane order of
+// the backward's MFMA B operand (`gfrag`: [B][2 ceil(L/64)][NJ/32][2][64 lanes][8], one coalesced
+// 1-KB store / load per wave-instruction); the backward is then 128 MFMAs per 32-position tile fed
+// by a streamed, prefetched load, with no recompute and no transcendental.
+//
+// Fragment order (backward MFMA k-step (jt, s), lane (r = position, h), element jj):
+//   j = jt*32 + 16 s + 8 (jj >> 2) + 4 h + (jj & 3)        (= the A-operand rows of the Wv^T reads)
+// The forward holds D[pos][j] (lane = column j, 16 positions in registers, so the column sums stay
+// in-lane); each 32x32 block of GELU' goes through a per-wave LDS tile Gt[j][pos] (ds_write_b64 of
+// 4 contiguous positions) and comes back transposed (ds_read_b64_tr_b16) as two fragments.
+constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
+constexpr int GT_BYTES = 32 * GT_STRIDE;
+
+__global__ void __launch_bounds__(512) ln_attn_fwd2_kernel(
+    const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
+    const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
+    float* __restrict__ vpart, bf16x8* __restrict__ gfrag, int B, int L, int NJ, float eps) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ws = smem;                                          // NJ rows x 256 B
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  unsigned char* gt = smem + NJ * 256 + w * GT_BYTES;               // this wave's transpose tile
+  const int NW = blockDim.x >> 6;
+  const int T2 = (L + BML - 1) / BML;
+  const int TW = (L + 63) / 64;
+  const int NJT = NJ / 32;
+  const long items = (long)B * TW;
+  stage_weight(ws, wv, NJ);
+  __syncthreads();
+  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos0 = tw * 64;
+    float mean, rstd;
+    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+    bf16x8 hf0[8], hf1[8];
+    {
+      const int pa = pos0 + r, pb = pos0 + 32 + r;
+      const int ca = min(pa, L - 1), cb = min(pb, L - 1);
+      const size_t ra = ((size_t)b * L + ca) * CH, rb = ((size_t)b * L + cb) * CH;
+      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
+      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
+    }
+    float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
+    // fragment base of this item's two 32-position tiles: [b][2 tw + pt][jt][s][lane]
+    bf16x8* gdst = gfrag + ((size_t)b * 2 * TW + 2 * tw) * NJT * 2 * 64 + lane;
+    auto epi = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
+      f32x2 sv = {0.f, 0.f};
+#pragma unroll
+      for (int pt = 0; pt < 2; ++pt) {
+        const f32x16_t& c = pt ? c1 : c0;
+#pragma unroll
+        for (int hf = 0; hf < 2; ++hf) {
+          const f32x2 xv[4] = {(f32x2){c[8 * hf], c[8 * hf + 1]}, (f32x2){c[8 * hf + 2], c[8 * hf + 3]},
+                               (f32x2){c[8 * hf + 4], c[8 * hf + 5]}, (f32x2){c[8 * hf + 6], c[8 * hf + 7]}};
+          f32x2 gv[4], gd[4];
+          gelu2_both_n<4>(xv, gv, gd);
+#pragma unroll
+          for (int gg = 0; gg < 2; ++gg) {
+            const int g = 2 * hf + gg;
+            sv += gv[2 * gg] + gv[2 * gg + 1];
+            // positions 8g + 4h .. +3 of column j = r -> Gt[r][8g + 4h]
+            uint2 pk;
+            pk.x = (unsigned)f2bf(gd[2 * gg].x) | ((unsigned)f2bf(gd[2 * gg].y) << 16);
+            pk.y = (unsigned)f2bf(gd[2 * gg + 1].x) | ((unsigned)f2bf(gd[2 * gg + 1].y) << 16);
+            *reinterpret_cast<uint2*>(gt + r * GT_STRIDE + (8 * g + 4 * h) * 2) = pk;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          const int rlo = 16 * s + 4 * h + q;
+          const bf16x8 f = cat_tr(lds_tr(gt, rlo * GT_STRIDE + tc * 2), lds_tr(gt, (rlo + 8) * GT_STRIDE + tc * 2));
+          gdst[((size_t)pt * NJT * 2 + jt * 2 + s) * 64] = f;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+      float sacc = sv.x + sv.y;
+      sacc += __shfl_xor(sacc, 32, 64);
+      if (h == 0) vrow[jt * 32 + r] = sacc;
+    };
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256(r, kk * 2 + h));
+    f32x16_t p0 = zero16(), p1 = zero16();
+    for (int jt = 0; jt < NJT; ++jt) {
+      f32x16_t c0 = zero16(), c1 = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        c0 = mfma32(hf0[kk], wf[kk], c0);
+        c1 = mfma32(hf1[kk], wf[kk], c1);
+      }
+      if (jt + 1 < NJT) {
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256((jt + 1) * 32 + r, kk * 2 + h));
+      }
+      if (jt > 0) epi(p0, p1, jt - 1);
+      p0 = c0;
+      p1 = c1;
+    }
+    epi(p0, p1, NJT - 1);
+  }
+}
+
+// attention pool backward from the stored GELU' fragments + LayerNorm-2 backward partials:
+//   dh2[pos][ci] = dh2_in + sum_j Wv[j][ci] dv[b][j] GELU'[pos][j]
+// Work item = one 32-position tile, one wave per SIMD (4 waves, <= 512 registers).  Every load of an
+// item is issued at its start, in the order the wave consumes them (vmcnt retires in issue order):
+// the dv row, all 2 NJT GELU' fragments of the tile (one coalesced 1-KiB load each, ~32 KiB in
+// flight per wave), then the epilogue operands; no load is outstanding across the item loop's back
+// edge, so the compiler's waits stay exact.
+template <int NJT>
+__global__ void __launch_bounds__(256) attn_bwd2_kernel(
+    const bf16x8* __restrict__ gfrag, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
+    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
+    const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, float eps) {
+  constexpr int NJ = NJT * 32;
+  constexpr int NF = 2 * NJT;                       // fragments (k-steps) per 32-position tile
+  constexpr int NDV = NJ / 256;                     // 1-KiB DMA instructions per dv row
+  constexpr int NW = 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ws = smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int T2 = (L + BML - 1) / BML;
+  const int TW = (L + 31) / 32;
+  const int TWG = 2 * ((L + 63) / 64);              // 32-position tiles per sample in gfrag
+  const int TV = (L + BMV - 1) / BMV;
+  const long items = (long)B * TW;
+  const long stride = (long)gridDim.x * NW;
+  stage_weight(ws, wv, NJ);
+  // per-wave dv rows, double-buffered: item k reads slot k & 1; the DMA of item k+1's row into the
+  // other slot is issued with item k's epilogue operands (whose waits retire it)
+  unsigned char* dvslot = ws + NJ * 256 + w * 2 * NJ * 4;
+  int woff[4], woff8[4];   // Wv^T fragment offsets at step 0; step i adds 16 i rows = 4096 i bytes
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    woff[ct] = swz256e(4 * h + q, ct * 32 + tc);
+    woff8[ct] = swz256e(4 * h + q + 8, ct * 32 + tc);
+  }
+  auto dv_src = [&](long it) {
+    const int b = (int)(it / TW), tw = (int)(it - (it / TW) * TW);
+    return dvpart + ((size_t)b * TV + (tw * 32) / BMV) * NJ;
+  };
+  long item = (long)blockIdx.x * NW + w;
+  if (item < items) {
+    const float* dvg = dv_src(item);
+#pragma unroll
+    for (int k = 0; k < NDV; ++k) glds16_ln(dvg + lane * 4 + 256 * k, dvslot + 1024 * k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  int slot = 0;
+  for (; item < items; item += stride, slot ^= 1) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos = tw * 32 + r;
+    const bool okb = pos < L;
+    const bf16x8* gsrc = gfrag + ((size_t)b * TWG + tw) * NF * 64 + lane;
+    const float* dv = reinterpret_cast<const float*>(dvslot + slot * NJ * 4);
+    const bool has_next = item + stride < items;
+    const float* dvn = dv_src(has_next ? item + stride : item);
+    bf16x8 ring[NF];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      ring[i] = gsrc[i * 64];
+      __builtin_amdgcn_sched_barrier(0);      // keep the issue order = the consumption order
+    }
+    const int pc = min(pos, L - 1);
+    const size_t roff = ((size_t)b * L + pc) * CH;
+    // branch-free loads (a load under a branch makes the compiler's vmcnt tracking fall back to
+    // vmcnt(0) at the merge): a missing dh2_in reads s2 and is masked
+    const bf16_t* dsrc = dh2_in != nullptr ? dh2_in : s2;
+    const float dmask = dh2_in != nullptr ? 1.f : 0.f;
+    const float* stb = st2 + (size_t)b * T2 * 2;
+    uint2 dq[4][4], sq[4][4];
+    float4 gq4[4][4];
+    float2 pm0, pm1;
+    // the epilogue operands are issued EPI steps before the end of the tile: vmcnt counts at most 63
+    // outstanding operations per wave (2 + 2 NJT ring + 50 would overflow it if issued up front)
+    auto epi_loads = [&]() {
+      if (has_next) {
+#pragma unroll
+        for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ci0 = ct * 32 + 8 * i + 4 * h;
+          dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
+          sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
+          gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+        }
+      pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
+      pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
+    };
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    f32x16_t y[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
+    constexpr int EPI = NF < 8 ? NF : 8;
+#pragma unroll
+    for (int i = 0; i < NF; ++i) {
+      if (i == NF - EPI) {
+        __builtin_amdgcn_sched_barrier(0);
+        epi_loads();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      float dvv[8], gv[8];
+      load_f4(dv + 16 * i + 4 * h, dvv);            // j = jt*32 + 16 s (= 16 i) + 4 h + ...
+      load_f4(dv + 16 * i + 8 + 4 * h, dvv + 4);
+      unpack8(__builtin_bit_cast(uint4, ring[i]), gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gv[e] *= dvv[e];
+      const bf16x8 fb = pack8(gv);
+      const unsigned char* wsi = ws + 4096 * i;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const bf16x8 fw = cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct]));
+        y[ct] = mfma32(fw, fb, y[ct]);
+      }
+    }
+    // LN2 statistics of sample b (Chan merge of the tile partials; T2 <= 128 from the early loads)
+    float mean, rstd;
+    if (T2 <= 128) {
+      float n = 0.f, m = 0.f, M2 = 0.f;
+      if (lane < T2) chan_merge(n, m, M2, (float)(min(BML, L - lane * BML) * CH), pm0.x, pm0.y);
+      if (lane + 64 < T2) chan_merge(n, m, M2, (float)(min(BML, L - (lane + 64) * BML) * CH), pm1.x, pm1.y);
+      wave_chan(n, m, M2);
+      mean = m;
+      rstd = rsqrtf(M2 / n + eps);
+    } else {
+      wave_ln_stats(stb, T2, BML, L, CH, eps, mean, rstd);
+    }
+    float sa = 0.f, sc = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ci0 = ct * 32 + 8 * g + 4 * h;
+        float din[4], sv[4], o[4];
+        unpack4(dq[ct][g], din);
+        unpack4(sq[ct][g], sv);
+        const float gg[4] = {gq4[ct][g].x, gq4[ct][g].y, gq4[ct][g].z, gq4[ct][g].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = bfround(fmaf(din[e], dmask, y[ct][4 * g + e]));
+          const float xh = (sv[e] - mean) * rstd;
+          const float dxh = o[e] * gg[e];
+          sa += okb ? dxh : 0.f;
+          sc += okb ? dxh * xh : 0.f;
+        }
+        if (okb) *reinterpret_cast<uint2*>(dh2 + roff + ci0) = packq4(o);
+      }
+    }
+    sa = wave_reduce_sum(sa);
+    sc = wave_reduce_sum(sc);
+    if (lane == 0) {
+      sums2[((size_t)b * TW + tw) * 2] = sa;
+      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Per-sample constants for the LayerNorm-2 / local-MLP backward: one wave per sample combines the
 // tile partials once (instead of every consumer workgroup doing it):
 //   c[b] = (mean2, rstd2, m1_2, m2_2, mean1, rstd1, 0, 0)
@@ -806,6 +1096,9 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
@@ -859,6 +1152,38 @@ PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, co
                      (const bf16_t*)s2,
                      st2, g2, (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ,
                      eps);
+  return pbx_launch_status();
+}
+
+// v2 pool: also writes gfrag (bf16 GELU' fragments, B * 2 ceil(L/64) * NJ * 32 elements)
+PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
+                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, int nw, float eps,
+                                hipStream_t st) {
+  set_ln_attrs();
+  if (NJ % 64 != 0 || NJ * 256 + nw * GT_BYTES > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
+  const long items = (long)B * ((L + 63) / 64);
+  long wgl = (items + nw - 1) / nw;
+  if (wgl > num_cus()) wgl = num_cus();
+  hipLaunchKernelGGL(ln_attn_fwd2_kernel, dim3((int)wgl), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
+                     (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag, B, L,
+                     NJ, eps);
+  return pbx_launch_status();
+}
+
+// v2 pool backward (NJ = 256 or 512): reads gfrag instead of recomputing h2 Wv
+PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2, const float* g2,
+                             const void* dh2_in, const float* dvpart, int bmv, const void* wv, void* dh2,
+                             float* sums2, int B, int L, int NJ, float eps, hipStream_t st) {
+  set_ln_attrs();
+  const int nw = 4;
+  if ((NJ != 256 && NJ != 512) || bmv % 32 != 0) return (int)hipErrorInvalidValue;
+  const long items = (long)B * ((L + 31) / 32);
+  long wgl = (items + nw - 1) / nw;
+  if (wgl > num_cus()) wgl = num_cus();
+  const int lds = NJ * 256 + nw * 2 * NJ * 4;
+  hipLaunchKernelGGL(NJ == 512 ? attn_bwd2_kernel<16> : attn_bwd2_kernel<8>, dim3((int)wgl), dim3(64 * nw), lds, st,
+                     (const bf16x8*)gfrag, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
+                     (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
   return pbx_launch_status();
 }
 

@@ -39,6 +39,8 @@ _lib.register("pbx_pack_conv", [_P, _P, _P, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_attn_bwd", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
@@ -57,6 +59,16 @@ CONV_IMPL = os.environ.get("PBX_CONV", "v3")
 # conv weight-gradient form (k = 9): "v2" (csrc/wgrad.hip: LDS-DMA double buffer, 64 output channels
 # per workgroup, one workgroup per CU) or "v1" (csrc/conv.hip wgrad_kernel); PBX_WGRAD=v1 selects v1.
 WGRAD_IMPL = os.environ.get("PBX_WGRAD", "v2")
+
+
+# attention-pool form: "v2" (the forward stores GELU' as bf16 MFMA fragments, the backward streams
+# them: no recompute GEMM, no transcendental in the backward) or "v1" (backward recomputes h2 Wv and
+# GELU'); PBX_ATTN_POOL=v1 selects the latter.  v2 needs NJ = H*VD in (256, 512).
+ATTN_POOL = os.environ.get("PBX_ATTN_POOL", "v2")
+
+
+def attn_pool_v2(NJ: int) -> bool:
+    return ATTN_POOL == "v2" and NJ in (256, 512)
 
 
 # v3 forward tile: 128 positions (two workgroups per CU; measured faster in the full step than 256,
@@ -199,9 +211,18 @@ class LocalBlockFn(torch.autograd.Function):
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
-        _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                  wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
-        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
+        if attn_pool_v2(NJ):
+            # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
+            gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
+            _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
+                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), gfrag.data_ptr(), B, L, NJ, nwf, LN_EPS,
+                      stream)
+            hsave = gfrag
+        else:
+            _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
+                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
+            hsave = h2
+        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, hsave, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
         ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
         ctx.set_materialize_grads(False)
         ctx.params = params
@@ -210,7 +231,8 @@ class LocalBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh2, dvpart):
         streams.wait_ready(dvpart)           # produced by the global-track backward on its aux stream
-        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        # hs: the GELU' fragments (v2 pool) or h2 (v1 pool, recomputed projection)
+        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, hs, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
         B, L, KS, dil, BM1, T1, T2, NJ, BMV = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -231,9 +253,14 @@ class LocalBlockFn(torch.autograd.Function):
         TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_attn_bwd", h2.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                  dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, nwb,
-                  LN_EPS, stream)
+        if attn_pool_v2(NJ):
+            _lib.call("pbx_attn_bwd2", hs.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
+                      LN_EPS, stream)
+        else:
+            _lib.call("pbx_attn_bwd", hs.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, nwb,
+                      LN_EPS, stream)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
         dh1 = torch.empty_like(x)
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)
