@@ -472,7 +472,8 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
 constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
 constexpr int GT_BYTES = 32 * GT_STRIDE;
 
-__global__ void __launch_bounds__(512) ln_attn_fwd2_kernel(
+template <int NWAVE, int NI>   // NI: GELU pairs interleaved per core call (4: one half-tile, 8: a tile, 16: both)
+__global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
     float* __restrict__ vpart, bf16x8* __restrict__ gfrag, int B, int L, int NJ, float eps) {
@@ -507,25 +508,34 @@ __global__ void __launch_bounds__(512) ln_attn_fwd2_kernel(
     bf16x8* gdst = gfrag + ((size_t)b * 2 * TW + 2 * tw) * NJT * 2 * 64 + lane;
     auto epi = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
       f32x2 sv = {0.f, 0.f};
+      // GELU / GELU' of both 32x32 tiles: NI pairs per interleaved core call
+      f32x2 gdall[16];
+#pragma unroll
+      for (int c8 = 0; c8 < 16; c8 += NI) {
+        f32x2 xv[NI], gv[NI], gd[NI];
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+          const int pi = c8 + k;                  // pair index 0..15: tile pi >> 3, values 2 (pi & 7) ..
+          const f32x16_t& c = (pi >> 3) ? c1 : c0;
+          xv[k] = (f32x2){c[2 * (pi & 7)], c[2 * (pi & 7) + 1]};
+        }
+        gelu2_both_n<NI>(xv, gv, gd);
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+          sv += gv[k];
+          gdall[c8 + k] = gd[k];
+        }
+      }
 #pragma unroll
       for (int pt = 0; pt < 2; ++pt) {
-        const f32x16_t& c = pt ? c1 : c0;
 #pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const f32x2 xv[4] = {(f32x2){c[8 * hf], c[8 * hf + 1]}, (f32x2){c[8 * hf + 2], c[8 * hf + 3]},
-                               (f32x2){c[8 * hf + 4], c[8 * hf + 5]}, (f32x2){c[8 * hf + 6], c[8 * hf + 7]}};
-          f32x2 gv[4], gd[4];
-          gelu2_both_n<4>(xv, gv, gd);
-#pragma unroll
-          for (int gg = 0; gg < 2; ++gg) {
-            const int g = 2 * hf + gg;
-            sv += gv[2 * gg] + gv[2 * gg + 1];
-            // positions 8g + 4h .. +3 of column j = r -> Gt[r][8g + 4h]
-            uint2 pk;
-            pk.x = (unsigned)f2bf(gd[2 * gg].x) | ((unsigned)f2bf(gd[2 * gg].y) << 16);
-            pk.y = (unsigned)f2bf(gd[2 * gg + 1].x) | ((unsigned)f2bf(gd[2 * gg + 1].y) << 16);
-            *reinterpret_cast<uint2*>(gt + r * GT_STRIDE + (8 * g + 4 * h) * 2) = pk;
-          }
+        for (int g = 0; g < 4; ++g) {
+          // positions 8g + 4h .. +3 of column j = r -> Gt[r][8g + 4h]
+          const f32x2 a = gdall[pt * 8 + 2 * g], bq = gdall[pt * 8 + 2 * g + 1];
+          uint2 pk;
+          pk.x = (unsigned)f2bf(a.x) | ((unsigned)f2bf(a.y) << 16);
+          pk.y = (unsigned)f2bf(bq.x) | ((unsigned)f2bf(bq.y) << 16);
+          *reinterpret_cast<uint2*>(gt + r * GT_STRIDE + (8 * g + 4 * h) * 2) = pk;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1096,7 +1106,9 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -1160,11 +1172,17 @@ PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g
                                 void* h2, float* vpart, void* gfrag, int B, int L, int NJ, int nw, float eps,
                                 hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + nw * GT_BYTES > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
-  const long items = (long)B * ((L + 63) / 64);
-  long wgl = (items + nw - 1) / nw;
-  if (wgl > num_cus()) wgl = num_cus();
-  hipLaunchKernelGGL(ln_attn_fwd2_kernel, dim3((int)wgl), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
+  if (NJ % 64 != 0 || NJ * 256 + (nw & 15) * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
+  // nw (low 4 bits) = 8: two waves per SIMD, 4 GELU pairs per core call; 4: one wave per SIMD with
+  // 8 independent pairs per core call (or 16 when nw = 4 | 16 << 4) for ILP
+  const int ni = nw >> 4 ? nw >> 4 : ((nw & 15) == 8 ? 4 : 8);
+  nw &= 15;
+  if (nw != 4 && nw != 8) return (int)hipErrorInvalidValue;
+  auto* k = nw == 8 ? ln_attn_fwd2_kernel<8, 4> : (ni == 16 ? ln_attn_fwd2_kernel<4, 16> : ln_attn_fwd2_kernel<4, 8>);
+  const long items2 = (long)B * ((L + 63) / 64);
+  long wg2 = (items2 + nw - 1) / nw;
+  if (wg2 > num_cus()) wg2 = num_cus();
+  hipLaunchKernelGGL(k, dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
                      (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag, B, L,
                      NJ, eps);
   return pbx_launch_status();

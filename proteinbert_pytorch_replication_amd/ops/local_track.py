@@ -67,6 +67,10 @@ WGRAD_IMPL = os.environ.get("PBX_WGRAD", "v2")
 ATTN_POOL = os.environ.get("PBX_ATTN_POOL", "v2")
 
 
+# pool-v2 forward launch: waves per workgroup | GELU pairs per interleaved core call << 4
+ATTN_FWD2_CFG = int(os.environ.get("PBX_ATTN_FWD2", "8"), 0)
+
+
 def attn_pool_v2(NJ: int) -> bool:
     return ATTN_POOL == "v2" and NJ in (256, 512)
 
@@ -215,8 +219,8 @@ class LocalBlockFn(torch.autograd.Function):
             # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
             gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
             _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), gfrag.data_ptr(), B, L, NJ, nwf, LN_EPS,
-                      stream)
+                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), gfrag.data_ptr(), B, L, NJ,
+                      ATTN_FWD2_CFG, LN_EPS, stream)
             hsave = gfrag
         else:
             _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
