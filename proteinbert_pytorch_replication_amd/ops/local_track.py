@@ -215,7 +215,10 @@ class LocalBlockFn(torch.autograd.Function):
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
-        if attn_pool_v2(NJ):
+        # the GELU' fragments only serve a backward pass: inference / frozen-encoder forwards skip them
+        need_bwd = any(ctx.needs_input_grad)
+        ctx.pool_v2 = attn_pool_v2(NJ) and need_bwd
+        if ctx.pool_v2:
             # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
             gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
             _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
@@ -257,7 +260,7 @@ class LocalBlockFn(torch.autograd.Function):
         TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        if attn_pool_v2(NJ):
+        if ctx.pool_v2:
             _lib.call("pbx_attn_bwd2", hs.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
                       LN_EPS, stream)
