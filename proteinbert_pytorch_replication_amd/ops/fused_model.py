@@ -25,6 +25,11 @@ def hip_supported(model) -> Tuple[bool, str]:
         return False, f"conv_kernel_size={cfg['conv_kernel_size']} (HIP kernels are specialised for 9)"
     if cfg["vocab_size"] > 32:
         return False, "vocab_size > 32"
+    if cfg["semantics"] == "paper":
+        from .paper_attention import KEY_DIM, VALUE_DIM
+        if cfg["key_dim"] != KEY_DIM or cfg["global_dim"] // cfg["num_heads"] != VALUE_DIM:
+            return False, (f"paper semantics: the HIP attention core is built for key_dim={KEY_DIM}, "
+                           f"value_dim={VALUE_DIM}")
     if (cfg["global_dim"] % 32) != 0:
         return False, "global_dim must be a multiple of 32"
     return True, ""

@@ -52,8 +52,11 @@ def bf16_of(p: torch.Tensor) -> torch.Tensor:
     v = getattr(p, "_pbx_bf16", None)
     if v is not None:
         if p._version != p._pbx_bf16_ver:      # written outside the optimizer: refresh the mirror
+            # through .data: every mirror is a view of ONE shadow buffer and shares its autograd
+            # version counter, so a tracked copy here would invalidate the mirrors of OTHER
+            # parameters already saved for backward in this forward pass (their bytes are untouched)
             with torch.no_grad():
-                v.copy_(p.detach())
+                v.data.copy_(p.detach())
             p._pbx_bf16_ver = p._version
         return v
     return p.detach().to(BF16)

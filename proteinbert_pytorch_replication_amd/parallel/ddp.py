@@ -63,6 +63,11 @@ class BucketedAllReduce:
         for b in self.param_bucket:
             self.bucket_nparams[b] += 1
         self._pending = list(self.bucket_nparams)
+        # a parameter is counted ONCE per step: fused backward kernels write some gradients in place
+        # and announce them (_on_direct_grads), and autograd still runs those parameters'
+        # AccumulateGrad node (with no gradient) and its post-accumulate hook afterwards -- counting
+        # both launched buckets before their last gradient was written
+        self._ready = [False] * len(arena.params)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
         self._tmp: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._next = 0
@@ -75,23 +80,24 @@ class BucketedAllReduce:
             add_grad_ready_listener(self._on_direct_grads)
 
     # --------------------------------------------------------------------------------
-    def _make_hook(self, idx: int):
-        b = self.param_bucket[idx]
+    def _mark(self, i: int) -> None:
+        if not self._ready[i]:
+            self._ready[i] = True
+            self._pending[self.param_bucket[i]] -= 1
 
+    def _make_hook(self, idx: int):
         def hook(_p):
-            self._pending[b] -= 1
-            if self._pending[b] == 0:
-                self._launch_ready()
+            self._mark(idx)
+            self._launch_ready()
         return hook
 
     def _on_direct_grads(self, params) -> None:
-        """Gradients written in place by a fused backward kernel (no AccumulateGrad hook)."""
+        """Gradients written in place by a fused backward kernel (enqueued on the current or an aux
+        stream; the collective is ordered behind both)."""
         for p in params:
             i = self._index.get(id(p))
-            if i is None:
-                continue
-            b = self.param_bucket[i]
-            self._pending[b] -= 1
+            if i is not None:
+                self._mark(i)
         self._launch_ready()
 
     def _dtype_for(self, b: int) -> torch.dtype:
@@ -121,6 +127,7 @@ class BucketedAllReduce:
 
     def start_step(self) -> None:
         self._pending = list(self.bucket_nparams)
+        self._ready = [False] * len(self._ready)
         self._next = 0
         self._works = [None] * len(self.buckets)
 

@@ -137,3 +137,39 @@ def test_fault_injection_then_resume_from_latest(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "STEPS 2" in r.stdout          # resumed at iteration 4, ran 5 and 6
+
+
+def test_bucketer_counts_each_parameter_once():
+    """A fused backward announces the gradients it wrote in place (notify_grads_ready) and autograd
+    then still runs those parameters' post-accumulate hooks: each parameter must count once toward
+    its bucket, else buckets are reduced before their last gradient is written (found on 2 GPU
+    ranks: the global->local weights were reduced before their in-place write)."""
+    import datetime
+    import torch.distributed as dist
+    from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce
+    from proteinbert_pytorch_replication_amd.train.arena import FlatArena
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            timeout=datetime.timedelta(seconds=30))
+    try:
+        params = [torch.nn.Parameter(torch.randn(300)) for _ in range(6)]
+        arena = FlatArena(params)
+        ddp = BucketedAllReduce(arena, bucket_mb=600 * 4 / 2 ** 20, force=True)
+        assert len(ddp.buckets) >= 2
+        launched = []
+        ddp._launch = lambda b: launched.append(b)
+        first = [p for p in arena.params if ddp.param_bucket[arena.param_index()[id(p)]] == 0]
+        # direct announcement of ONE parameter of bucket 0, then its autograd hook as well
+        ddp._on_direct_grads(first[:1])
+        ddp._make_hook(arena.param_index()[id(first[0])])(first[0])
+        assert launched == [] and min(ddp._pending) >= 0
+        for p in first[1:]:
+            ddp._make_hook(arena.param_index()[id(p)])(p)
+        assert launched == [0]
+        ddp.start_step()
+        assert ddp._pending == ddp.bucket_nparams and not any(ddp._ready)
+    finally:
+        dist.destroy_process_group()
