@@ -189,14 +189,16 @@ __global__ void __launch_bounds__(512) pc_ln_linear_fwd_kernel(
   }
 }
 
-// Backward of the above.  dh2 = dh2a + dh2b (either may be null):
+// Backward of the above.  dh2 = dh2a + dh2b + dh2c (any may be null: the next block's gradient and
+// the attention's, one buffer per head pair):
 //   xh2 = (s2 - mean2) rstd2 ; ds2 = rstd2 (dh2 g2 - <dh2 g2> - xh2 <dh2 g2 xh2>)    (<.> = mean over C)
 //   dpre = ds2 GELU'(pre) ; dh1 = ds2 + dpre Wl ; ds1 = rstd1 (dh1 g1 - <dh1 g1> - xh1 <dh1 g1 xh1>)
 //   dWl += dpre^T h1 ; dbl += sum dpre ; dg2 += sum dh2 xh2 ; db2 += sum dh2 ; dg1 += sum dh1 xh1 ;
 //   db1 += sum dh1 ; dgbp[b][t][c] = sum_{rows of item} ds1
 // LDS: Wl 32 KB + h1 tile 8 KB + dpre tile 8 KB (reused for ds1) + D^T tile 16.5 KB -> 2 workgroups/CU.
 __global__ void __launch_bounds__(512) pc_ln_linear_bwd_kernel(
-    const bf16_t* __restrict__ dh2a, const bf16_t* __restrict__ dh2b, const bf16_t* __restrict__ s1,
+    const bf16_t* __restrict__ dh2a, const bf16_t* __restrict__ dh2b, const bf16_t* __restrict__ dh2c,
+    const bf16_t* __restrict__ s1,
     const float4* __restrict__ stats, const float* __restrict__ g1, const float* __restrict__ be1,
     const bf16_t* __restrict__ wl, const float* __restrict__ bl, const float* __restrict__ g2,
     bf16_t* __restrict__ ds1, float* __restrict__ dgbp, float* __restrict__ dg2, float* __restrict__ db2,
@@ -235,19 +237,21 @@ __global__ void __launch_bounds__(512) pc_ln_linear_bwd_kernel(
   bool okn;
   size_t offn = row_of(item, okn);
   uint4 n_s = ldq(s1 + offn, okn), n_a = ldq(dh2a + offn, okn && dh2a), n_b = ldq(dh2b + offn, okn && dh2b);
+  uint4 n_c = ldq(dh2c + offn, okn && dh2c);
   float4 n_st = okn ? stats[offn / CH] : make_float4(0.f, 1.f, 0.f, 1.f);
   __syncthreads();
   for (; item < items; item += gridDim.x) {
     const bool ok = okn;
     const size_t off = offn;
     const float mean1 = n_st.x, rstd1 = n_st.y, mean2 = n_st.z, rstd2 = n_st.w;
-    float x[8], xh1[8], hv[8], dh[8], tmp[8];
+    float x[8], xh1[8], hv[8], dh[8], tmp[8], tmc[8];
     unpack8(n_s, x);
     unpack8(n_a, dh);
     unpack8(n_b, tmp);
+    unpack8(n_c, tmc);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      dh[e] += tmp[e];
+      dh[e] += tmp[e] + tmc[e];
       xh1[e] = (x[e] - mean1) * rstd1;
       hv[e] = ok ? bfround(xh1[e] * ga1[e] + bt1[e]) : 0.f;
     }
@@ -257,6 +261,7 @@ __global__ void __launch_bounds__(512) pc_ln_linear_bwd_kernel(
     n_s = ldq(s1 + offn, okn);
     n_a = ldq(dh2a + offn, okn && dh2a);
     n_b = ldq(dh2b + offn, okn && dh2b);
+    n_c = ldq(dh2c + offn, okn && dh2c);
     n_st = okn ? stats[offn / CH] : make_float4(0.f, 1.f, 0.f, 1.f);
     if (w < 4) gemm_fwd(ws, ht, yt, w, r, h);
     __syncthreads();                                                       // B: pre tile ready
@@ -407,9 +412,10 @@ PBX_EXPORT int pbx_pc_ln_linear_fwd(const void* s1, const float* g1, const float
   return pbx_launch_status();
 }
 
-// dh2a / dh2b: bf16 [B, L, 128] or null (summed); ds1 bf16 [B, L, 128] (written); dgbp fp32
+// dh2a / dh2b / dh2c: bf16 [B, L, 128] or null (summed); ds1 bf16 [B, L, 128] (written); dgbp fp32
 // [B, ceil(L/32), 128] (written); dg2/db2/dg1/db1/dbl [128] and dwl [128, 128] fp32 accumulated into.
-PBX_EXPORT int pbx_pc_ln_linear_bwd(const void* dh2a, const void* dh2b, const void* s1, const void* stats,
+PBX_EXPORT int pbx_pc_ln_linear_bwd(const void* dh2a, const void* dh2b, const void* dh2c, const void* s1,
+                                    const void* stats,
                                     const float* g1, const float* be1, const void* wl, const float* bl, const float* g2,
                                     void* ds1, float* dgbp, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                     float* dbl, int B, int L, hipStream_t st) {
@@ -417,7 +423,7 @@ PBX_EXPORT int pbx_pc_ln_linear_bwd(const void* dh2a, const void* dh2b, const vo
   const long items = (long)B * ((L + TR - 1) / TR);
   const int lds = 32768 + 2 * TR * 256 + TR * YS * 4;
   hipLaunchKernelGGL(pc_ln_linear_bwd_kernel, dim3(pc_grid(items)), dim3(512), lds, st, (const bf16_t*)dh2a,
-                     (const bf16_t*)dh2b, (const bf16_t*)s1, (const float4*)stats, g1, be1, (const bf16_t*)wl, bl, g2,
+                     (const bf16_t*)dh2b, (const bf16_t*)dh2c, (const bf16_t*)s1, (const float4*)stats, g1, be1, (const bf16_t*)wl, bl, g2,
                      (bf16_t*)ds1, dgbp, dg2, db2, dg1, db1, dwl, dbl, B, L);
   return pbx_launch_status();
 }

@@ -19,6 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import torch
 
@@ -30,13 +31,21 @@ from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, pack_conv, _grad_d
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_pc_ln_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                       _I, _I, _P])
+                                       _P, _I, _I, _P])
+_lib.register("pbx_pa_fused_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+
+# paper attention form: "fused" (csrc/paper_fused.hip: K/V projections on MFMA inside the attention
+# kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}) or "split" (library K/V GEMM +
+# csrc/paper_attn.hip core); PBX_PAPER_ATTN=split selects the latter
+PAPER_ATTN = os.environ.get("PBX_PAPER_ATTN", "fused")
+FUSED_CHUNK_F, FUSED_CHUNK_B = 256, 128     # positions per forward / backward work item
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
 
 
-def _split_k_chunks(R: int, cap: int = 64) -> int:
+def _split_k_chunks(R: int, cap: int = 128) -> int:
     """Number of row chunks for the split-K weight-gradient GEMMs (K = B*L rows): the library GEMM
     of a [128, R] x [R, 768] product has 12 output tiles, i.e. 12 busy CUs; chunked bmm gives
     chunks x 12 tiles and the chunk partials are summed in fp32."""
@@ -90,17 +99,29 @@ class PaperBlockFn(torch.autograd.Function):
         gf = g.detach().float()
         q = torch.tanh(torch.einsum("bg,hgk->bhk", gf, Wq.detach().float()))             # [B, H, K]
         qs = (q * (1.0 / math.sqrt(K))).contiguous()
-        wcat = torch.cat([Wk.detach().permute(1, 0, 2).reshape(C, H * K),
-                          Wv.detach().permute(1, 0, 2).reshape(C, H * VD)], dim=1).to(BF16)   # [C, H*(K+VD)]
-        pre = torch.mm(h2.view(B * L, C), wcat)                                           # [R, N] bf16
-        ns = _nsplit(B, H, L)
-        part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
         o = torch.empty(B, H * VD, device=dev, dtype=F32)
         lse = torch.empty(B * H, device=dev, dtype=F32)
         mk = None if mask is None else mask.contiguous()
-        _lib.call("pbx_paper_attn_fwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), part.data_ptr(),
-                  o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
-        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wcat, pre, mk, o, lse, h2)
+        fused = PAPER_ATTN == "fused" and H in (2, 4)
+        if fused:
+            # [H][Wk_h^T (64 rows) | Wv_h^T (128 rows)][C] bf16: the MFMA A/B rows of the fused kernels
+            wimg = torch.cat([Wk.detach().permute(0, 2, 1), Wv.detach().permute(0, 2, 1)], dim=1).to(BF16).contiguous()
+            ns = -(-L // FUSED_CHUNK_F)
+            part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
+            _lib.call("pbx_pa_fused_fwd", h2.data_ptr(), wimg.data_ptr(), qs.data_ptr(), _lib.ptr(mk),
+                      part.data_ptr(), o.data_ptr(), lse.data_ptr(), B, L, H, stream)
+            wsave, pre = wimg, None
+        else:
+            wcat = torch.cat([Wk.detach().permute(1, 0, 2).reshape(C, H * K),
+                              Wv.detach().permute(1, 0, 2).reshape(C, H * VD)], dim=1).to(BF16)   # [C, H*(K+VD)]
+            pre = torch.mm(h2.view(B * L, C), wcat)                                       # [R, N] bf16
+            ns = _nsplit(B, H, L)
+            part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
+            _lib.call("pbx_paper_attn_fwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), part.data_ptr(),
+                      o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
+            wsave = wcat
+        ctx.fused = fused
+        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wsave, pre, mk, o, lse, h2)
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
         ctx.set_materialize_grads(False)
@@ -108,7 +129,7 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, do):
-        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wcat, pre, mk, o, lse, h2) = ctx.saved_tensors
+        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wsave, pre, mk, o, lse, h2) = ctx.saved_tensors
         B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -120,15 +141,28 @@ class PaperBlockFn(torch.autograd.Function):
         R, C = B * L, CH
         dh2 = None if dh2 is None else dh2.to(BF16).contiguous()
         dg = None
-        dh2_att = None
+        dh2_att = [None, None]
         if do is not None:
             dO = do.float().contiguous()
-            dpre = torch.empty_like(pre)
-            dq_part = torch.empty(B * H, ns, K, device=dev, dtype=F32)
-            _lib.call("pbx_paper_attn_bwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), lse.data_ptr(),
-                      o.data_ptr(), dO.data_ptr(), dpre.data_ptr(), dq_part.data_ptr(), B, L, H, K, VD, ns, stream)
+            if ctx.fused:
+                # keys / values recomputed on MFMA; dh2 per head pair, dpre rows for the dW GEMM
+                npair = H // 2
+                dh2p = torch.empty((npair, B, L, C), dtype=BF16, device=dev)
+                dpre = torch.empty((R, H * (K + VD)), dtype=BF16, device=dev)
+                nsb = -(-L // FUSED_CHUNK_B)
+                dq_part = torch.empty(B * H, nsb, K, device=dev, dtype=F32)
+                _lib.call("pbx_pa_fused_bwd", h2.data_ptr(), wsave.data_ptr(), qs.data_ptr(), _lib.ptr(mk),
+                          lse.data_ptr(), o.data_ptr(), dO.data_ptr(), dh2p.data_ptr(), dpre.data_ptr(),
+                          dq_part.data_ptr(), B, L, H, stream)
+                dh2_att = [dh2p[i] for i in range(npair)] + [None] * (2 - npair)
+            else:
+                dpre = torch.empty_like(pre)
+                dq_part = torch.empty(B * H, ns, K, device=dev, dtype=F32)
+                _lib.call("pbx_paper_attn_bwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), lse.data_ptr(),
+                          o.data_ptr(), dO.data_ptr(), dpre.data_ptr(), dq_part.data_ptr(), B, L, H, K, VD, ns,
+                          stream)
+                dh2_att = [torch.mm(dpre, wsave.t()), None]                               # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
-            dh2_att = torch.mm(dpre, wcat.t())                                             # [R, C] bf16
             nc = _split_k_chunks(R)
             dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
                               out_dtype=F32).sum(dim=0)                                   # [C, N] fp32
@@ -140,7 +174,8 @@ class PaperBlockFn(torch.autograd.Function):
         ds1 = torch.empty_like(x)
         T = (L + TR - 1) // TR
         dgbp = torch.empty((B, T, CH), dtype=F32, device=dev)
-        _lib.call("pbx_pc_ln_linear_bwd", _lib.ptr(dh2), _lib.ptr(dh2_att), s1.data_ptr(), stats.data_ptr(),
+        _lib.call("pbx_pc_ln_linear_bwd", _lib.ptr(dh2), _lib.ptr(dh2_att[0]), _lib.ptr(dh2_att[1]),
+                  s1.data_ptr(), stats.data_ptr(),
                   g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(),
                   dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
                   dbl.data_ptr(), B, L, stream)
@@ -221,7 +256,8 @@ class PaperHeadsLossFn(torch.autograd.Function):
         dlog.mul_((wl * inv).unsqueeze(1))
         dlog_bf = dlog.to(BF16)
         dh = torch.mm(dlog_bf, bf16_of(wo)).view(B, L, C)                             # bf16
-        dwo = mm32(dlog_bf.t(), hb)
+        nc = _split_k_chunks(B * L)                                                    # K = B*L: split-K
+        dwo = torch.bmm(dlog_bf.view(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C), out_dtype=F32).sum(dim=0)
         dbo = dlog.sum(dim=0)
         z = mm32(g2_bf, bf16_of(wa).t())
         dz = torch.empty((B, A), dtype=BF16, device=dev)

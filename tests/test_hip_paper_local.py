@@ -86,13 +86,19 @@ def test_paper_local_block_backward(L, B):
         assert e < 3e-2, f"{n}: rel err {e:.3e}"
 
 
-def test_paper_model_fused_loss_and_grads_vs_torch():
-    """Whole paper-semantics model (2 blocks) through the fused HIP path vs the fp32 torch oracle."""
+@pytest.mark.parametrize("L,attn", [(256, "fused"), (200, "fused"), (600, "fused"), (256, "split")])
+def test_paper_model_fused_loss_and_grads_vs_torch(L, attn, monkeypatch):
+    """Whole paper-semantics model (2 blocks) through the fused HIP path vs the fp32 torch oracle;
+    padded synthetic sequences exercise the attention mask, L=600 several 256-position chunks.
+    attn: "fused" = K/V projections inside the attention kernels (csrc/paper_fused.hip), "split" =
+    library K/V GEMM + csrc/paper_attn.hip core."""
     from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.ops import paper_track
     from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss, hip_supported
     from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
+    monkeypatch.setattr(paper_track, "PAPER_ATTN", attn)
     torch.manual_seed(0)
-    L, A = 256, 1024
+    A = 1024
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
                     num_blocks=2, device="cuda", backend="hip", semantics="paper")
     assert hip_supported(m)[0]
