@@ -71,20 +71,25 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // Reduce-scatter over the 32 lanes of a half-wave: on entry every lane holds v[0..31]; on exit lane r
-// (= lane & 31) returns sum over the 32 lanes of v[r].  31 exchanges instead of 32 x 5.
-__device__ __forceinline__ float reduce_scatter32(float (&v)[32], int r) {
+// (= lane & 31) returns sum over the 32 lanes of v[r].  31 exchanges instead of 32 x 5.  Each stage
+// is a template instance so every register index is a compile-time constant (a runtime index into a
+// register array becomes a compare/select chain per access).
+template <int N>
+__device__ __forceinline__ void rs_stage(float (&v)[32], int r) {
+  const bool up = (r & N) != 0;
 #pragma unroll
-  for (int off = 16, n = 16; off >= 1; off >>= 1, n >>= 1) {
-    const bool up = (r & off) != 0;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i < n) {
-        const float send = up ? v[i] : v[i + n];
-        const float keep = up ? v[i + n] : v[i];
-        v[i] = keep + __shfl_xor(send, off, 64);
-      }
-    }
+  for (int i = 0; i < N; ++i) {
+    const float send = up ? v[i] : v[i + N];
+    const float keep = up ? v[i + N] : v[i];
+    v[i] = keep + __shfl_xor(send, N, 64);
   }
+}
+__device__ __forceinline__ float reduce_scatter32(float (&v)[32], int r) {
+  rs_stage<16>(v, r);
+  rs_stage<8>(v, r);
+  rs_stage<4>(v, r);
+  rs_stage<2>(v, r);
+  rs_stage<1>(v, r);
   return v[0];
 }
 
@@ -213,9 +218,9 @@ __global__ __launch_bounds__(64) void pa_fused_combine_kernel(const float* __res
 // backward: recompute keys / values per tile, p = exp(s - lse);
 //   dv = p dO GELU'(v_pre) ; ds = p (dO . v - dO . o) ; dk = ds q (1 - tanh^2) ; dq = sum_l ds tanh(k)
 //   dh2 (per head pair) = Wv dv + Wk dk ; dpre rows = [dk | dv] (for dW = h2^T dpre)
-// one wave per SIMD (4 waves, 128-position chunks): the recompute + two gradient GEMM chains of a
-// tile need ~300 registers
-constexpr int NWB = 4;
+// 8 waves (two per SIMD) of 32 positions; the keys are recomputed after the value loop instead of
+// keeping 32 tanh values live across it, which fits a wave in 256 registers
+constexpr int NWB = 8;
 constexpr int CHUNKB = 32 * NWB;
 __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ wimg, const float* __restrict__ qs,
@@ -261,8 +266,7 @@ __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
 #pragma unroll 1
     for (int j = 0; j < HP; ++j) {
       const int hd = h0 + j;
-      // ---- keys, score, p
-      float t[32];
+      // ---- keys (pass 1): score and p
       float sp = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -270,13 +274,8 @@ __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 q4 = *reinterpret_cast<const float4*>(qsl + j * PK + kb * 32 + 8 * g + 4 * h);
-          const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float tv = tanh_fast(ka[4 * g + e]);
-            t[kb * 16 + 4 * g + e] = tv;
-            sp = fmaf(qq[e], tv, sp);
-          }
+          sp += q4.x * tanh_fast(ka[4 * g]) + q4.y * tanh_fast(ka[4 * g + 1]) + q4.z * tanh_fast(ka[4 * g + 2]) +
+                q4.w * tanh_fast(ka[4 * g + 3]);
         }
       }
       const float s = sp + __shfl_xor(sp, 32, 64);
@@ -323,34 +322,32 @@ __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
       }
       dp += __shfl_xor(dp, 32, 64);
       const float ds = p * (dp - cst[2 * j + 1]);
-      // ---- keys: dk = ds q (1 - t^2), dh2 += Wk dk ; dq partial terms ds * t
-      float dk[32];
+      // ---- keys (pass 2, recomputed: cheaper than 32 live registers across the value loop):
+      //      dk = ds q (1 - t^2) -> dpre, dh2 += Wk dk ; dq terms u = ds t
+      float u[32];
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+      for (int kb = 0; kb < 2; ++kb) {
+        const f32x16_t ka = rows_x_h(ws, j * HROWS + kb * 32, hf, r, h);
+        float dk[16];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const float4 q4 = *reinterpret_cast<const float4*>(qsl + j * PK + kb * 32 + 8 * g + 4 * h);
           const float qq[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const float tv = t[kb * 16 + 4 * g + e];
-            dk[kb * 16 + 4 * g + e] = ds * qq[e] * fmaf(-tv, tv, 1.0f);
-            t[kb * 16 + 4 * g + e] = ds * tv;                        // reuse: dq terms
+            const float tv = tanh_fast(ka[4 * g + e]);
+            dk[4 * g + e] = ds * qq[e] * fmaf(-tv, tv, 1.0f);
+            u[kb * 16 + 4 * g + e] = ds * tv;
           }
         }
-      if (inb) {
-        bf16_t* drow = dpre + row * NC + hd * PK;
+        if (inb) {
+          bf16_t* drow = dpre + row * NC + hd * PK + kb * 32;
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<uint2*>(drow + kb * 32 + 8 * g + 4 * h) = packq4(dk + kb * 16 + 4 * g);
-      }
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
+          for (int g = 0; g < 4; ++g) *reinterpret_cast<uint2*>(drow + 8 * g + 4 * h) = packq4(dk + 4 * g);
+        }
 #pragma unroll
         for (int sh = 0; sh < 2; ++sh) {
-          const bf16x8 fb = pack8(dk + kb * 16 + 8 * sh);
+          const bf16x8 fb = pack8(dk + 8 * sh);
           const int rlo = j * HROWS + kb * 32 + 16 * sh + 4 * h + q;
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct) {
@@ -359,8 +356,9 @@ __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
             y[ct] = mfma32(fa, fb, y[ct]);
           }
         }
+      }
       // dq: lane (r, h) ends with k = (r >> 4) * 32 + 8 ((r & 15) >> 2) + 4 h + (r & 3)
-      const float dqv = reduce_scatter32(t, r);
+      const float dqv = reduce_scatter32(u, r);
       dqs[(w * HP + j) * PK + (r >> 4) * 32 + 8 * ((r & 15) >> 2) + 4 * h + (r & 3)] = dqv;
     }
     // dh2 of this head pair: y[ct][4g + e] = D[c = ct*32 + 8g + 4h + e][pos]

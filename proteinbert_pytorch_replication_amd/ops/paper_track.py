@@ -39,7 +39,7 @@ _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _
 # kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}) or "split" (library K/V GEMM +
 # csrc/paper_attn.hip core); PBX_PAPER_ATTN=split selects the latter
 PAPER_ATTN = os.environ.get("PBX_PAPER_ATTN", "fused")
-FUSED_CHUNK_F, FUSED_CHUNK_B = 256, 128     # positions per forward / backward work item
+FUSED_CHUNK_F, FUSED_CHUNK_B = 256, 256     # positions per forward / backward work item
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
