@@ -220,8 +220,7 @@ __global__ __launch_bounds__(64) void pa_fused_combine_kernel(const float* __res
 //   dh2 (per head pair) = Wv dv + Wk dk ; dpre rows = [dk | dv] (for dW = h2^T dpre)
 // 8 waves (two per SIMD) of 32 positions; the keys are recomputed after the value loop instead of
 // keeping 32 tanh values live across it, which fits a wave in 256 registers
-constexpr int NWB = 8;
-constexpr int CHUNKB = 32 * NWB;
+template <int NWB>
 __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ wimg, const float* __restrict__ qs,
     const unsigned char* __restrict__ mask, const float* __restrict__ lse, const float* __restrict__ o,
@@ -237,6 +236,7 @@ __global__ void __launch_bounds__(64 * NWB) pa_fused_bwd_kernel(
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int h0 = blockIdx.y * HP;
+  constexpr int CHUNKB = 32 * NWB;
   const int nsplit = (L + CHUNKB - 1) / CHUNKB;
   const long items = (long)B * nsplit;
   const int NC = H * (PK + PV);                                      // dpre row length
@@ -399,7 +399,8 @@ bool g_pf_attrs = false;
 void pf_attrs() {
   if (g_pf_attrs) return;
   (void)hipFuncSetAttribute((const void*)pa_fused_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)pa_fused_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)pa_fused_bwd_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)pa_fused_bwd_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   g_pf_attrs = true;
 }
 dim3 pf_grid(long items, int H) {
@@ -427,16 +428,16 @@ PBX_EXPORT int pbx_pa_fused_fwd(const void* h2, const void* wimg, const float* q
 }
 
 // dh2 [H/2][B, L, 128] bf16 (one buffer per head pair, every in-range row written); dpre [B, L, H*(64+128)]
-// bf16 ([dk heads | dv heads], in-range rows written); dq_part [B*H][ceil(L/128)][64] fp32 (written)
+// bf16 ([dk heads | dv heads], in-range rows written); dq_part [B*H][ceil(L/(32 nwb))][64] fp32 (written)
 PBX_EXPORT int pbx_pa_fused_bwd(const void* h2, const void* wimg, const float* qs, const void* mask, const float* lse,
                                 const float* o, const float* dO, void* dh2, void* dpre, float* dq_part, int B, int L,
-                                int H, hipStream_t st) {
-  if (B <= 0 || L <= 0 || H <= 0 || (H % HP) != 0) return (int)hipErrorInvalidValue;
+                                int H, int nwb, hipStream_t st) {
+  if (B <= 0 || L <= 0 || H <= 0 || (H % HP) != 0 || (nwb != 4 && nwb != 8)) return (int)hipErrorInvalidValue;
   pf_attrs();
-  const int nsplit = (L + CHUNKB - 1) / CHUNKB;
-  const int lds = WBYTES + (HP * PK + HP * PV + HP * 2 + NWB * HP * PK) * 4;
-  hipLaunchKernelGGL(pa_fused_bwd_kernel, pf_grid((long)B * nsplit, H), dim3(64 * NWB), lds, st, (const bf16_t*)h2,
-                     (const bf16_t*)wimg, qs, (const unsigned char*)mask, lse, o, dO, (bf16_t*)dh2, (bf16_t*)dpre,
-                     dq_part, B, L, H);
+  const int nsplit = (L + 32 * nwb - 1) / (32 * nwb);
+  const int lds = WBYTES + (HP * PK + HP * PV + HP * 2 + nwb * HP * PK) * 4;
+  hipLaunchKernelGGL(nwb == 8 ? pa_fused_bwd_kernel<8> : pa_fused_bwd_kernel<4>, pf_grid((long)B * nsplit, H),
+                     dim3(64 * nwb), lds, st, (const bf16_t*)h2, (const bf16_t*)wimg, qs, (const unsigned char*)mask,
+                     lse, o, dO, (bf16_t*)dh2, (bf16_t*)dpre, dq_part, B, L, H);
   return pbx_launch_status();
 }

@@ -33,13 +33,14 @@ _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _
 _lib.register("pbx_pc_ln_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _P, _I, _I, _P])
 _lib.register("pbx_pa_fused_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
-_lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 
 # paper attention form: "fused" (csrc/paper_fused.hip: K/V projections on MFMA inside the attention
 # kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}) or "split" (library K/V GEMM +
 # csrc/paper_attn.hip core); PBX_PAPER_ATTN=split selects the latter
 PAPER_ATTN = os.environ.get("PBX_PAPER_ATTN", "fused")
-FUSED_CHUNK_F, FUSED_CHUNK_B = 256, 256     # positions per forward / backward work item
+FUSED_CHUNK_F = 256                         # positions per forward work item
+FUSED_BWD_WAVES = int(os.environ.get("PBX_PF_BWD_WAVES", "8"))   # backward: 32 positions per wave
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
@@ -149,11 +150,11 @@ class PaperBlockFn(torch.autograd.Function):
                 npair = H // 2
                 dh2p = torch.empty((npair, B, L, C), dtype=BF16, device=dev)
                 dpre = torch.empty((R, H * (K + VD)), dtype=BF16, device=dev)
-                nsb = -(-L // FUSED_CHUNK_B)
+                nsb = -(-L // (32 * FUSED_BWD_WAVES))
                 dq_part = torch.empty(B * H, nsb, K, device=dev, dtype=F32)
                 _lib.call("pbx_pa_fused_bwd", h2.data_ptr(), wsave.data_ptr(), qs.data_ptr(), _lib.ptr(mk),
                           lse.data_ptr(), o.data_ptr(), dO.data_ptr(), dh2p.data_ptr(), dpre.data_ptr(),
-                          dq_part.data_ptr(), B, L, H, stream)
+                          dq_part.data_ptr(), B, L, H, FUSED_BWD_WAVES, stream)
                 dh2_att = [dh2p[i] for i in range(npair)] + [None] * (2 - npair)
             else:
                 dpre = torch.empty_like(pre)
