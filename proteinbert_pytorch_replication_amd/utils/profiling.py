@@ -5,7 +5,7 @@ The reference only times iterations on the host (``ProteinBERT/utils.py:284,306,
 * :class:`StepProfiler` - a ``torch.profiler`` window over training steps ``[start, start + count)``
   (HIP kernels through roctracer on ROCm, CPU ops elsewhere), written as a Chrome trace plus a
   per-kernel table; kernel-level counters come from ``rocprofv3`` around the same command
-  (``tools/gpu_prof.sh``, ``tools/gpu_pmc2.sh``).
+  (``tools/gpu_prof.sh``, ``tools/gpu_pmc_final.sh``).
 * :func:`marker` - a named range (``torch.cuda.nvtx`` -> roctx on ROCm) that shows up in rocprofv3
   / the trace, around phases such as ``pbx/step`` or ``pbx/checkpoint``.
 """
