@@ -79,6 +79,8 @@ def stream_ptr(device: Optional[torch.device] = None) -> int:
 
 
 def call(name: str, *args) -> None:
+    if name not in _SIGS:   # ctypes would pass Python ints as 32-bit C ints and truncate device pointers
+        raise HipError(f"{name}: launcher not registered (import the ops module that declares it)")
     rc = getattr(lib(), name)(*args)
     if rc != 0:
         raise HipError(f"{name} failed with hipError {rc}")

@@ -1,0 +1,59 @@
+"""Time the fragment-streamed conv kernels (conv_fwd3 / conv_dgrad3, csrc/conv2.hip) at the bench shape
+(B=512, L=512) with whatever library PBX_HIP_LIB names: phase ablations are separate builds of the
+same source built with extra -D flags (tools/ubench/build_flags.sh <name> -D...).
+
+    PBX_HIP_LIB=tools/ubench/abl/libpbx_noepi.so python tools/ubench/convbench.py --tag noepi
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from proteinbert_pytorch_replication_amd.ops import _lib, local_track  # noqa: E402,F401  (registers the launchers)
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--B", type=int, default=512)
+ap.add_argument("--L", type=int, default=512)
+ap.add_argument("--iters", type=int, default=20)
+ap.add_argument("--tag", default="")
+a = ap.parse_args()
+B, L, C, KS, dil = a.B, a.L, 128, 9, 5
+dev = torch.device("cuda")
+st = _lib.stream_ptr(dev)
+bf = torch.bfloat16
+
+
+def timeit(fn, n=a.iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1000.0
+
+
+flops = 2 * 2 * B * L * C * C * KS
+x = (torch.randn(B, L, C, device=dev) * 0.5).to(bf)
+w = torch.randn(C, C, KS, device=dev) * 0.03
+fp, ft = torch.empty(KS, C, C, dtype=bf, device=dev), torch.empty(KS, C, C, dtype=bf, device=dev)
+_lib.call("pbx_pack_conv_frag", w.data_ptr(), fp.data_ptr(), ft.data_ptr(), KS, st)
+bias = torch.randn(C, device=dev) * 0.1
+gb = torch.randn(B, C, device=dev) * 0.1
+pre_n, pre_w, s1 = (torch.empty_like(x) for _ in range(3))
+stt = torch.empty(B, (L + 127) // 128, 2, device=dev)
+fwd = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
+                        bias.data_ptr(), gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(),
+                        stt.data_ptr(), B, L, KS, dil, 128, st)
+us = timeit(fwd)
+print(f"[{a.tag}] conv_fwd3   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
+dx, dpn, dpw = (torch.empty_like(x) for _ in range(3))
+dg = lambda: _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
+                       ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, st)
+us = timeit(dg)
+print(f"[{a.tag}] conv_dgrad3 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
