@@ -114,6 +114,14 @@ __device__ __forceinline__ void col_atomic(const float (*v)[4], const bool* rok,
   }
 }
 
+// mean of wp[0..K) on every lane: one load round trip per 64 values (a per-thread scalar loop waits
+// one scalar-cache round trip per element)
+__device__ __forceinline__ float wave_mean(const float* __restrict__ wp, int K, int lane) {
+  float a = 0.f;
+  for (int i = lane; i < K; i += 64) a += wp[i];
+  return wave_reduce_sum(a) / (float)K;
+}
+
 // ------------------------------------------------------------------------------------------------
 // forward.  NW waves of NT column tiles each (G = 16 NT NW); NGL = 0 (last block, no gb) or 128
 // (waves 0 .. NGL/16 - 1 compute one gb column tile each).
@@ -141,6 +149,7 @@ __global__ void __launch_bounds__(NW * 64) glob_fwd_kernel(
     grow[i] = min(row0 + 4 * q + i, B - 1);       // clamped: loads stay in bounds, stores masked
   }
   const int col0 = w * NT * 16;
+  const float scale = wave_mean(wp, K, lane);
   // A tile <- g_bf rows
   for (int idx = tid; idx < RB * G / 8; idx += NW * 64) {
     const int row = idx / (G / 8), ch = idx % (G / 8);
@@ -148,9 +157,6 @@ __global__ void __launch_bounds__(NW * 64) glob_fwd_kernel(
     *reinterpret_cast<uint4*>(at + atile(row, ch, G)) =
         *reinterpret_cast<const uint4*>(g_bf + (size_t)gr * G + ch * 8);
   }
-  float scale = 0.f;
-  for (int i = 0; i < K; ++i) scale += wp[i];
-  scale /= (float)K;
   float res[NT][4], vs[NT][4];
 #pragma unroll
   for (int t = 0; t < NT; ++t)
@@ -159,17 +165,27 @@ __global__ void __launch_bounds__(NW * 64) glob_fwd_kernel(
       res[t][i] = g[(size_t)grow[i] * G + col0 + t * 16 + c16];
       vs[t][i] = 0.f;
     }
-  // attention partial sums: tile loop outside, so the NT * 4 loads of one tile are in flight together
-  for (int tv = 0; tv < TV; ++tv) {
-    float v[NT][4];
+  // attention partial sums: the loads of TVU tiles are in flight together (clamped tile index, the
+  // surplus ones weighted 0: no branch, so no wait per tile)
+  constexpr int TVU = 4;
+  for (int tv0 = 0; tv0 < TV; tv0 += TVU) {
+    float v[TVU][NT][4];
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+    for (int u = 0; u < TVU; ++u) {
+      const int tv = min(tv0 + u, TV - 1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[t][i] = vpart[((size_t)grow[i] * TV + tv) * G + col0 + t * 16 + c16];
+      for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int t = 0; t < NT; ++t)
+        for (int i = 0; i < 4; ++i) v[u][t][i] = vpart[((size_t)grow[i] * TV + tv) * G + col0 + t * 16 + c16];
+    }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) vs[t][i] += v[t][i];
+    for (int u = 0; u < TVU; ++u) {
+      const float m = tv0 + u < TV ? 1.f : 0.f;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) vs[t][i] = fmaf(m, v[u][t][i], vs[t][i]);
+    }
   }
   __syncthreads();
 
@@ -341,9 +357,7 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
     __syncthreads();                              // A tile is rewritten below
   }
 
-  float scale = 0.f;
-  for (int i = 0; i < K; ++i) scale += wp[i];
-  scale /= (float)K;
+  const float scale = wave_mean(wp, K, lane);
 
   // LayerNorm + GELU backward of one stage: dy (acc) -> ds = rstd (dy g - m1 - xh m2) ;
   // du = ds GELU'(pre) (A tile + global) ; column sums dgam += dy xh, dbet += dy, dbias += du.
