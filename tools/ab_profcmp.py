@@ -1,11 +1,12 @@
 """Compare two rocprofv3 kernel_stats.csv files (per-call average by kernel): python tools/ab_profcmp.py A B"""
 import csv
 import glob
+import os
 import sys
 
 
 def load(d):
-    f = glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True)[0]
+    f = max(glob.glob(f"{d}/**/*kernel_stats.csv", recursive=True), key=os.path.getmtime)
     return {r["Name"][:70]: (float(r["AverageNs"]) / 1e3, int(r["Calls"]), float(r["TotalDurationNs"]) / 1e3)
             for r in csv.DictReader(open(f))}
 
