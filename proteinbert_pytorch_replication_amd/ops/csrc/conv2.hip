@@ -61,19 +61,19 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   unsigned char* xs = smem;                                   // XR x 256 B (swz256)
   unsigned char* ot = smem + XR * 256;                        // [TBM][128] bf16 staging tile
   float* bsm = reinterpret_cast<float*>(ot + TOT);            // bn | bw | gb[b] | LN scratch
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
   const bf16_t* xsmp = x + (size_t)b * L * CH;
-  const bf16x8* fw = (cv ? fww : fwn) + cq * 64 + lane;     // + frag_index(k, kb, 0) * 64
+  const bf16x8* fw = (cv ? fww : fwn) + cq * 64;            // wave-uniform; + frag_index(k, kb, 0) * 64 + lane
   const int NI = KS * 8;                                      // K-steps: taps x 16-channel blocks
   // A-fragment ring: step it uses fr[it & 3], the load for step it + 3 is in flight meanwhile (the
   // loop is unrolled by the ring size so the ring never rotates registers, which would make the
   // compiler wait for the newest load every step)
   bf16x8 fr[4];
-  fr[0] = fw[0];
-  fr[1] = fw[256];
-  fr[2] = fw[512];
+  fr[0] = fw[lane];
+  fr[1] = fw[256 + lane];
+  fr[2] = fw[512 + lane];
   if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
   stage_chunks(
       XR * 16,
@@ -89,17 +89,22 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
 #pragma unroll
   for (int i = 0; i < NPT; ++i) acc[i] = zero16();
   const int d = cv ? dil : 1;
-  for (int it0 = 0; it0 < NI; it0 += 4) {
+  // tap loop outside, the 8 channel blocks of a tap unrolled: the swz256 byte offset of (row rb + 32 pt,
+  // chunk 2 kb + h) is rowb + 8192 pt + ((32 kb) ^ gs) with rowb / gs fixed per tap, so a step costs one
+  // v_xad_u32 instead of the ~7 VALU of the general swizzle; the weight fragment address is a scalar
+  // base + the lane offset (no per-step 64-bit vector add)
+  for (int k = 0; k < KS; ++k) {
+    const int rb = halo + r + (k - half) * d;
+    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = it0 + u;
-      fr[(u + 3) & 3] = fw[min(it + 3, NI - 1) * 256];
+    for (int kb = 0; kb < 8; ++kb) {
+      const int it = k * 8 + kb;
+      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
+      fr[(kb + 3) & 3] = fwk[lane];
       __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
-      const int k = it >> 3, kb = it & 7;
-      const int rb = halo + r + (k - half) * d;
+      const int off = ((32 * kb) ^ gs) + rowb;
 #pragma unroll
-      for (int pt = 0; pt < NPT; ++pt)
-        acc[pt] = mfma32(fr[u], lds_frag(xs, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
+      for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(xs, off + pt * 8192), acc[pt]);
     }
   }
 
@@ -132,8 +137,13 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       }
   }
   __syncthreads();
-  float lsum = 0.f, lsq = 0.f;
-  int cnt = 0;
+  // s1 = x + GELU(pre_n) + GELU(pre_w) + gb in packed pairs; the LayerNorm partial of the tile as
+  // plain (sum, sum of squares) of the stored bf16 values -- per row, masked once -- merged to
+  // (mean, M2) by one thread at the end (the per-thread / per-lane Chan merges cost a division each)
+  f32x2 s2v = {0.f, 0.f};                          // (sum, sum of squares)
+  const float4 g0 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8);
+  const float4 g1 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8 + 4);
+  const f32x2 gbp[4] = {(f32x2){g0.x, g0.y}, (f32x2){g0.z, g0.w}, (f32x2){g1.x, g1.y}, (f32x2){g1.z, g1.w}};
 #pragma unroll
   for (int i = 0; i < NPT; ++i) {
     const int idx = tid + 512 * i;
@@ -146,7 +156,7 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       *reinterpret_cast<uint4*>(pre_n + off) = pnq;
       *reinterpret_cast<uint4*>(pre_w + off) = pwq;
     }
-    float xv[8], pn[8], pw[8], o[8];
+    float xv[8], pn[8], pw[8];
     unpack8(xq[i], xv);
     unpack8(pnq, pn);
     unpack8(pwq, pw);
@@ -156,35 +166,40 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       gi[e] = (f32x2){pn[2 * e], pn[2 * e + 1]};
       gi[4 + e] = (f32x2){pw[2 * e], pw[2 * e + 1]};
     }
-    gelu2_fast_n<8, false>(gi, go);
-    const float4 g0 = *reinterpret_cast<const float4*>(bsm + 2 * CH + c * 8);
-    const float4 g1 = *reinterpret_cast<const float4*>(bsm + 2 * CH + c * 8 + 4);
-    const float gba[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    gelu2_fast_n<4, false>(gi, go);
+    gelu2_fast_n<4, false>(gi + 4, go + 4);
+    float o[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float gn = (e & 1) ? go[e >> 1].y : go[e >> 1].x;
-      const float gw = (e & 1) ? go[4 + (e >> 1)].y : go[4 + (e >> 1)].x;
-      o[e] = bfround(xv[e] + gn + gw + gba[e]);
-      lsum += ok ? o[e] : 0.f;
-      lsq += ok ? o[e] * o[e] : 0.f;
+    for (int e = 0; e < 4; ++e) {
+      const f32x2 v = (f32x2){xv[2 * e], xv[2 * e + 1]} + go[e] + go[4 + e] + gbp[e];
+      o[2 * e] = v.x;
+      o[2 * e + 1] = v.y;
     }
-    cnt += ok ? 8 : 0;
-    if (ok) *reinterpret_cast<uint4*>(s1 + off) = packq8(o);
+    const uint4 oq = packq8(o);
+    if (ok) *reinterpret_cast<uint4*>(s1 + off) = oq;
+    float orr[8];
+    unpack8(oq, orr);                                // the stored (rounded) values
+    f32x2 rs = {0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const f32x2 pv = {orr[e], orr[e + 1]};
+      rs += (f32x2){pv.x + pv.y, pv.x * pv.x + pv.y * pv.y};
+    }
+    s2v += ok ? rs : (f32x2){0.f, 0.f};
   }
-  float* scratch = bsm + 3 * CH;                  // 8 waves x (n, mean, M2)
+  float* scratch = bsm + 3 * CH;                  // 8 waves x (sum, sum of squares)
   {
-    float n = (float)cnt, m = cnt > 0 ? lsum / n : 0.f;
-    float M2 = cnt > 0 ? fmaxf(lsq - lsum * m, 0.f) : 0.f;
-    wave_chan(n, m, M2);
-    if (lane == 0) { scratch[3 * w] = n; scratch[3 * w + 1] = m; scratch[3 * w + 2] = M2; }
+    const float sa = wave_reduce_sum(s2v.x), sq = wave_reduce_sum(s2v.y);
+    if (lane == 0) { scratch[2 * w] = sa; scratch[2 * w + 1] = sq; }
   }
   __syncthreads();
   if (tid == 0) {
-    float tn = 0.f, tm = 0.f, tM2 = 0.f;
+    float sa = 0.f, sq = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) chan_merge(tn, tm, tM2, scratch[3 * i], scratch[3 * i + 1], scratch[3 * i + 2]);
-    stats[((size_t)b * T + t) * 2] = tm;
-    stats[((size_t)b * T + t) * 2 + 1] = tM2;
+    for (int i = 0; i < 8; ++i) { sa += scratch[2 * i]; sq += scratch[2 * i + 1]; }
+    const float n = (float)(vrows * CH), m = sa / n;
+    stats[((size_t)b * T + t) * 2] = m;
+    stats[((size_t)b * T + t) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
   }
 }
 
@@ -203,16 +218,16 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   const int RN = BM + 2 * halo_n;
   unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
   unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
   const size_t sbase = (size_t)b * L * CH;
-  const bf16x8* fw = (cv ? ftw : ftn) + cq * 64 + lane;
+  const bf16x8* fw = (cv ? ftw : ftn) + cq * 64;          // wave-uniform (+ lane per load)
   const int NI = KS * 8;
   bf16x8 fr[4];                                   // A-fragment ring, as in conv_fwd3
-  fr[0] = fw[0];
-  fr[1] = fw[256];
-  fr[2] = fw[512];
+  fr[0] = fw[lane];
+  fr[1] = fw[256 + lane];
+  fr[2] = fw[512 + lane];
 
   // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
 #pragma unroll 1
@@ -263,16 +278,18 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   const int d = cv ? dil : 1;
   const unsigned char* as = cv ? aw : an;
   const int halo = cv ? halo_w : halo_n;
-  for (int it0 = 0; it0 < NI; it0 += 4) {
+  for (int k = 0; k < KS; ++k) {                  // tap loop / unrolled channel blocks, as in conv_fwd3
+    const int rb = halo + r - (k - half) * d;
+    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int it = it0 + u;
-      fr[(u + 3) & 3] = fw[min(it + 3, NI - 1) * 256];
+    for (int kb = 0; kb < 8; ++kb) {
+      const int it = k * 8 + kb;
+      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
+      fr[(kb + 3) & 3] = fwk[lane];
       __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
-      const int k = it >> 3, kb = it & 7;
-      const int rb = halo + r - (k - half) * d;
+      const int off = ((32 * kb) ^ gs) + rowb;
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[u], lds_frag(as, swz256(rb + pt * 32, kb * 2 + h)), acc[pt]);
+      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(as, off + pt * 8192), acc[pt]);
     }
   }
 
