@@ -175,7 +175,7 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
             make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
     __syncthreads();
-    float pre[8], o[8], lsum = 0.f;
+    float pre[8], o[8];
     const float4 ya = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
     const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
     const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
@@ -188,33 +188,39 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
       gelu2_fast_n<4, false>(xi, gg);
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      o[e] = okl ? bfround(h1[e] + ((e & 1) ? gg[e >> 1].y : gg[e >> 1].x)) : 0.f;
-      lsum += o[e];
-    }
+    for (int e = 0; e < 8; ++e) o[e] = h1[e] + ((e & 1) ? gg[e >> 1].y : gg[e >> 1].x);
+    const uint4 oq = packq8(o);
     if (okl) {
       const size_t off = ((size_t)b * L + l) * CH + ch * 8;
       *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);
-      *reinterpret_cast<uint4*>(s2 + off) = packq8(o);
+      *reinterpret_cast<uint4*>(s2 + off) = oq;
     }
-    // this thread's (count, mean, M2), merged across the wave into the LDS partial table
-    float n = okl ? 8.f : 0.f, m = okl ? lsum * 0.125f : 0.f, M2 = 0.f;
+    // (sum, sum of squares) of the stored values, reduced over the wave into the LDS partial table
+    // (a per-lane Chan merge costs a division per butterfly step)
+    float orr[8];
+    unpack8(oq, orr);
+    float sa = 0.f, sq = 0.f;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) M2 += okl ? (o[e] - m) * (o[e] - m) : 0.f;
-    wave_chan(n, m, M2);
-    if (lane == 0) { part[(i * 8 + w) * 2] = m; part[(i * 8 + w) * 2 + 1] = M2; }
+    for (int e = 0; e < 8; ++e) {
+      sa += orr[e];
+      sq += orr[e] * orr[e];
+    }
+    sa = wave_reduce_sum(okl ? sa : 0.f);
+    sq = wave_reduce_sum(okl ? sq : 0.f);
+    if (lane == 0) { part[(i * 8 + w) * 2] = sa; part[(i * 8 + w) * 2 + 1] = sq; }
   }
   __syncthreads();
   const int vrows = min(PB, L - l0);
   for (int i = tid; i < nb; i += 512) {
-    float n = 0.f, m = 0.f, M2 = 0.f;
+    float sa = 0.f, sq = 0.f;
 #pragma unroll
     for (int ww = 0; ww < 8; ++ww) {
-      const float nw = (float)(max(0, min(4, vrows - 4 * ww)) * CH);
-      chan_merge(n, m, M2, nw, part[(i * 8 + ww) * 2], part[(i * 8 + ww) * 2 + 1]);
+      sa += part[(i * 8 + ww) * 2];
+      sq += part[(i * 8 + ww) * 2 + 1];
     }
+    const float m = sa / (float)(vrows * CH);
     st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = m;
-    st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = M2;
+    st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
   }
 }
 
