@@ -992,9 +992,11 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
   }
   float ga[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (okl) load_f8(g1 + (size_t)l * CH + ch * 8, ga);
-  const size_t coff = (size_t)l * CH + ch * 8;
-  uint4 n_dh = ldq(dh1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
-  uint4 n_s = ldq(s1 + (size_t)b0 * L * CH + coff, okl && b0 < b1);
+  // loads from a clamped valid row (masked at use): a select on the load becomes a branch around
+  // it, and the wait for it a vmcnt(0)
+  const size_t coff = (size_t)min(l, L - 1) * CH + ch * 8;
+  uint4 n_dh = *reinterpret_cast<const uint4*>(dh1 + (size_t)min(b0, B - 1) * L * CH + coff);
+  uint4 n_s = *reinterpret_cast<const uint4*>(s1 + (size_t)min(b0, B - 1) * L * CH + coff);
   __syncthreads();
   for (int b = b0; b < b1; ++b) {
     const float* tb = tab + 4 * (b - b0);
@@ -1003,21 +1005,29 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     float dv[8], sv[8], o[8];
     unpack8(n_dh, dv);
     unpack8(n_s, sv);
-    const size_t noff = (size_t)(b + 1) * L * CH + coff;
-    n_dh = ldq(dh1 + noff, okl && b + 1 < b1);
-    n_s = ldq(s1 + noff, okl && b + 1 < b1);
+    const size_t noff = (size_t)min(b + 1, B - 1) * L * CH + coff;
+    n_dh = *reinterpret_cast<const uint4*>(dh1 + noff);
+    n_s = *reinterpret_cast<const uint4*>(s1 + noff);
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = okl ? rstd * (dv[e] * ga[e] - m1 - (sv[e] - mean) * rstd * m2) : 0.f;
     const uint4 qv = packq8(o);
-    if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + coff) = qv;
+    if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + (size_t)l * CH + ch * 8) = qv;
+    // dgb column sums: the wave's 4 rows by shuffles, one [128] partial per wave, 8 adds per channel
     unpack8(qv, o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) rb[j * CH + ch * 8 + e] = o[e];
+    for (int e = 0; e < 8; ++e) {
+      o[e] += __shfl_xor(o[e], 16, 64);
+      o[e] += __shfl_xor(o[e], 32, 64);
+    }
+    if (lane < 16) {
+      *reinterpret_cast<float4*>(rb + w * CH + ch * 8) = make_float4(o[0], o[1], o[2], o[3]);
+      *reinterpret_cast<float4*>(rb + w * CH + ch * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+    }
     __syncthreads();   // (double buffer: the next sample writes the other half)
     if (tid < CH) {
       float a = 0.f;
-#pragma unroll 8
-      for (int k = 0; k < PB; ++k) a += rb[k * CH + tid];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += rb[k * CH + tid];
       atomicAdd(dgb + (size_t)b * CH + tid, a);
     }
   }
