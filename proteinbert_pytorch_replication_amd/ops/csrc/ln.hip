@@ -753,9 +753,13 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
 __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict__ st2, int T2, int BM2,
                                                          const float* __restrict__ sums2, int TS2,
                                                          const float* __restrict__ st1, int T1, int BM1,
-                                                         float* __restrict__ consts, int B, int L, float eps) {
+                                                         float* __restrict__ consts, float* __restrict__ zero128,
+                                                         int B, int L, float eps) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
+  // zero row b of the [B, 128] accumulator the LN1 finalize adds into (saves a fill launch per block)
+  if (zero128 != nullptr)
+    *reinterpret_cast<float2*>(zero128 + (size_t)b * CH + 2 * (threadIdx.x & 63)) = make_float2(0.f, 0.f);
   float mean2, rstd2, m1, m2, mean1, rstd1;
   wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BM2, L, CH, eps, mean2, rstd2);
   wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, 1.0f / (float)(L * CH), m1, m2);
@@ -1227,11 +1231,11 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
                                   int BM1, const float* g1, const float* be1, const void* wl, float* consts,
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
-                                  float* dbl, int B, int L, float eps, hipStream_t st) {
+                                  float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
-                     consts, B, L, eps);
+                     consts, dgb_zero, B, L, eps);
   const int pairs = (L + 1) / 2;
   int nsplit = (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
   if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;

@@ -42,7 +42,7 @@ _lib.register("pbx_attn_bwd", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                     _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl
+                                     _P, _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl, dgb
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
@@ -273,14 +273,14 @@ class LocalBlockFn(torch.autograd.Function):
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)
         sums1 = torch.empty((B, TS1, 2), dtype=torch.float32, device=dev)
         consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
+        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts kernel
         _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(), TA,
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  B, L, LN_EPS, stream)
+                  dgb.data_ptr(), B, L, LN_EPS, stream)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
-        dgb = torch.zeros((B, CH), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(), TS1,
                   g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, stream)
         if streams.GLOBAL_ENABLED:
