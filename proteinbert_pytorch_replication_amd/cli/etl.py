@@ -60,7 +60,7 @@ def uniref_h5_parser() -> argparse.ArgumentParser:
                    required=True, help="Path to a CSV file with the count of each GO annotation.")
     p.add_argument("--output-h5-dataset-file", dest="output_h5_dataset_file", metavar="/path/to/dataset.h5",
                    type=get_parser_file_type(p), required=True,
-                   help="Output dataset (HDF5 when h5py is importable, else a .pbxds directory).")
+                   help="Output dataset (HDF5 for *.h5 paths, else a .pbxds directory).")
     p.add_argument("--min-records-to-keep-annotation", dest="min_records_to_keep_annotation", metavar="100",
                    type=int, default=100, help="Minimal number of records required to encode an annotation.")
     p.add_argument("--log-progress-every", dest="log_progress_every", metavar="10000", type=int, default=10000,
@@ -72,7 +72,7 @@ def uniref_h5_parser() -> argparse.ArgumentParser:
     p.add_argument("--no-shuffle", dest="no_shuffle", action="store_true", help="Disable the record shuffle.")
     p.add_argument("--silent", dest="silent", action="store_true", help="Run in silent mode.")
     p.add_argument("--format", dest="format", choices=["auto", "h5", "pbxds"], default="auto",
-                   help="Output store format (auto: h5 for *.h5 paths when h5py is importable).")
+                   help="Output store format (auto: h5 for *.h5 paths, pbxds otherwise).")
     return p
 
 

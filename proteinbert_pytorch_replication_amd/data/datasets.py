@@ -77,9 +77,8 @@ class UniRefGO_StorePretrainingDataset(data.Dataset):
 
     Replaces the reference's broken HDF5 reader: it reads the
     layout that the reference writer actually produces
-    (``uniref_dataset.py:236-245``), through :class:`ProteinStore` (HDF5 when
-    h5py is importable, otherwise the memory-mapped ``.pbxds`` directory
-    format).  ``rank``/``world_size`` shard the index space for DP.
+    (``uniref_dataset.py:236-245``), through :class:`ProteinStore` (the reference HDF5
+    file, or the memory-mapped ``.pbxds`` directory format).  ``rank``/``world_size`` shard the index space for DP.
     """
 
     def __init__(self, path: str, seq_max_length: int = 128, rank: int = 0, world_size: int = 1, **kw):
@@ -97,7 +96,7 @@ class UniRefGO_StorePretrainingDataset(data.Dataset):
         return len(self.indices)
 
 
-# Reference-compatible alias; the store opens real HDF5 files when h5py is present.
+# Reference-compatible alias; the store opens the reference's HDF5 files (with or without h5py).
 UniRefGO_HDF5PretrainingDataset = UniRefGO_StorePretrainingDataset
 
 

@@ -6,9 +6,11 @@ The reference writes HDF5 with root-level datasets
     included_annotations[n_ann] str, uniprot_ids[n] str, seqs[n] str,
     seq_lengths[n] int32, annotation_masks[n, n_ann] bool
 
-h5py is not importable in this image, so two interchangeable backends exist:
+Two interchangeable backends exist:
 
-* ``.h5``     - the exact reference layout, used when h5py is importable;
+* ``.h5``     - the exact reference layout.  Read and written by h5py when it is importable,
+  otherwise by the dependency-free implementation in :mod:`.hdf5` (h5py and libhdf5 are not in
+  this image);
 * ``.pbxds``  - a directory of memory-mappable ``.npy`` arrays with the same
   fields (sequence bytes + offsets, bit-packed annotation masks).  It is what
   the native batch builder (``ops/csrc/pbx_loader.cpp``) reads without
@@ -29,11 +31,17 @@ try:  # pragma: no cover - h5py is absent in the build image
 except Exception:  # noqa: BLE001
     h5py = None
 
+from . import hdf5 as pbx_h5
+
 PBXDS_VERSION = 1
 
 
 def has_h5py() -> bool:
     return h5py is not None
+
+
+def _text(v) -> str:
+    return v.decode("utf-8") if isinstance(v, (bytes, np.bytes_)) else str(v)
 
 
 class ProteinStore:
@@ -43,9 +51,7 @@ class ProteinStore:
     def open(path: str) -> "ProteinStore":
         if os.path.isdir(path) and os.path.exists(os.path.join(path, "meta.json")):
             return PbxdsStore(path)
-        if path.endswith((".h5", ".hdf5")):
-            if h5py is None:
-                raise RuntimeError(f"{path} is HDF5 but h5py is not importable; convert it to .pbxds")
+        if path.endswith((".h5", ".hdf5")) and os.path.isfile(path):
             return H5Store(path)
         raise FileNotFoundError(f"no dataset store at {path}")
 
@@ -90,26 +96,35 @@ class PbxdsStore(ProteinStore):
         return bytes(self.id_bytes[a:b]).decode("utf-8")
 
 
-class H5Store(ProteinStore):  # pragma: no cover - needs h5py
-    def __init__(self, path: str):
-        self.f = h5py.File(path, "r")
-        self.included_annotations = [x.decode() if isinstance(x, bytes) else str(x)
-                                     for x in self.f["included_annotations"][:]]
+class H5Store(ProteinStore):
+    """The reference HDF5 layout (h5py when importable, else :class:`.hdf5.H5File` over mmap).
+
+    Fixes the reference reader's defects: root-level datasets as E3 writes them, no
+    removed ``Dataset.value`` API, a working ``__len__``."""
+
+    def __init__(self, path: str, backend: str = "auto"):
+        if backend == "auto":
+            backend = "h5py" if h5py is not None else "pbx"
+        self.backend = backend
+        self.f = h5py.File(path, "r") if backend == "h5py" else pbx_h5.H5File(path)
+        self.included_annotations = [_text(x) for x in self.f["included_annotations"][:]]
         self.n_annotations = len(self.included_annotations)
+        self._seqs, self._ids, self._masks = self.f["seqs"], self.f["uniprot_ids"], self.f["annotation_masks"]
 
     def __len__(self) -> int:
-        return int(self.f["seqs"].shape[0])
+        return int(self._seqs.shape[0])
 
     def seq(self, i: int) -> str:
-        s = self.f["seqs"][i]
-        return s.decode() if isinstance(s, bytes) else str(s)
+        return _text(self._seqs[i])
 
     def annotation_mask(self, i: int) -> np.ndarray:
-        return np.asarray(self.f["annotation_masks"][i], dtype=bool)
+        return np.array(self._masks[i], dtype=bool)
 
     def uniprot_id(self, i: int) -> str:
-        s = self.f["uniprot_ids"][i]
-        return s.decode() if isinstance(s, bytes) else str(s)
+        return _text(self._ids[i])
+
+    def close(self) -> None:
+        self.f.close()
 
 
 class ProteinStoreWriter:
@@ -125,8 +140,6 @@ class ProteinStoreWriter:
     def __init__(self, path: str, included_annotations: Sequence[str], fmt: str = "auto"):
         if fmt == "auto":
             fmt = "h5" if path.endswith((".h5", ".hdf5")) else "pbxds"
-        if fmt == "h5" and h5py is None:
-            raise RuntimeError("h5py is not importable; write the .pbxds format instead")
         self.path, self.fmt = path, fmt
         self.included_annotations = list(included_annotations)
         self.n_ann = len(self.included_annotations)
@@ -138,10 +151,8 @@ class ProteinStoreWriter:
             self._fseq = open(os.path.join(path, "seq_bytes.raw"), "wb")
             self._fid = open(os.path.join(path, "id_bytes.raw"), "wb")
             self._fbits = open(os.path.join(path, "annotation_bits.raw"), "wb")
-        else:  # pragma: no cover - needs h5py
-            self._seqs: List[bytes] = []
-            self._ids: List[bytes] = []
-            self._bits: List[np.ndarray] = []
+        else:  # streaming HDF5 writer (same layout h5py writes; no h5py needed)
+            self._h5 = pbx_h5.H5Writer(path, self.included_annotations)
 
     def append(self, uniprot_id: str, seq: str, annotation_indices: Iterable[int]) -> None:
         mask = np.zeros(self.n_ann, dtype=bool)
@@ -161,10 +172,8 @@ class ProteinStoreWriter:
             self._fseq.write(sq)
             self._fid.write(uid)
             self._fbits.write(bits.tobytes())
-        else:  # pragma: no cover
-            self._seqs.append(sq)
-            self._ids.append(uid)
-            self._bits.append(bits)
+        else:
+            self._h5.append(uniprot_id, seq, bits)
 
     def __len__(self) -> int:
         return len(self._seq_lens)
@@ -172,8 +181,8 @@ class ProteinStoreWriter:
     def close(self) -> None:
         if self.fmt == "pbxds":
             self._write_pbxds()
-        else:  # pragma: no cover
-            self._write_h5()
+        else:
+            self._h5.close()
 
     def _raw_to_npy(self, raw_name: str, npy_name: str, shape) -> None:
         raw = os.path.join(self.path, raw_name)
@@ -212,16 +221,3 @@ class ProteinStoreWriter:
         with open(os.path.join(self.path, "meta.json"), "w") as f:
             json.dump({"version": PBXDS_VERSION, "n": n, "n_annotations": self.n_ann,
                        "included_annotations": self.included_annotations}, f)
-
-    def _write_h5(self) -> None:  # pragma: no cover - needs h5py
-        n = len(self._seqs)
-        with h5py.File(self.path, "w") as f:
-            f.create_dataset("included_annotations", data=[a.encode() for a in self.included_annotations],
-                             dtype=h5py.string_dtype())
-            f.create_dataset("uniprot_ids", data=self._ids, dtype=h5py.string_dtype())
-            f.create_dataset("seqs", data=self._seqs, dtype=h5py.string_dtype())
-            f.create_dataset("seq_lengths", data=np.array([len(s) for s in self._seqs], dtype=np.int32))
-            masks = np.zeros((n, self.n_ann), dtype=bool)
-            for i, b in enumerate(self._bits):
-                masks[i] = np.unpackbits(b, bitorder="little")[:self.n_ann].astype(bool)
-            f.create_dataset("annotation_masks", data=masks, dtype=bool)

@@ -4,7 +4,7 @@ Reference: ``ProteinBERT/uniref_dataset.py`` (E1-E5) and the two CLIs ``create_u
 ``creare_uniref_h5_db.py`` (C1, C2).  CPU-only; not a performance target.  Implemented on the
 standard library (``xml.etree.ElementTree`` streaming, ``sqlite3``) plus pandas, with a native
 FASTA index reader instead of pyfaidx and the dataset written through
-:class:`..data.store.ProteinStoreWriter` (HDF5 when h5py is importable, ``.pbxds`` otherwise).
+:class:`..data.store.ProteinStoreWriter` (HDF5 for ``*.h5`` paths, ``.pbxds`` otherwise).
 """
 from .go import parse_go_annotations_meta, add_children_and_parents, index_to_all_ancestors  # noqa: F401
 from .fasta import FastaIndex  # noqa: F401

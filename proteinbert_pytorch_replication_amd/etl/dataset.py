@@ -3,8 +3,8 @@
 ``create_h5_dataset`` keeps the reference's two passes (count, then write in ``save_chunk_size``
 chunks of a seeded shuffle) and its annotation vocabulary rule (GO ids with ``count >=
 min_records_to_keep_annotation``, sorted).  The output goes through :class:`ProteinStoreWriter`:
-the reference HDF5 layout for ``*.h5`` paths when h5py is importable, the memory-mappable
-``.pbxds`` directory otherwise (which the native loader reads).
+the reference HDF5 layout for ``*.h5`` paths (h5py, or the dependency-free writer in
+``data/hdf5.py``), the memory-mappable ``.pbxds`` directory otherwise (which the native loader reads).
 """
 from __future__ import annotations
 
@@ -15,7 +15,7 @@ from typing import Dict, Iterable, Iterator, List, Optional, Sequence, Tuple
 import numpy as np
 import pandas as pd
 
-from ..data.store import ProteinStoreWriter, has_h5py
+from ..data.store import ProteinStoreWriter
 from ..utils.iteration import to_chunks
 from ..utils.log import log
 from .fasta import FastaIndex
@@ -87,7 +87,7 @@ def create_dataset_store(protein_annotations_sqlite_db_file_path: str, fasta_fil
     if verbose:
         log("Will encode the %d most common annotations." % len(common_ids))
     if fmt == "auto":
-        fmt = "h5" if output_path.endswith((".h5", ".hdf5")) and has_h5py() else "pbxds"
+        fmt = "h5" if output_path.endswith((".h5", ".hdf5")) else "pbxds"
     writer = ProteinStoreWriter(output_path, [str(a) for a in common_ids], fmt=fmt)
     it = load_seqs_and_annotations(protein_annotations_sqlite_db_file_path, fasta_file_path, shuffle=shuffle,
                                    records_limit=records_limit, verbose=verbose,
@@ -108,13 +108,9 @@ def create_h5_dataset(protein_annotations_sqlite_db_file_path: str, fasta_file_p
                       go_annotations_meta_csv_file_path: str, output_h5_file_path: str, shuffle: bool = True,
                       min_records_to_keep_annotation: int = 100, records_limit: Optional[int] = None,
                       save_chunk_size: int = 10000, verbose: bool = True, log_progress_every: int = 10000) -> int:
-    """Reference-named entry point (``uniref_dataset.py:201``).  Without h5py the store is written
-    as ``.pbxds`` next to the requested path (``<path>.pbxds`` when it ends in ``.h5``)."""
+    """Reference-named entry point (``uniref_dataset.py:201``): the reference HDF5 layout
+    (``data/hdf5.py`` writes it when h5py is not importable)."""
     out = output_h5_file_path
-    if out.endswith((".h5", ".hdf5")) and not has_h5py():
-        out = out.rsplit(".", 1)[0] + ".pbxds"
-        if verbose:
-            log("h5py unavailable: writing %s instead of %s" % (out, output_h5_file_path))
     return create_dataset_store(protein_annotations_sqlite_db_file_path, fasta_file_path,
                                 go_annotations_meta_csv_file_path, out, shuffle=shuffle,
                                 min_records_to_keep_annotation=min_records_to_keep_annotation,

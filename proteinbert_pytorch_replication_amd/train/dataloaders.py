@@ -4,8 +4,8 @@ Reference: ``create_pretrain_dataloaders`` (``ProteinBERT/utils.py:71-107``, T4)
 ``optimal_num_workers_testing`` (``utils.py:30-68``, T5).
 
 * ``create_pretrain_dataloaders(train_dir, batch_size, recursive_dir, num_workers, ...)`` finds the
-  dataset store(s) under ``train_dir`` (``.pbxds`` directories; ``.h5`` files when h5py is
-  importable) and returns a rank-sharded loader: the native C++ batch builder
+  dataset store(s) under ``train_dir`` (``.pbxds`` directories; ``.h5`` files in the reference
+  layout, read by h5py or ``data/hdf5.py``) and returns a rank-sharded loader: the native C++ batch builder
   (:class:`..data.native_loader.NativeStoreLoader`, ``num_workers`` = builder threads) for
   ``.pbxds``, otherwise a ``torch.utils.data.DataLoader`` over the store dataset with a
   :class:`..parallel.sampler.ShardedSampler`.  Several stores are chained per epoch.
@@ -25,7 +25,6 @@ from torch.utils.data import DataLoader, Dataset
 
 from ..data.datasets import UniRefGO_StorePretrainingDataset, collate_triples
 from ..data.native_loader import NativeStoreLoader, native_loader_available
-from ..data.store import has_h5py
 from ..parallel import dist as pdist
 from ..parallel.sampler import ShardedSampler
 
@@ -35,7 +34,7 @@ def find_stores(train_dir: str, recursive_dir: bool = False) -> List[str]:
         return [train_dir]
     if os.path.isfile(train_dir):
         return [train_dir]
-    pats = ["*.pbxds"] + (["*.h5", "*.hdf5"] if has_h5py() else [])
+    pats = ["*.pbxds", "*.h5", "*.hdf5"]
     out: List[str] = []
     for pat in pats:
         out += glob.glob(os.path.join(train_dir, "**", pat) if recursive_dir else os.path.join(train_dir, pat),

@@ -162,3 +162,16 @@ def test_cli_end_to_end(fixtures):
     assert [st2.uniprot_id(i) for i in range(len(st2))] == ["P1_HUMAN", "P2_HUMAN"]
     assert st2.included_annotations == ["GO:0000001", "GO:0000002", "GO:0000003", "GO:0000004"][:1] + \
         [a for a in ["GO:0000002", "GO:0000003", "GO:0000004"] if meta.loc[a, "count"] >= 3]
+    # the reference flags with an .h5 path write the reference HDF5 layout (no h5py needed)
+    out3 = tmp / "ds3.h5"
+    main_uniref_h5(["--protein-annotations-sqlite-db-file", str(db), "--protein-fasta-file", str(fasta),
+                    "--go-annotations-meta-csv-file", str(csv), "--output-h5-dataset-file", str(out3),
+                    "--min-records-to-keep-annotation", "2", "--silent", "--no-shuffle"])
+    from proteinbert_pytorch_replication_amd.data.hdf5 import H5File
+    with H5File(str(out3)) as f:
+        assert f.keys() == ["annotation_masks", "included_annotations", "seq_lengths", "seqs", "uniprot_ids"]
+        ids = [x.decode() for x in f["uniprot_ids"][:]]
+        assert sorted(ids) == sorted(got)
+        for i, uid in enumerate(ids):
+            assert f["seqs"][i].decode() == got[uid][0] and f["seq_lengths"][i] == len(got[uid][0])
+            assert f["annotation_masks"][i].tolist() == got[uid][1]
