@@ -117,6 +117,11 @@ __device__ __forceinline__ f32x2 gelu_grad2_fast(f32x2 x) {
 // ops; N interleaved chains fill those slots and the transcendental latencies.
 template <int N, bool GRAD>
 __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
+#ifdef PBX_ABL_NOGELU   // ablation builds only (tools/ubench/build_flags.sh): the cost of the GELU chains
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = x[i] * 0.5f;
+  return;
+#endif
   f32x2 ax[N], t[N], e[N], pl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -157,6 +162,14 @@ __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
 // backward) pays ~5 extra packed ops per pair instead of a second core.
 template <int N>
 __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd) {
+#ifdef PBX_ABL_NOGELU
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    g[i] = x[i] * 0.5f;
+    gd[i] = x[i] * 0.25f;
+  }
+  return;
+#endif
   f32x2 ax[N], t[N], e[N], pl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {

@@ -192,7 +192,7 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const uint4 oq = packq8(o);
     if (okl) {
       const size_t off = ((size_t)b * L + l) * CH + ch * 8;
-      *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);
+      if (pre_l != nullptr) *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);   // null: recomputed
       *reinterpret_cast<uint4*>(s2 + off) = oq;
     }
     // (sum, sum of squares) of the stored values, reduced over the wave into the LDS partial table
@@ -780,10 +780,16 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
 // affine gradients therefore accumulate in registers over every sample the workgroup sees and are
 // written once (no cross-workgroup reduction when nsplit == 1); dWl sums 32 x nsamples rows per
 // workgroup before its one atomic flush.  LN1 partials: sums1[b][pair][2].
+//
+// RECOMP: the MLP pre-activation is not read from memory but recomputed on MFMA from the h1 tile the
+// kernel builds anyway (pre = h1 Wl^T + bl, fp32): the forward then skips its [B, L, 128] pre_l store
+// and this kernel one [B, L, 128] read, for one 32x128x128 MFMA pass and two barriers per chunk.
+template <bool RECOMP>
 __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ g2,
-    const bf16_t* __restrict__ pre_l, const bf16_t* __restrict__ s1, const float* __restrict__ g1,
-    const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ consts,
+    const bf16_t* __restrict__ pre_l, const float* __restrict__ bl, const bf16_t* __restrict__ s1,
+    const float* __restrict__ g1, const float* __restrict__ be1, const bf16_t* __restrict__ wl,
+    const float* __restrict__ consts,
     bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
     float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B,
     int L) {
@@ -808,6 +814,8 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     load_f8(g1 + (size_t)l * CH + ch * 8, ga1);
     load_f8(be1 + (size_t)l * CH + ch * 8, bt1);
   }
+  float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (RECOMP) load_f8(bl + ch * 8, bb);
   float adg2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float adg1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float adbl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -819,7 +827,8 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   int bs = b0 + (j >> 1);
   bool ok = okl && bs < b1;
   size_t off = (size_t)bs * L * CH + coff;
-  uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_pr = ldq(pre_l + off, ok), n_s1 = ldq(s1 + off, ok);
+  uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_s1 = ldq(s1 + off, ok);
+  uint4 n_pr = RECOMP ? make_uint4(0u, 0u, 0u, 0u) : ldq(pre_l + off, ok);
   float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
   if (bs < b1) {
     n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
@@ -833,8 +842,54 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
     unpack8(n_dh, dh);
     unpack8(n_s2, sv2);
-    unpack8(n_pr, pr);
     unpack8(n_s1, sv1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xh2 = (sv2[e] - mean2) * rstd2;
+      adg2[e] += okc ? dh[e] * xh2 : 0.f;
+      adb2[e] += okc ? dh[e] : 0.f;
+      ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
+      xh1[e] = (sv1[e] - mean1) * rstd1;
+      hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(hv);
+    auto prefetch = [&]() {
+      bs = bc + 16 + (j >> 1);
+      ok = okl && bs < b1;
+      off = (size_t)bs * L * CH + coff;
+      n_dh = ldq(dh2 + off, ok);
+      n_s2 = ldq(s2 + off, ok);
+      if (!RECOMP) n_pr = ldq(pre_l + off, ok);
+      n_s1 = ldq(s1 + off, ok);
+      if (bs < b1) {
+        n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
+        n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+      }
+    };
+    if (RECOMP) {
+      // pre[row][co] = sum_ci h1[row][ci] Wl[co][ci] + bl[co]: the forward's MFMA, from the same
+      // bf16 h1 tile (waves 0-3, D[co][row] into the fp32 tile), while the next chunk loads
+      __syncthreads();
+      prefetch();
+      if (w < 4) {
+        f32x16_t acc = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
+              make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+      }
+      __syncthreads();
+      const float4 pa = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
+      const float4 pb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
+      const float pv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pr[e] = pv[e] + bb[e];
+    } else {
+      unpack8(n_pr, pr);
+    }
     float gp[8];
     {
       const f32x2 xi[4] = {(f32x2){pr[0], pr[1]}, (f32x2){pr[2], pr[3]}, (f32x2){pr[4], pr[5]},
@@ -848,18 +903,9 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       }
     }
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float xh2 = (sv2[e] - mean2) * rstd2;
-      adg2[e] += okc ? dh[e] * xh2 : 0.f;
-      adb2[e] += okc ? dh[e] : 0.f;
-      ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
-      dp[e] = ds2[e] * gp[e];
-      xh1[e] = (sv1[e] - mean1) * rstd1;
-      hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
-    }
+    for (int e = 0; e < 8; ++e) dp[e] = ds2[e] * gp[e];
     const uint4 dq = packq8(dp);
     *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
-    *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(hv);
     {
       float dpr[8];
       unpack8(dq, dpr);
@@ -868,17 +914,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     }
     __syncthreads();
     // prefetch the next chunk while the MFMAs run
-    bs = bc + 16 + (j >> 1);
-    ok = okl && bs < b1;
-    off = (size_t)bs * L * CH + coff;
-    n_dh = ldq(dh2 + off, ok);
-    n_s2 = ldq(s2 + off, ok);
-    n_pr = ldq(pre_l + off, ok);
-    n_s1 = ldq(s1 + off, ok);
-    if (bs < b1) {
-      n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
-      n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
-    }
+    if (!RECOMP) prefetch();
     if (w < 4) {
       // D[ci][row] = sum_co Wl[co][ci] dpre[row][co]: A = Wl^T (transposed LDS read), B = dpre rows
       f32x16_t acc = zero16();
@@ -1131,7 +1167,8 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
 }
@@ -1227,24 +1264,38 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
 
 // dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics).
 // consts: [B][8] fp32 workspace; sums1: [B][ceil(L/2)][2] LN1 partials (TS1 = ceil(L/2)).
-PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
-                                  const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
-                                  int BM1, const float* g1, const float* be1, const void* wl, float* consts,
-                                  void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
-                                  float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
+// bl != nullptr: recompute the MLP pre-activation (pre_l unused, may be null); wg_per_cu: workgroups
+// per CU to aim the (position pair, sample split) grid at (0: one)
+PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
+                                   const float* g2, const void* pre_l, const float* bl, const void* s1,
+                                   const float* st1, int T1, int BM1, const float* g1, const float* be1,
+                                   const void* wl, float* consts, void* dh1, float* sums1, float* dg2, float* db2,
+                                   float* dg1, float* db1, float* dwl, float* dbl, float* dgb_zero, int B, int L,
+                                   float eps, int wg_per_cu, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
                      consts, dgb_zero, B, L, eps);
   const int pairs = (L + 1) / 2;
-  int nsplit = (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
+  int nsplit = wg_per_cu > 0 ? (wg_per_cu * num_cus() + pairs - 1) / pairs
+                             : (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
   if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
   if (nsplit < 1) nsplit = 1;
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
-  hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(pairs, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
-                     (const bf16_t*)s2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
+  auto* k = bl != nullptr ? ln2_linear_bwd_kernel<true> : ln2_linear_bwd_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(pairs, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
+                     (const bf16_t*)s2, g2, (const bf16_t*)pre_l, bl, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
                      consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
+                                  const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
+                                  int BM1, const float* g1, const float* be1, const void* wl, float* consts,
+                                  void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
+                                  float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
+  return pbx_ln2_linear_bwd2(dh2, s2, st2, sums2, TS2, g2, pre_l, nullptr, s1, st1, T1, BM1, g1, be1, wl, consts,
+                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, B, L, eps, 0, st);
 }
 
 // dgb ([B, 128] fp32) is accumulated into

@@ -43,6 +43,8 @@ _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl, dgb
+_lib.register("pbx_ln2_linear_bwd2", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P,
+                                      _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
@@ -78,6 +80,11 @@ def attn_pool_v2(NJ: int) -> bool:
 # v3 forward tile: 128 positions (two workgroups per CU; measured faster in the full step than 256,
 # one workgroup per CU with each streamed weight fragment feeding 8 MFMAs); PBX_CONV_TILE=256 selects it
 CONV3_TILE = int(os.environ.get("PBX_CONV_TILE", "128"))
+# local-MLP pre-activation: "recompute" (the LN2/MLP backward recomputes h1 Wl^T + bl on MFMA, the
+# forward stores nothing) or "store" (forward writes it as a bf16 [B, L, 128] tensor)
+PRE_L = os.environ.get("PBX_PRE_L", "store")
+# workgroups per CU the LN2/MLP backward grid aims at (0: one)
+LN2_WG_PER_CU = int(os.environ.get("PBX_LN2_WGCU", "0"))
 
 
 def conv_tile(L: int) -> int:
@@ -206,11 +213,11 @@ class LocalBlockFn(torch.autograd.Function):
         s1 = torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
         conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
-        pre_l = torch.empty_like(x)
+        pre_l = torch.empty_like(x) if PRE_L == "store" else None
         s2 = torch.empty_like(x)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_linear_fwd", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
-                  wl_b.data_ptr(), bl.data_ptr(), pre_l.data_ptr(), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS,
+                  wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS,
                   stream)
         NJ = wv_bf16.shape[0]
         nwf = attn_fwd_waves(L)
@@ -231,7 +238,9 @@ class LocalBlockFn(torch.autograd.Function):
             _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
             hsave = h2
-        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, hsave, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
+        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l if pre_l is not None else bl, s2, st2, hsave, wtn,
+                              wtw, wl_b, wv_bf16, g1, be1, g2)
+        ctx.pre_l_stored = pre_l is not None
         ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
         ctx.set_materialize_grads(False)
         ctx.params = params
@@ -276,11 +285,13 @@ class LocalBlockFn(torch.autograd.Function):
         sums1 = torch.empty((B, TS1, 2), dtype=torch.float32, device=dev)
         consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
         dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts kernel
-        _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(), TA,
-                  g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
+        # pre_l slot: the stored pre-activation, or the MLP bias it is recomputed with
+        pre_ptr, bl_ptr = (pre_l.data_ptr(), None) if ctx.pre_l_stored else (None, pre_l.data_ptr())
+        _lib.call("pbx_ln2_linear_bwd2", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(), TA,
+                  g2.data_ptr(), pre_ptr, bl_ptr, s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, stream)
+                  dgb.data_ptr(), B, L, LN_EPS, LN2_WG_PER_CU, stream)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
         _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(), TS1,

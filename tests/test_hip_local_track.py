@@ -60,9 +60,14 @@ def test_local_block_forward(L, B):
     assert rel(vpart.sum(1), rv) < 1.5e-2
 
 
-@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1)])
-def test_local_block_backward(L, B):
+@pytest.mark.parametrize("L,B,pre_l,wgcu", [(512, 2, "store", 0), (200, 3, "store", 0), (4096, 1, "store", 0),
+                                            (512, 2, "recompute", 0), (200, 3, "recompute", 2),
+                                            (4096, 1, "recompute", 0), (300, 40, "recompute", 2)])
+def test_local_block_backward(L, B, pre_l, wgcu, monkeypatch):
+    from proteinbert_pytorch_replication_amd.ops import local_track as lt
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
+    monkeypatch.setattr(lt, "PRE_L", pre_l)            # MLP pre-activation stored, or recomputed in backward
+    monkeypatch.setattr(lt, "LN2_WG_PER_CU", wgcu)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
