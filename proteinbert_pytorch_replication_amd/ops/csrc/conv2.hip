@@ -48,7 +48,7 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
     bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
-    float* __restrict__ stats, int L, int KS, int dil) {
+    float* __restrict__ stats, float* __restrict__ colsum, int L, int KS, int dil) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
   constexpr int TOT = TBM * 256;                              // bytes of one [TBM][128] bf16 tile
@@ -74,7 +74,10 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   fr[0] = fw[lane];
   fr[1] = fw[256 + lane];
   fr[2] = fw[512 + lane];
-  if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
+  // gb == nullptr ("late gb"): s1 is stored without the broadcast global->local vector, which its
+  // consumers add (the global track of the previous block may still be running beside this kernel)
+  if (tid < 3 * CH)
+    bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : (gb != nullptr ? gb[(size_t)b * CH + tid - 2 * CH] : 0.f);
   stage_chunks(
       XR * 16,
       [&](int idx) {
@@ -141,6 +144,7 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   // plain (sum, sum of squares) of the stored bf16 values -- per row, masked once -- merged to
   // (mean, M2) by one thread at the end (the per-thread / per-lane Chan merges cost a division each)
   f32x2 s2v = {0.f, 0.f};                          // (sum, sum of squares)
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // channel sums of this thread's rows
   const float4 g0 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8);
   const float4 g1 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8 + 4);
   const f32x2 gbp[4] = {(f32x2){g0.x, g0.y}, (f32x2){g0.z, g0.w}, (f32x2){g1.x, g1.y}, (f32x2){g1.z, g1.w}};
@@ -186,13 +190,37 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       rs += (f32x2){pv.x + pv.y, pv.x * pv.x + pv.y * pv.y};
     }
     s2v += ok ? rs : (f32x2){0.f, 0.f};
+    if (colsum != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) csum[e] += ok ? orr[e] : 0.f;
+    }
   }
   float* scratch = bsm + 3 * CH;                  // 8 waves x (sum, sum of squares)
   {
     const float sa = wave_reduce_sum(s2v.x), sq = wave_reduce_sum(s2v.y);
     if (lane == 0) { scratch[2 * w] = sa; scratch[2 * w + 1] = sq; }
   }
+  float* cpart = reinterpret_cast<float*>(ot);    // [8 waves][128] channel partials (ot is free after the loop)
+  if (colsum != nullptr) {
+    // lanes l, l^16, l^32, l^48 share the 8-channel chunk (l & 15)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      csum[e] += __shfl_xor(csum[e], 16, 64);
+      csum[e] += __shfl_xor(csum[e], 32, 64);
+    }
+    __syncthreads();                              // every wave is done reading the ot tile
+    if (lane < 16) {
+      *reinterpret_cast<float4*>(cpart + w * CH + lane * 8) = make_float4(csum[0], csum[1], csum[2], csum[3]);
+      *reinterpret_cast<float4*>(cpart + w * CH + lane * 8 + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
+    }
+  }
   __syncthreads();
+  if (colsum != nullptr && tid < CH) {
+    float a = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += cpart[i * CH + tid];
+    colsum[((size_t)b * T + t) * CH + tid] = a;
+  }
   if (tid == 0) {
     float sa = 0.f, sq = 0.f;
 #pragma unroll
@@ -375,9 +403,11 @@ static void set_conv3_attrs() {
 
 // LayerNorm partials in `stats` are per tbm-position tile: [B][ceil(L/tbm)][2] (tbm = 128 or 256).  fwn/fww: forward
 // fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels.
-PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
-                             int dil, int tbm, hipStream_t st) {
+// gb may be null ("late gb": s1 without the broadcast vector); colsum (nullable): [B][ceil(L/tbm)][128]
+// channel sums of the stored s1 per tile, for the exact LayerNorm statistics once gb is known
+PBX_EXPORT int pbx_conv_fwd3x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, float* colsum, int B,
+                              int L, int KS, int dil, int tbm, hipStream_t st) {
   set_conv3_attrs();
   if (tbm != 128 && tbm != 256) return (int)hipErrorInvalidValue;
   const int lds = fwd3_lds(KS, dil, tbm);
@@ -386,12 +416,18 @@ PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, co
   if (tbm == 256)
     hipLaunchKernelGGL((conv_fwd3_kernel<256, 2>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
                        (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
-                       (bf16_t*)s1, stats, L, KS, dil);
+                       (bf16_t*)s1, stats, colsum, L, KS, dil);
   else
     hipLaunchKernelGGL((conv_fwd3_kernel<128, 4>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
                        (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
-                       (bf16_t*)s1, stats, L, KS, dil);
+                       (bf16_t*)s1, stats, colsum, L, KS, dil);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
+                             int dil, int tbm, hipStream_t st) {
+  return pbx_conv_fwd3x(x, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, nullptr, B, L, KS, dil, tbm, st);
 }
 
 PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* pre_w, const void* ftn,

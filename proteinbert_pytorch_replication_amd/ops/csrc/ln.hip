@@ -124,7 +124,8 @@ __device__ __forceinline__ void sample_stats(float* sh, const float* __restrict_
 __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
     const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ bl,
-    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, int B, int L, float eps) {
+    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, const float* __restrict__ gb,
+    const float* __restrict__ cs1, float* __restrict__ st1f, int B, int L, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* ht = smem + 32768;                                  // h1 tile bf16, PB x 256 B
@@ -141,10 +142,21 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
   const int nb = b1 - b0;
   float* part = tab + 2 * nb;
   stage_weight(ws, wl, CH);
+  // gb != nullptr ("late gb"): s1 was stored without the broadcast global->local vector; the
+  // statistics of s1 + gb come from the s1 tile partials, their channel sums cs1 and gb
   for (int i = w; i < nb; i += 8) {
     float mean, rstd;
-    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
-    if (lane == 0) { tab[2 * i] = mean; tab[2 * i + 1] = rstd; }
+    const int bi = b0 + i;
+    if (gb != nullptr)
+      wave_ln_stats_gb(st1 + (size_t)bi * T1 * 2, T1, BM1, L, cs1 + (size_t)bi * T1 * CH, gb + (size_t)bi * CH, eps,
+                       mean, rstd);
+    else
+      wave_ln_stats(st1 + (size_t)bi * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    if (lane == 0) {
+      tab[2 * i] = mean;
+      tab[2 * i + 1] = rstd;
+      if (st1f != nullptr && blockIdx.x == 0) { st1f[2 * bi] = mean; st1f[2 * bi + 1] = rstd; }
+    }
   }
   float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bb[8];
   if (okl) {
@@ -159,6 +171,12 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const float mean = tab[2 * i], rstd = tab[2 * i + 1];
     float sv[8], h1[8];
     unpack8(nxt, sv);
+    if (gb != nullptr) {
+      float gv[8];
+      load_f8(gb + (size_t)b * CH + ch * 8, gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sv[e] += gv[e];
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) h1[e] = okl ? (sv[e] - mean) * rstd * gam[e] + bet[e] : 0.f;
     *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(h1);
@@ -754,7 +772,7 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
                                                          const float* __restrict__ sums2, int TS2,
                                                          const float* __restrict__ st1, int T1, int BM1,
                                                          float* __restrict__ consts, float* __restrict__ zero128,
-                                                         int B, int L, float eps) {
+                                                         const float* __restrict__ st1f, int B, int L, float eps) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   // zero row b of the [B, 128] accumulator the LN1 finalize adds into (saves a fill launch per block)
@@ -763,7 +781,12 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
   float mean2, rstd2, m1, m2, mean1, rstd1;
   wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BM2, L, CH, eps, mean2, rstd2);
   wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, 1.0f / (float)(L * CH), m1, m2);
-  wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
+  if (st1f != nullptr) {          // final (mean, rstd) of LN1 written by the forward (late gb)
+    mean1 = st1f[2 * b];
+    rstd1 = st1f[2 * b + 1];
+  } else {
+    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
+  }
   if ((threadIdx.x & 63) == 0) {
     float4* c = reinterpret_cast<float4*>(consts + (size_t)b * 8);
     c[0] = make_float4(mean2, rstd2, m1, m2);
@@ -791,8 +814,8 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const float* __restrict__ g1, const float* __restrict__ be1, const bf16_t* __restrict__ wl,
     const float* __restrict__ consts,
     bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
-    float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B,
-    int L) {
+    float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl,
+    const float* __restrict__ gb, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16 [32][128]
@@ -829,6 +852,12 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   size_t off = (size_t)bs * L * CH + coff;
   uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_s1 = ldq(s1 + off, ok);
   uint4 n_pr = RECOMP ? make_uint4(0u, 0u, 0u, 0u) : ldq(pre_l + off, ok);
+  // late gb: s1 + gb[sample] (the forward stored s1 without the broadcast vector)
+  float4 n_g0 = make_float4(0.f, 0.f, 0.f, 0.f), n_g1 = n_g0;
+  if (gb != nullptr && bs < b1) {
+    n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
+    n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
+  }
   float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
   if (bs < b1) {
     n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
@@ -843,6 +872,11 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     unpack8(n_dh, dh);
     unpack8(n_s2, sv2);
     unpack8(n_s1, sv1);
+    {
+      const float gv[8] = {n_g0.x, n_g0.y, n_g0.z, n_g0.w, n_g1.x, n_g1.y, n_g1.z, n_g1.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sv1[e] += gv[e];
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xh2 = (sv2[e] - mean2) * rstd2;
@@ -864,6 +898,10 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       if (bs < b1) {
         n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
         n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+        if (gb != nullptr) {
+          n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
+          n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
+        }
       }
     };
     if (RECOMP) {
@@ -1012,7 +1050,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
 __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     const bf16_t* __restrict__ dh1, const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1,
     const float* __restrict__ sums1, int TS1, const float* __restrict__ g1, bf16_t* __restrict__ ds1,
-    float* __restrict__ dgb, int B, int L, float eps) {
+    float* __restrict__ dgb, const float* __restrict__ gb, const float* __restrict__ st1f, int B, int L, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem);            // 2 x [PB][CH] (double-buffered)
   float* tab = red + 2 * PB * CH;                          // [nb][4]: mean rstd m1 m2
@@ -1026,7 +1064,12 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
   const float inv_n = 1.0f / (float)(L * CH);
   for (int i = w; i < nb; i += 8) {
     float mean, rstd, m1, m2;
-    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    if (st1f != nullptr) {
+      mean = st1f[2 * (b0 + i)];
+      rstd = st1f[2 * (b0 + i) + 1];
+    } else {
+      wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    }
     wave_bwd_consts(sums1 + (size_t)(b0 + i) * TS1 * 2, TS1, inv_n, m1, m2);
     if (lane == 0) { tab[4 * i] = mean; tab[4 * i + 1] = rstd; tab[4 * i + 2] = m1; tab[4 * i + 3] = m2; }
   }
@@ -1045,6 +1088,12 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     float dv[8], sv[8], o[8];
     unpack8(n_dh, dv);
     unpack8(n_s, sv);
+    if (gb != nullptr) {          // late gb: s1 + gb[b]
+      float gv[8];
+      load_f8(gb + (size_t)b * CH + ch * 8, gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sv[e] += gv[e];
+    }
     const size_t noff = (size_t)min(b + 1, B - 1) * L * CH + coff;
     n_dh = *reinterpret_cast<const uint4*>(dh1 + noff);
     n_s = *reinterpret_cast<const uint4*>(s1 + noff);
@@ -1179,17 +1228,27 @@ static int ln_groups(int B, int L) {
   return g < 1 ? 1 : (g > B ? B : g);
 }
 
-PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int BM1, const float* g1,
-                                 const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
-                                 float* st2, int B, int L, float eps, hipStream_t st) {
+// gb/cs1 (nullable, "late gb"): s1 lacks the broadcast vector gb [B, 128]; cs1 = conv_fwd3x channel
+// sums.  st1f (nullable): final LN1 (mean, rstd) per sample, for the backward kernels.
+PBX_EXPORT int pbx_ln_linear_fwdx(const void* s1, const float* st1, int T1, int BM1, const float* g1,
+                                  const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
+                                  float* st2, const float* gb, const float* cs1, float* st1f, int B, int L, float eps,
+                                  hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
   const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
   const int lds = 32768 + PB * 256 + PB * YS * 4 + nbmax * 18 * 4;
   if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
   hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
-                     (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
+                     (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, gb, cs1, st1f, B, L, eps);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int BM1, const float* g1,
+                                 const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
+                                 float* st2, int B, int L, float eps, hipStream_t st) {
+  return pbx_ln_linear_fwdx(s1, st1, T1, BM1, g1, be1, wl, bl, pre_l, s2, st2, nullptr, nullptr, nullptr, B, L, eps,
+                            st);
 }
 
 // nw: waves per workgroup; vpart is [B][ceil(L / 64)][NJ] (one row per 64-position wave tile)
@@ -1270,12 +1329,13 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
                                    const float* g2, const void* pre_l, const float* bl, const void* s1,
                                    const float* st1, int T1, int BM1, const float* g1, const float* be1,
                                    const void* wl, float* consts, void* dh1, float* sums1, float* dg2, float* db2,
-                                   float* dg1, float* db1, float* dwl, float* dbl, float* dgb_zero, int B, int L,
-                                   float eps, int wg_per_cu, hipStream_t st) {
+                                   float* dg1, float* db1, float* dwl, float* dbl, float* dgb_zero,
+                                   const float* gb, const float* st1f, int B, int L, float eps, int wg_per_cu,
+                                   hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
-                     consts, dgb_zero, B, L, eps);
+                     consts, dgb_zero, st1f, B, L, eps);
   const int pairs = (L + 1) / 2;
   int nsplit = wg_per_cu > 0 ? (wg_per_cu * num_cus() + pairs - 1) / pairs
                              : (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
@@ -1285,7 +1345,7 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
   auto* k = bl != nullptr ? ln2_linear_bwd_kernel<true> : ln2_linear_bwd_kernel<false>;
   hipLaunchKernelGGL(k, dim3(pairs, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
                      (const bf16_t*)s2, g2, (const bf16_t*)pre_l, bl, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
-                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, B, L);
+                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, gb, B, L);
   return pbx_launch_status();
 }
 
@@ -1295,21 +1355,28 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
   return pbx_ln2_linear_bwd2(dh2, s2, st2, sums2, TS2, g2, pre_l, nullptr, s1, st1, T1, BM1, g1, be1, wl, consts,
-                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, B, L, eps, 0, st);
+                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, nullptr, nullptr, B, L, eps, 0, st);
 }
 
 // dgb ([B, 128] fp32) is accumulated into
-PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
-                                const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
-                                float eps, hipStream_t st) {
+// gb (nullable): late-gb s1 (add gb[b]); st1f (nullable): final LN1 (mean, rstd) per sample
+PBX_EXPORT int pbx_ln1_finalizex(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
+                                 const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, const float* gb,
+                                 const float* st1f, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
   const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
   const int lds = 2 * PB * CH * 4 + nbmax * 16;
   if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
   hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
-                     BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, B, L, eps);
+                     BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, gb, st1f, B, L, eps);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
+                                const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
+                                float eps, hipStream_t st) {
+  return pbx_ln1_finalizex(dh1, s1, st1, T1, BM1, sums1, TS1, g1, ds1, dgb, nullptr, nullptr, B, L, eps, st);
 }
 
 PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long rows, hipStream_t st) {

@@ -205,9 +205,14 @@ class FusedGlobalBlockFn(torch.autograd.Function):
     :class:`GlobalBlockFn`."""
 
     @staticmethod
-    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl, packed=None):
+    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl, packed=None, aux=False):
         """``packed``: the six fragment images (f1, f1T, f2, f2T, fgl, fglT) already built by
-        :func:`pack_batch` for this step, else they are built here."""
+        :func:`pack_batch` for this step, else they are built here.
+
+        ``aux``: run the kernel on the ``gfwd`` aux stream and mark the outputs ready there; every
+        main-stream consumer must call :func:`.streams.wait_ready` on them first (the late-gb local
+        block does so after launching its convolution, so that kernel overlaps this one: the global
+        track occupies 32 workgroups for ~35 us per block)."""
         dev = g.device
         B, G = g.shape
         TV = vpart.shape[1]
@@ -225,10 +230,22 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         g1_bf, g2_bf = e(B, G, dt=BF16), e(B, G, dt=BF16)
         pregl, gb = (e(B, NGL), e(B, NGL)) if NGL else (None, torch.zeros((B, 0), dtype=F32, device=dev))
         vp = vpart.contiguous()
-        _lib.call("pbx_glob_fwd", _ptrs(g.contiguous(), g_bf.contiguous(), vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
-                                        fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
-                                        gb if NGL else None),
-                  B, G, NGL, TV, K, LN_EPS, _s(dev))
+        gc, gbc = g.contiguous(), g_bf.contiguous()
+
+        def launch():
+            _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                            fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                            gb if NGL else None),
+                      B, G, NGL, TV, K, LN_EPS, _s(dev))
+
+        if aux and dev.type == "cuda":
+            # outputs were allocated on the main stream above; the aux stream starts after the main
+            # stream's work so far, and the inputs stay referenced until the end-of-step join
+            with streams.on_aux(dev, "gfwd", keep=[gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b, fgl, bgl]):
+                launch()
+            streams.mark_ready(dev, "gfwd", [g2, g2_bf, gb])
+        else:
+            launch()
         ctx.save_for_backward(g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT)
         ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
         ctx.meta = (TV, NGL)
@@ -273,7 +290,7 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         else:
             weight_grads()
         dvpart = dvs.unsqueeze(1).expand(B, TV, G)
-        return (dg, None, dvpart, *gr.finish(), None)
+        return (dg, None, dvpart, *gr.finish(), None, None)
 
 
 class GlobalBlockFn(torch.autograd.Function):
@@ -396,6 +413,8 @@ class HeadsLossFn(torch.autograd.Function):
         _lib.call("pbx_local_head", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
                   y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(),
                   dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, st)
+        # the last global block may still run on its aux stream: the local head above overlapped it
+        streams.wait_ready(g2, g2_bf)
         z = mm32(g2_bf, bf16_of(wa).t())
         dz = torch.empty((B, A), dtype=BF16, device=dev)
         dba = torch.zeros(A, dtype=F32, device=dev)

@@ -31,6 +31,9 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 _lib.register("pbx_conv_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd3x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_ln_linear_fwdx", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
+_lib.register("pbx_ln1_finalizex", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
@@ -44,7 +47,7 @@ _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, 
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl, dgb
 _lib.register("pbx_ln2_linear_bwd2", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P,
-                                      _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P])
+                                      _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
@@ -85,6 +88,16 @@ CONV3_TILE = int(os.environ.get("PBX_CONV_TILE", "128"))
 PRE_L = os.environ.get("PBX_PRE_L", "store")
 # workgroups per CU the LN2/MLP backward grid aims at (0: one)
 LN2_WG_PER_CU = int(os.environ.get("PBX_LN2_WGCU", "0"))
+# "late gb": the conv forward stores s1 WITHOUT the broadcast global->local vector gb (plus per-tile
+# channel sums), the LN1 consumers add it and correct the statistics exactly; the conv then no longer
+# waits for the previous block's global track, which runs beside it on an aux stream.  Measured 1-2 %
+# SLOWER on the B=512 L=512 step (same-box A/B, high- or normal-priority aux stream: the 32 global-track
+# workgroups find no CU with free LDS beside the convolution's), so it is opt-in.
+LATE_GB = os.environ.get("PBX_LATE_GB", "0") == "1"
+
+
+def late_gb_enabled() -> bool:
+    return LATE_GB and CONV_IMPL == "v3"
 
 
 def conv_tile(L: int) -> int:
@@ -94,11 +107,12 @@ def conv_tile(L: int) -> int:
     return 256 if L >= 256 else 128
 
 
-def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, BM, stream) -> None:
+def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, BM, stream, colsum=None) -> None:
+    """``gb`` None (v3 only): s1 without the broadcast vector, ``colsum`` [B, T, 128] its tile channel sums."""
     if CONV_IMPL == "v3":
-        _lib.call("pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
-                  gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
-                  BM, stream)
+        _lib.call("pbx_conv_fwd3x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                  _p(gb), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), _p(colsum), B, L, KS,
+                  dil, BM, stream)
     else:
         _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
                   gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
@@ -207,18 +221,28 @@ class LocalBlockFn(torch.autograd.Function):
             wpn, wtn = pack_conv(wn)
             wpw, wtw = pack_conv(ww)
         wl_b = bf16_of(wl)
-        gb = gb.detach().float().contiguous()
+        late = late_gb_enabled()
         pre_n = torch.empty_like(x)
         pre_w = torch.empty_like(x)
         s1 = torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
-        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
+        cs1 = st1f = None
+        if late:
+            # s1 without gb: the convolution does not wait for the global track producing gb
+            cs1 = torch.empty((B, T1, CH), dtype=torch.float32, device=dev)
+            st1f = torch.empty((B, 2), dtype=torch.float32, device=dev)
+            conv_fwd(x, wpn, wpw, bn, bw, None, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream, cs1)
+            streams.wait_ready(gb)
+            gb = gb.detach().float().contiguous()
+        else:
+            gb = gb.detach().float().contiguous()
+            conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
         pre_l = torch.empty_like(x) if PRE_L == "store" else None
         s2 = torch.empty_like(x)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_ln_linear_fwd", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
-                  wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS,
-                  stream)
+        _lib.call("pbx_ln_linear_fwdx", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
+                  wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), _p(gb if late else None),
+                  _p(cs1), _p(st1f), B, L, LN_EPS, stream)
         NJ = wv_bf16.shape[0]
         nwf = attn_fwd_waves(L)
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
@@ -239,7 +263,7 @@ class LocalBlockFn(torch.autograd.Function):
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, nwf, LN_EPS, stream)
             hsave = h2
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l if pre_l is not None else bl, s2, st2, hsave, wtn,
-                              wtw, wl_b, wv_bf16, g1, be1, g2)
+                              wtw, wl_b, wv_bf16, g1, be1, g2, gb if late else None, st1f)
         ctx.pre_l_stored = pre_l is not None
         ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
         ctx.set_materialize_grads(False)
@@ -250,7 +274,8 @@ class LocalBlockFn(torch.autograd.Function):
     def backward(ctx, dh2, dvpart):
         streams.wait_ready(dvpart)           # produced by the global-track backward on its aux stream
         # hs: the GELU' fragments (v2 pool) or h2 (v1 pool, recomputed projection)
-        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, hs, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, hs, wtn, wtw, wl_b, wv_bf16, g1, be1, g2, gb_late,
+         st1f) = ctx.saved_tensors
         B, L, KS, dil, BM1, T1, T2, NJ, BMV = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -291,11 +316,11 @@ class LocalBlockFn(torch.autograd.Function):
                   g2.data_ptr(), pre_ptr, bl_ptr, s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, LN2_WG_PER_CU, stream)
+                  dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, LN2_WG_PER_CU, stream)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
-        _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(), TS1,
-                  g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, stream)
+        _lib.call("pbx_ln1_finalizex", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+                  TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, stream)
         if streams.GLOBAL_ENABLED:
             # the previous block's global-track backward (next autograd node, aux stream) needs only
             # dgb: let it start here, beside the conv data gradient below

@@ -65,11 +65,24 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
         if backend == "nccl":
             kw["device_id"] = info.device
+            opts = nccl_pg_options()
+            if opts is not None:
+                kw["pg_options"] = opts
         if not dist.is_initialized():
             dist.init_process_group(**kw)
         info.backend = backend
     _INFO = info
     return info
+
+
+def nccl_pg_options():
+    """RCCL's own streams at high priority: the gradient all-reduce kernels are dispatched ahead of
+    the backward kernels they overlap.  ``PBX_RCCL_HIGH_PRIO=0`` turns it off."""
+    if os.environ.get("PBX_RCCL_HIGH_PRIO", "1") != "1" or not hasattr(dist, "ProcessGroupNCCL"):
+        return None
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return opts
 
 
 def get_info() -> DistInfo:

@@ -46,9 +46,13 @@ def torch_local(x, gb, blk):
     return h2, vsum
 
 
-@pytest.mark.parametrize("L,B", [(512, 3), (200, 2), (300, 2), (64, 4), (1024, 2), (4096, 1)])
-def test_local_block_forward(L, B):
+@pytest.mark.parametrize("L,B,late", [(512, 3, False), (200, 2, False), (300, 2, False), (64, 4, False),
+                                      (1024, 2, False), (4096, 1, False), (512, 3, True), (300, 2, True),
+                                      (4096, 1, True)])
+def test_local_block_forward(L, B, late, monkeypatch):
+    from proteinbert_pytorch_replication_amd.ops import local_track as lt
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
+    monkeypatch.setattr(lt, "LATE_GB", late)     # conv stores s1 without gb; LN1 consumers add it
     m, blk = make_block(L)
     x = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb = torch.randn(B, 128, device="cuda") * 0.5
@@ -60,14 +64,17 @@ def test_local_block_forward(L, B):
     assert rel(vpart.sum(1), rv) < 1.5e-2
 
 
-@pytest.mark.parametrize("L,B,pre_l,wgcu", [(512, 2, "store", 0), (200, 3, "store", 0), (4096, 1, "store", 0),
-                                            (512, 2, "recompute", 0), (200, 3, "recompute", 2),
-                                            (4096, 1, "recompute", 0), (300, 40, "recompute", 2)])
-def test_local_block_backward(L, B, pre_l, wgcu, monkeypatch):
+@pytest.mark.parametrize("L,B,pre_l,wgcu,late", [(512, 2, "store", 0, False), (200, 3, "store", 0, False),
+                                                 (4096, 1, "store", 0, False), (512, 2, "recompute", 0, False),
+                                                 (200, 3, "recompute", 2, False), (4096, 1, "recompute", 0, False),
+                                                 (300, 40, "recompute", 2, False), (512, 2, "store", 0, True),
+                                                 (300, 5, "recompute", 0, True), (4096, 1, "store", 0, True)])
+def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track as lt
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     monkeypatch.setattr(lt, "PRE_L", pre_l)            # MLP pre-activation stored, or recomputed in backward
     monkeypatch.setattr(lt, "LN2_WG_PER_CU", wgcu)
+    monkeypatch.setattr(lt, "LATE_GB", late)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
@@ -110,14 +117,19 @@ def test_embedding_kernels():
     assert rel(E.grad, dref) < 1e-5
 
 
-def test_full_model_loss_and_grads_vs_torch():
+@pytest.mark.parametrize("late", [False, True])
+def test_full_model_loss_and_grads_vs_torch(late, monkeypatch):
+    """late: the late-gb local blocks with every global block on its aux stream (overlapping the next
+    block's convolution and, for the last block, the local head)."""
     from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.ops import local_track as lt
+    monkeypatch.setattr(lt, "LATE_GB", late)
     from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss
     from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
     torch.manual_seed(0)
     L, A = 256, 8943
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
-                    num_blocks=2, device="cuda", backend="hip")
+                    num_blocks=3 if late else 2, device="cuda", backend="hip")
     X, Y, W = SyntheticUniRefGO(L, A, 6, "cuda", seed=3).next_batch()
     loss = fused_pretrain_loss(m, X, Y, W)
     loss.backward()
