@@ -50,6 +50,47 @@ def _gelu(x: torch.Tensor) -> torch.Tensor:
     return F.gelu(x)  # exact erf GELU == nn.GELU() default
 
 
+class GlobalAttentionHead(nn.Module):
+    """One local -> global attention head as a standalone module, reference API
+    (``modules.py:21-60``): ``Wv_parameter [C, vd]``, ``Wk_parameter [C, K]``, ``Wq_parameter [G, K]``
+    (``randn`` init), ``forward({"local": [B, L, C], "global": [B, G]}) -> [B, K, vd]``.
+
+    ``semantics="reference"``: the reference's softmax runs over the K identical query rows, so every
+    output row is exactly ``(1/K) sum_l GELU(h Wv)`` -- computed in that closed form (Q and K never
+    influence the result); :meth:`forward_faithful` is the literal computation.  ``"paper"``: one
+    query per head, softmax over positions, the ``[B, vd]`` result repeated over the K rows.
+    :class:`GlobalAttention` holds the heads of a block stacked for the fused kernels.
+    """
+
+    def __init__(self, local_dim: int, global_dim: int, value_dim: int, key_dim: int, device=None,
+                 semantics: str = "reference"):
+        super().__init__()
+        device = device or _DEFAULT_DEVICE
+        self.key_dim, self.global_dim, self.semantics = key_dim, global_dim, semantics
+        self.Wv_parameter = nn.Parameter(torch.randn(local_dim, value_dim, device=device))
+        self.Wk_parameter = nn.Parameter(torch.randn(local_dim, key_dim, device=device))
+        self.Wq_parameter = nn.Parameter(torch.randn(global_dim, key_dim, device=device))
+
+    def forward_faithful(self, x: Dict[str, torch.Tensor]) -> torch.Tensor:
+        K = self.key_dim
+        q = torch.tanh(torch.matmul(x["global"].unsqueeze(1).expand(-1, K, -1), self.Wq_parameter))
+        k = torch.tanh(torch.matmul(x["local"], self.Wk_parameter))
+        v = _gelu(torch.matmul(x["local"], self.Wv_parameter))
+        return torch.matmul(torch.softmax(torch.matmul(q, k.transpose(1, 2)) / math.sqrt(K), dim=1), v)
+
+    def forward(self, x: Dict[str, torch.Tensor]) -> torch.Tensor:
+        h, K = x["local"], self.key_dim
+        v = _gelu(torch.matmul(h, self.Wv_parameter))                                   # [B, L, vd]
+        if self.semantics == "paper":
+            q = torch.tanh(torch.matmul(x["global"], self.Wq_parameter))               # [B, K]
+            k = torch.tanh(torch.matmul(h, self.Wk_parameter))                         # [B, L, K]
+            p = torch.softmax(torch.einsum("bk,blk->bl", q, k) / math.sqrt(K), dim=-1)
+            o = torch.einsum("bl,blv->bv", p, v)
+        else:
+            o = v.sum(dim=1) / K
+        return o.unsqueeze(1).expand(-1, K, -1)
+
+
 class _HeadView:
     """Read/write view of one stacked attention head, named like the reference
     ``GlobalAttentionHead`` attributes (``modules.py:36-47``)."""

@@ -89,3 +89,26 @@ def test_loss_and_grad_parity(reference_modules):
         g_r, g_o = rp[n].grad, p.grad
         scale = g_r.abs().max().item() + 1e-12
         assert (g_o - g_r).abs().max().item() <= 1e-4 * scale + 1e-7, n
+
+
+def test_standalone_attention_head_matches_reference(reference_modules):
+    """``GlobalAttentionHead`` (reference ``modules.py:21-60``): same parameters, same [B, K, vd] output;
+    the closed form equals the literal computation, and in paper semantics every row is the
+    position-softmax single-query attention."""
+    from proteinbert_pytorch_replication_amd.models import GlobalAttentionHead
+    torch.manual_seed(3)
+    ref = reference_modules.GlobalAttentionHead(16, 32, 8, 8, device="cpu")
+    ours = GlobalAttentionHead(16, 32, 8, 8)
+    ours.load_state_dict(ref.state_dict(), strict=True)
+    x = {"local": torch.randn(3, 20, 16) * 0.3, "global": torch.randn(3, 32) * 0.3}
+    with torch.no_grad():
+        r = ref(x)
+        torch.testing.assert_close(ours(x), r, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(ours.forward_faithful(x), r, rtol=1e-5, atol=1e-6)
+        ours.semantics = "paper"
+        o = ours(x)
+        q = torch.tanh(x["global"] @ ours.Wq_parameter)
+        k = torch.tanh(x["local"] @ ours.Wk_parameter)
+        p = torch.softmax((k @ q.unsqueeze(-1)).squeeze(-1) / 8 ** 0.5, dim=-1)
+        v = torch.nn.functional.gelu(x["local"] @ ours.Wv_parameter)
+        torch.testing.assert_close(o[:, 5], (p.unsqueeze(-1) * v).sum(1), rtol=1e-5, atol=1e-6)
