@@ -372,29 +372,6 @@ __global__ void __launch_bounds__(512) local_head_mfma_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
-  const int l = blockIdx.x;
-  // h_l rows c0 .. c0 + HC - 1 -> hs (zero beyond B)
-  // All of h_l (B <= 608 rows x 256 B) is loaded into registers once, up front (<= 5 chunks x 4 x 16 B
-  // per thread): one HBM round trip instead of one per chunk and pass, and no second read for dWo.
-  constexpr int MAXC = 5;
-  uint4 hreg[MAXC][4];
-#pragma unroll
-  for (int c = 0; c < MAXC; ++c)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 512 * i;
-      const int b = c * HC + (idx >> 4);
-      hreg[c][i] = b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
-                         : make_uint4(0u, 0u, 0u, 0u);
-    }
-  // chunk c (compile-time index after unrolling) -> hs
-  auto stage_h = [&](const uint4 (&hc)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + 512 * i;
-      *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = hc[i];
-    }
-  };
   // Wo (bf16, zero rows beyond V)
   for (int idx = tid; idx < 32 * 16; idx += 512) {
     const int v = idx >> 4, c8 = idx & 15;
@@ -406,205 +383,234 @@ __global__ void __launch_bounds__(512) local_head_mfma_kernel(
     }
     *reinterpret_cast<uint4*>(wos + swz256(v, c8)) = packq8(e);
   }
-  // logits, one h chunk at a time (wave w -> row tile w of the chunk)
   const float bov = r < V ? bo[r] : 0.f;
+  // a workgroup walks positions l = blockIdx.x, + gridDim.x, ...: its dWo / dbo partials sum over them
+  // and are written once (row blockIdx.x of dwo_part / dbo_part)
+  float lsum = 0.f, dbo_acc = 0.f;
+  f32x16_t dwo_acc = zero16();
+  for (int l = blockIdx.x; l < L; l += gridDim.x) {
+    __syncthreads();                              // the previous position's dh stores read hs
+    // h_l rows c0 .. c0 + HC - 1 -> hs (zero beyond B)
+    // All of h_l (B <= 608 rows x 256 B) is loaded into registers once, up front (<= 5 chunks x 4 x 16 B
+    // per thread): one HBM round trip instead of one per chunk and pass, and no second read for dWo.
+    constexpr int MAXC = 5;
+    uint4 hreg[MAXC][4];
 #pragma unroll
-  for (int c = 0; c < MAXC; ++c) {
-    const int c0 = c * HC;
-    if (c0 >= Bp) break;
-    __syncthreads();                            // previous chunk consumed
-    stage_h(hreg[c]);
-    __syncthreads();
-    const int rt = c0 / 32 + w;
-    if (w < HC / 32 && rt < Bp / 32) {
-      f32x16_t acc = zero16();
+    for (int c = 0; c < MAXC; ++c)
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk)
-        acc = mfma32(lds_frag(hs, swz256(w * 32 + r, kk * 2 + hh)), lds_frag(wos, swz256(r, kk * 2 + hh)), acc);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int b = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
-        zs[b * 32 + r] = acc[i] + bov;
+      for (int i = 0; i < 4; ++i) {
+        const int idx = tid + 512 * i;
+        const int b = c * HC + (idx >> 4);
+        hreg[c][i] = b < B ? *reinterpret_cast<const uint4*>(h + ((size_t)b * L + l) * 128 + (idx & 15) * 8)
+                           : make_uint4(0u, 0u, 0u, 0u);
       }
-    }
-  }
-  __syncthreads();
-  // softmax over b for each v (16 partial columns per v)
-  {
-    const int v = tid & 31, part = tid >> 5;
-    float m = -3.4e38f;
-    if (v < V)
-      for (int b = part; b < B; b += 16) m = fmaxf(m, zs[b * 32 + v]);
-    red[part * 32 + v] = m;
-    __syncthreads();
-    if (tid < 32) {
-      float mm = -3.4e38f;
-      for (int k = 0; k < 16; ++k) mm = fmaxf(mm, red[k * 32 + tid]);
-      colv[32 + tid] = mm;
-    }
-    __syncthreads();
-    float sacc = 0.f;
-    if (v < V)
-      for (int b = part; b < B; b += 16) sacc += __expf(zs[b * 32 + v] - colv[32 + v]);
-    red[part * 32 + v] = sacc;
-    __syncthreads();
-    if (tid < 32) {
-      float ss = 0.f;
-      for (int k = 0; k < 16; ++k) ss += red[k * 32 + tid];
-      colv[64 + tid] = ss > 0.f ? 1.0f / ss : 0.f;
-      colv[tid] = 0.f;
-    }
-    __syncthreads();
-  }
-  for (int i = tid; i < B * 32; i += 512) {
-    const int v = i & 31;
-    zs[i] = v < V ? __expf(zs[i] - colv[32 + v]) * colv[64 + v] : 0.f;
-  }
-  __syncthreads();
-  // CE over v on the probabilities, one thread per sample: se_b = sum_v exp(P[b][v]) (P is a
-  // probability in [0, 1]: no max shift needed), loss_b = log se_b - P[b][y_b]; the per-row scalars
-  // (1/se_b, w_b/(BL), y_b) go to the free h staging tile.  G[b][v] = coef_b (exp(P)/se_b - [v==y_b]).
-  float* rsv = reinterpret_cast<float*>(hs);                  // [Bp] 1/se_b
-  float* cfv = rsv + Bp;                                      // [Bp] w_b / (B L)
-  int* ybv = reinterpret_cast<int*>(cfv + Bp);                // [Bp] y_b
-  float lsum = 0.f;
-  for (int b = tid; b < B; b += 512) {
-    const float* p = zs + b * 32;
-    float se = 0.f;
+    // chunk c (compile-time index after unrolling) -> hs
+    auto stage_h = [&](const uint4 (&hc)[4]) {
 #pragma unroll
-    for (int v4 = 0; v4 < 8; ++v4) {
-      const float4 q4 = *reinterpret_cast<const float4*>(p + 4 * v4);
-      const float pv[4] = {q4.x, q4.y, q4.z, q4.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) se += (4 * v4 + e) < V ? __expf(pv[e]) : 0.f;
-    }
-    const int yv = (int)y[(size_t)b * L + l];
-    const float wgt = wl[(size_t)b * L + l];
-    lsum += wgt * (__logf(se) - p[yv]);
-    rsv[b] = 1.0f / se;
-    cfv[b] = wgt * inv_bl;
-    ybv[b] = yv;
-  }
-  __syncthreads();
-  // colv[v] = sum_b G[b][v] P[b][v]: thread (v, part) over rows part, part + 16, ...; 16 partial
-  // columns combined in a fixed order
-  const int cv_v = tid & 31, cv_part = tid >> 5;
-  {
-    float acc = 0.f;
-    if (cv_v < V)
-      for (int b = cv_part; b < B; b += 16) {
-        const float pv = zs[b * 32 + cv_v];
-        const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
-        acc += g * pv;
+      for (int i = 0; i < 4; ++i) {
+        const int idx = tid + 512 * i;
+        *reinterpret_cast<uint4*>(hs + swz256(idx >> 4, idx & 15)) = hc[i];
       }
-    red[cv_part * 32 + cv_v] = acc;
-    __syncthreads();
-    if (tid < 32) {
-      float t = 0.f;
-      for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
-      colv[tid] = t;
-    }
-    __syncthreads();
-  }
-  // dz = P (G - colv) -> bf16 dzb for the MFMAs (zero beyond B and V) and dbo_l[v] = sum_b dz
-  {
-    float acc = 0.f;
-    const float cvv = colv[cv_v];
-    for (int b = cv_part; b < Bp; b += 16) {
-      float dz = 0.f;
-      if (b < B && cv_v < V) {
-        const float pv = zs[b * 32 + cv_v];
-        const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
-        dz = pv * (g - cvv);
-      }
-      acc += dz;
-      *reinterpret_cast<bf16_t*>(dzb + b * 64 + cv_v * 2) = f2bf(dz);
-    }
-    __syncthreads();                            // every colv / rsv read done before red is reused
-    red[cv_part * 32 + cv_v] = acc;
-    __syncthreads();
-    if (tid < V) {
-      float t = 0.f;
-      for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
-      dbo_part[(size_t)l * V + tid] = t;
-    }
-  }
-  // dWo_l: wave w -> channel tile w & 3, row half w >> 2 of each chunk (the two halves summed
-  // through LDS);  D[v][c] = sum_b dz^T[v][b] h[b][c]  (h chunks re-staged)
-  {
-    f32x16_t acc = zero16();
-    const int colb = (w & 3) * 32 + tc;
+    };
+    // logits, one h chunk at a time (wave w -> row tile w of the chunk)
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
       const int c0 = c * HC;
       if (c0 >= Bp) break;
-      __syncthreads();
+      __syncthreads();                            // previous chunk consumed
       stage_h(hreg[c]);
       __syncthreads();
-      const int nkb = min(HC, Bp - c0) / 16;
-      for (int kb = (w >> 2); kb < nkb; kb += 2) {
-        const int ra = kb * 16 + 8 * hh + q;
-        const bf16x8 fa =
-            cat_tr(lds_tr(dzb, (c0 + ra) * 64 + tc * 2), lds_tr(dzb, (c0 + ra + 4) * 64 + tc * 2));
-        const bf16x8 fb = cat_tr(lds_tr(hs, swz256e(ra, colb)), lds_tr(hs, swz256e(ra + 4, colb)));
-        acc = mfma32(fa, fb, acc);
+      const int rt = c0 / 32 + w;
+      if (w < HC / 32 && rt < Bp / 32) {
+        f32x16_t acc = zero16();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk)
+          acc = mfma32(lds_frag(hs, swz256(w * 32 + r, kk * 2 + hh)), lds_frag(wos, swz256(r, kk * 2 + hh)), acc);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int b = rt * 32 + (i & 3) + 8 * (i >> 2) + 4 * hh;
+          zs[b * 32 + r] = acc[i] + bov;
+        }
       }
     }
-    // waves 4-7 hand their half to waves 0-3 through the (free) dh staging tile
     __syncthreads();
-    float* xch = reinterpret_cast<float*>(hs);                // [4 waves][16][64 lanes] fp32 = 16 KB
-    if (w >= 4) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) xch[((w - 4) * 16 + i) * 64 + lane] = acc[i];
+    // softmax over b for each v (16 partial columns per v)
+    {
+      const int v = tid & 31, part = tid >> 5;
+      float m = -3.4e38f;
+      if (v < V)
+        for (int b = part; b < B; b += 16) m = fmaxf(m, zs[b * 32 + v]);
+      red[part * 32 + v] = m;
+      __syncthreads();
+      if (tid < 32) {
+        float mm = -3.4e38f;
+        for (int k = 0; k < 16; ++k) mm = fmaxf(mm, red[k * 32 + tid]);
+        colv[32 + tid] = mm;
+      }
+      __syncthreads();
+      float sacc = 0.f;
+      if (v < V)
+        for (int b = part; b < B; b += 16) sacc += __expf(zs[b * 32 + v] - colv[32 + v]);
+      red[part * 32 + v] = sacc;
+      __syncthreads();
+      if (tid < 32) {
+        float ss = 0.f;
+        for (int k = 0; k < 16; ++k) ss += red[k * 32 + tid];
+        colv[64 + tid] = ss > 0.f ? 1.0f / ss : 0.f;
+        colv[tid] = 0.f;
+      }
+      __syncthreads();
+    }
+    for (int i = tid; i < B * 32; i += 512) {
+      const int v = i & 31;
+      zs[i] = v < V ? __expf(zs[i] - colv[32 + v]) * colv[64 + v] : 0.f;
     }
     __syncthreads();
-    if (w < 4) {
-      float* dst = dwo_part + (size_t)l * V * 128;
+    // CE over v on the probabilities, one thread per sample: se_b = sum_v exp(P[b][v]) (P is a
+    // probability in [0, 1]: no max shift needed), loss_b = log se_b - P[b][y_b]; the per-row scalars
+    // (1/se_b, w_b/(BL), y_b) go to the free h staging tile.  G[b][v] = coef_b (exp(P)/se_b - [v==y_b]).
+    float* rsv = reinterpret_cast<float*>(hs);                  // [Bp] 1/se_b
+    float* cfv = rsv + Bp;                                      // [Bp] w_b / (B L)
+    int* ybv = reinterpret_cast<int*>(cfv + Bp);                // [Bp] y_b
+    for (int b = tid; b < B; b += 512) {
+      const float* p = zs + b * 32;
+      float se = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int v = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        if (v < V) dst[v * 128 + w * 32 + r] = acc[i] + xch[(w * 16 + i) * 64 + lane];
+      for (int v4 = 0; v4 < 8; ++v4) {
+        const float4 q4 = *reinterpret_cast<const float4*>(p + 4 * v4);
+        const float pv[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) se += (4 * v4 + e) < V ? __expf(pv[e]) : 0.f;
       }
+      const int yv = (int)y[(size_t)b * L + l];
+      const float wgt = wl[(size_t)b * L + l];
+      lsum += wgt * (__logf(se) - p[yv]);
+      rsv[b] = 1.0f / se;
+      cfv[b] = wgt * inv_bl;
+      ybv[b] = yv;
+    }
+    __syncthreads();
+    // colv[v] = sum_b G[b][v] P[b][v]: thread (v, part) over rows part, part + 16, ...; 16 partial
+    // columns combined in a fixed order
+    const int cv_v = tid & 31, cv_part = tid >> 5;
+    {
+      float acc = 0.f;
+      if (cv_v < V)
+        for (int b = cv_part; b < B; b += 16) {
+          const float pv = zs[b * 32 + cv_v];
+          const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
+          acc += g * pv;
+        }
+      red[cv_part * 32 + cv_v] = acc;
+      __syncthreads();
+      if (tid < 32) {
+        float t = 0.f;
+        for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
+        colv[tid] = t;
+      }
+      __syncthreads();
+    }
+    // dz = P (G - colv) -> bf16 dzb for the MFMAs (zero beyond B and V) and dbo_l[v] = sum_b dz
+    {
+      float acc = 0.f;
+      const float cvv = colv[cv_v];
+      for (int b = cv_part; b < Bp; b += 16) {
+        float dz = 0.f;
+        if (b < B && cv_v < V) {
+          const float pv = zs[b * 32 + cv_v];
+          const float g = cfv[b] * (__expf(pv) * rsv[b] - (cv_v == ybv[b] ? 1.f : 0.f));
+          dz = pv * (g - cvv);
+        }
+        acc += dz;
+        *reinterpret_cast<bf16_t*>(dzb + b * 64 + cv_v * 2) = f2bf(dz);
+      }
+      __syncthreads();                            // every colv / rsv read done before red is reused
+      red[cv_part * 32 + cv_v] = acc;
+      __syncthreads();
+      if (tid < V) {
+        float t = 0.f;
+        for (int k = 0; k < 16; ++k) t += red[k * 32 + tid];
+        dbo_acc += t;
+      }
+    }
+    // dWo_l: wave w -> channel tile w & 3, row half w >> 2 of each chunk (the two halves summed
+    // through LDS);  D[v][c] = sum_b dz^T[v][b] h[b][c]  (h chunks re-staged)
+    {
+      f32x16_t& acc = dwo_acc;
+      const int colb = (w & 3) * 32 + tc;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        const int c0 = c * HC;
+        if (c0 >= Bp) break;
+        __syncthreads();
+        stage_h(hreg[c]);
+        __syncthreads();
+        const int nkb = min(HC, Bp - c0) / 16;
+        for (int kb = (w >> 2); kb < nkb; kb += 2) {
+          const int ra = kb * 16 + 8 * hh + q;
+          const bf16x8 fa =
+              cat_tr(lds_tr(dzb, (c0 + ra) * 64 + tc * 2), lds_tr(dzb, (c0 + ra + 4) * 64 + tc * 2));
+          const bf16x8 fb = cat_tr(lds_tr(hs, swz256e(ra, colb)), lds_tr(hs, swz256e(ra + 4, colb)));
+          acc = mfma32(fa, fb, acc);
+        }
+      }
+    }
+    // dh: D[b][c] = sum_v dz[b][v] Wo[v][c]; per chunk: wave -> row tile, all 4 channel tiles, staged
+    // in hs for 256-B row stores
+    for (int c0 = 0; c0 < Bp; c0 += HC) {
+      __syncthreads();                            // hs free (previous chunk stored / dWo done)
+      const int rt = c0 / 32 + w;
+      if (w < HC / 32 && rt < Bp / 32) {
+      f32x16_t acc[4];
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(dzb + (rt * 32 + r) * 64 + (kk * 16 + 8 * hh) * 2);
+        const int rlo = kk * 16 + 8 * hh + q;
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const int col = ct * 32 + tc;
+          const bf16x8 fb = cat_tr(lds_tr(wos, swz256e(rlo, col)), lds_tr(wos, swz256e(rlo + 4, col)));
+          acc[ct] = mfma32(fa, fb, acc[ct]);
+        }
+      }
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int b = w * 32 + 8 * g + 4 * hh;    // chunk rows b .. b+3 (reg = 4g + e), column ct*32 + r
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            *reinterpret_cast<bf16_t*>(hs + swz256e(b + e, ct * 32 + r)) = f2bf(acc[ct][4 * g + e]);
+        }
+      }
+      __syncthreads();
+      for (int idx = tid; idx < HC * 16; idx += 512) {
+        const int b = c0 + (idx >> 4), c8 = idx & 15;
+        if (b < B)
+          *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
+              *reinterpret_cast<const uint4*>(hs + swz256(idx >> 4, c8));
+      }
+    }
+  }  // positions
+  // dWo: waves 4-7 hand their half to waves 0-3 through the (free) dh staging tile
+  __syncthreads();
+  float* xch = reinterpret_cast<float*>(hs);                  // [4 waves][16][64 lanes] fp32 = 16 KB
+  if (w >= 4) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) xch[((w - 4) * 16 + i) * 64 + lane] = dwo_acc[i];
+  }
+  __syncthreads();
+  if (w < 4) {
+    float* dst = dwo_part + (size_t)blockIdx.x * V * 128;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int v = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (v < V) dst[v * 128 + w * 32 + r] = dwo_acc[i] + xch[(w * 16 + i) * 64 + lane];
     }
   }
-  // dh: D[b][c] = sum_v dz[b][v] Wo[v][c]; per chunk: wave -> row tile, all 4 channel tiles, staged
-  // in hs for 256-B row stores
-  for (int c0 = 0; c0 < Bp; c0 += HC) {
-    __syncthreads();                            // hs free (previous chunk stored / dWo done)
-    const int rt = c0 / 32 + w;
-    if (w < HC / 32 && rt < Bp / 32) {
-    f32x16_t acc[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const bf16x8 fa = *reinterpret_cast<const bf16x8*>(dzb + (rt * 32 + r) * 64 + (kk * 16 + 8 * hh) * 2);
-      const int rlo = kk * 16 + 8 * hh + q;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const int col = ct * 32 + tc;
-        const bf16x8 fb = cat_tr(lds_tr(wos, swz256e(rlo, col)), lds_tr(wos, swz256e(rlo + 4, col)));
-        acc[ct] = mfma32(fa, fb, acc[ct]);
-      }
-    }
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int b = w * 32 + 8 * g + 4 * hh;    // chunk rows b .. b+3 (reg = 4g + e), column ct*32 + r
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          *reinterpret_cast<bf16_t*>(hs + swz256e(b + e, ct * 32 + r)) = f2bf(acc[ct][4 * g + e]);
-      }
-    }
-    __syncthreads();
-    for (int idx = tid; idx < HC * 16; idx += 512) {
-      const int b = c0 + (idx >> 4), c8 = idx & 15;
-      if (b < B)
-        *reinterpret_cast<uint4*>(dh + ((size_t)b * L + l) * 128 + c8 * 8) =
-            *reinterpret_cast<const uint4*>(hs + swz256(idx >> 4, c8));
-    }
-  }
+  if (tid < V) dbo_part[(size_t)blockIdx.x * V + tid] = dbo_acc;
   lsum = wave_reduce_sum(lsum);
   if (lane == 0) atomicAdd(loss, lsum * inv_bl);
 }
@@ -679,10 +685,11 @@ PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float*
   return pbx_launch_status();
 }
 
-// dwo_part: [L][V][128], dbo_part: [L][V] per-position partial gradients (sum over L by the caller)
-PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
-                              void* dh, float* dwo_part, float* dbo_part, float* loss, int B, int L, int V,
-                              hipStream_t st) {
+// dwo_part: [P][V][128], dbo_part: [P][V] partial gradients (summed over P rows by the caller): with
+// B <= 608 (MFMA form) P workgroups walk the positions (P <= L); the general form needs P == L
+PBX_EXPORT int pbx_local_head2(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
+                               void* dh, float* dwo_part, float* dbo_part, float* loss, int B, int L, int V, int P,
+                               hipStream_t st) {
   if (V > 32) return (int)hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
@@ -694,16 +701,23 @@ PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, c
   const int Bp = (B + 31) & ~31;
   const int lds_m = 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (16 * 32 + 96) * 4;
   if (lds_m <= 163840) {
-    hipLaunchKernelGGL(local_head_mfma_kernel, dim3(L), dim3(512), lds_m, st, (const bf16_t*)h, wo, bo,
+    if (P < 1 || P > L) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(local_head_mfma_kernel, dim3(P), dim3(512), lds_m, st, (const bf16_t*)h, wo, bo,
                        (const long long*)y, wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V,
                        1.0f / ((float)B * (float)L));
     return pbx_launch_status();
   }
   const int lds = (V * 128 + B * V + 12 * V) * 4;
-  if (lds > 163840) return (int)hipErrorInvalidValue;
+  if (lds > 163840 || P != L) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(local_head_kernel, dim3(L), dim3(256), lds, st, (const bf16_t*)h, wo, bo, (const long long*)y,
                      wl, (bf16_t*)dh, dwo_part, dbo_part, loss, B, L, V, 1.0f / ((float)B * (float)L));
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_local_head(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
+                              void* dh, float* dwo_part, float* dbo_part, float* loss, int B, int L, int V,
+                              hipStream_t st) {
+  return pbx_local_head2(h, wo, bo, y, wl, dh, dwo_part, dbo_part, loss, B, L, V, L, st);
 }
 
 PBX_EXPORT int pbx_go_head(const float* z, const float* bias, const float* y, const float* w, long wsr, long wsc,

@@ -825,203 +825,207 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int j = tid >> 4, ch = tid & 15;
-  const int l = blockIdx.x * 2 + (j & 1);
-  const bool okl = l < L;
-  const int TS1 = gridDim.x;
+  const int TS1 = (L + 1) / 2;                      // position pairs (LN1 partials per sample)
   const int nsplit = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nsplit), b1 = (int)((long)B * (blockIdx.y + 1) / nsplit);
   stage_weight(ws, wl, CH);
-  float ga2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (okl) {
-    load_f8(g2 + (size_t)l * CH + ch * 8, ga2);
-    load_f8(g1 + (size_t)l * CH + ch * 8, ga1);
-    load_f8(be1 + (size_t)l * CH + ch * 8, bt1);
-  }
   float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (RECOMP) load_f8(bl + ch * 8, bb);
-  float adg2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  float adg1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   float adbl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  // dWl accumulators: wave w owns co tile (w >> 1) and ci tiles 2 (w & 1) + {0, 1}
+  // dWl accumulators: wave w owns co tile (w >> 1) and ci tiles 2 (w & 1) + {0, 1}; they sum over every
+  // pair the workgroup walks (long sequences: fewer workgroups than pairs, so fewer dWl flushes)
   f32x16_t aw0 = zero16(), aw1 = zero16();
   const int wco = (w >> 1) * 32, wci = (w & 1) * 64;
-  const size_t coff = (size_t)l * CH + ch * 8;
-  // prefetch the first chunk
-  int bs = b0 + (j >> 1);
-  bool ok = okl && bs < b1;
-  size_t off = (size_t)bs * L * CH + coff;
-  uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_s1 = ldq(s1 + off, ok);
-  uint4 n_pr = RECOMP ? make_uint4(0u, 0u, 0u, 0u) : ldq(pre_l + off, ok);
-  // late gb: s1 + gb[sample] (the forward stored s1 without the broadcast vector)
-  float4 n_g0 = make_float4(0.f, 0.f, 0.f, 0.f), n_g1 = n_g0;
-  if (gb != nullptr && bs < b1) {
-    n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
-    n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
-  }
-  float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
-  if (bs < b1) {
-    n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
-    n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
-  }
-  for (int bc = b0; bc < b1; bc += 16) {
-    const int bcur = bs;
-    const bool okc = ok;
-    const size_t offc = off;
-    const float mean2 = n_c0.x, rstd2 = n_c0.y, m1 = n_c0.z, m2 = n_c0.w, mean1 = n_c1.x, rstd1 = n_c1.y;
-    float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
-    unpack8(n_dh, dh);
-    unpack8(n_s2, sv2);
-    unpack8(n_s1, sv1);
-    {
-      const float gv[8] = {n_g0.x, n_g0.y, n_g0.z, n_g0.w, n_g1.x, n_g1.y, n_g1.z, n_g1.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sv1[e] += gv[e];
+  for (int pair = blockIdx.x; pair < TS1; pair += gridDim.x) {
+    const int l = pair * 2 + (j & 1);
+    const bool okl = l < L;
+    float ga2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, ga1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bt1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (okl) {
+      load_f8(g2 + (size_t)l * CH + ch * 8, ga2);
+      load_f8(g1 + (size_t)l * CH + ch * 8, ga1);
+      load_f8(be1 + (size_t)l * CH + ch * 8, bt1);
     }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float xh2 = (sv2[e] - mean2) * rstd2;
-      adg2[e] += okc ? dh[e] * xh2 : 0.f;
-      adb2[e] += okc ? dh[e] : 0.f;
-      ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
-      xh1[e] = (sv1[e] - mean1) * rstd1;
-      hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
+    float adg2[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    float adg1[8] = {0, 0, 0, 0, 0, 0, 0, 0}, adb1[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const size_t coff = (size_t)l * CH + ch * 8;
+    // prefetch the first chunk
+    int bs = b0 + (j >> 1);
+    bool ok = okl && bs < b1;
+    size_t off = (size_t)bs * L * CH + coff;
+    uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_s1 = ldq(s1 + off, ok);
+    uint4 n_pr = RECOMP ? make_uint4(0u, 0u, 0u, 0u) : ldq(pre_l + off, ok);
+    // late gb: s1 + gb[sample] (the forward stored s1 without the broadcast vector)
+    float4 n_g0 = make_float4(0.f, 0.f, 0.f, 0.f), n_g1 = n_g0;
+    if (gb != nullptr && bs < b1) {
+      n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
+      n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
     }
-    *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(hv);
-    auto prefetch = [&]() {
-      bs = bc + 16 + (j >> 1);
-      ok = okl && bs < b1;
-      off = (size_t)bs * L * CH + coff;
-      n_dh = ldq(dh2 + off, ok);
-      n_s2 = ldq(s2 + off, ok);
-      if (!RECOMP) n_pr = ldq(pre_l + off, ok);
-      n_s1 = ldq(s1 + off, ok);
-      if (bs < b1) {
-        n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
-        n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
-        if (gb != nullptr) {
-          n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
-          n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
+    float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
+    if (bs < b1) {
+      n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
+      n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+    }
+    for (int bc = b0; bc < b1; bc += 16) {
+      const int bcur = bs;
+      const bool okc = ok;
+      const size_t offc = off;
+      const float mean2 = n_c0.x, rstd2 = n_c0.y, m1 = n_c0.z, m2 = n_c0.w, mean1 = n_c1.x, rstd1 = n_c1.y;
+      float dh[8], sv2[8], pr[8], sv1[8], ds2[8], dp[8], xh1[8], hv[8];
+      unpack8(n_dh, dh);
+      unpack8(n_s2, sv2);
+      unpack8(n_s1, sv1);
+      {
+        const float gv[8] = {n_g0.x, n_g0.y, n_g0.z, n_g0.w, n_g1.x, n_g1.y, n_g1.z, n_g1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sv1[e] += gv[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh2 = (sv2[e] - mean2) * rstd2;
+        adg2[e] += okc ? dh[e] * xh2 : 0.f;
+        adb2[e] += okc ? dh[e] : 0.f;
+        ds2[e] = okc ? rstd2 * (dh[e] * ga2[e] - m1 - xh2 * m2) : 0.f;
+        xh1[e] = (sv1[e] - mean1) * rstd1;
+        hv[e] = okc ? xh1[e] * ga1[e] + bt1[e] : 0.f;
+      }
+      *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(hv);
+      auto prefetch = [&]() {
+        bs = bc + 16 + (j >> 1);
+        ok = okl && bs < b1;
+        off = (size_t)bs * L * CH + coff;
+        n_dh = ldq(dh2 + off, ok);
+        n_s2 = ldq(s2 + off, ok);
+        if (!RECOMP) n_pr = ldq(pre_l + off, ok);
+        n_s1 = ldq(s1 + off, ok);
+        if (bs < b1) {
+          n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
+          n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
+          if (gb != nullptr) {
+            n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
+            n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
+          }
+        }
+      };
+      if (RECOMP) {
+        // pre[row][co] = sum_ci h1[row][ci] Wl[co][ci] + bl[co]: the forward's MFMA, from the same
+        // bf16 h1 tile (waves 0-3, D[co][row] into the fp32 tile), while the next chunk loads
+        __syncthreads();
+        prefetch();
+        if (w < 4) {
+          f32x16_t acc = zero16();
+#pragma unroll
+          for (int kk = 0; kk < 8; ++kk)
+            acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
+#pragma unroll
+          for (int g = 0; g < 4; ++g)
+            *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
+                make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
+        }
+        __syncthreads();
+        const float4 pa = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
+        const float4 pb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
+        const float pv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) pr[e] = pv[e] + bb[e];
+      } else {
+        unpack8(n_pr, pr);
+      }
+      float gp[8];
+      {
+        const f32x2 xi[4] = {(f32x2){pr[0], pr[1]}, (f32x2){pr[2], pr[3]}, (f32x2){pr[4], pr[5]},
+                             (f32x2){pr[6], pr[7]}};
+        f32x2 go[4];
+        gelu2_fast_n<4, true>(xi, go);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          gp[2 * e] = go[e].x;
+          gp[2 * e + 1] = go[e].y;
         }
       }
-    };
-    if (RECOMP) {
-      // pre[row][co] = sum_ci h1[row][ci] Wl[co][ci] + bl[co]: the forward's MFMA, from the same
-      // bf16 h1 tile (waves 0-3, D[co][row] into the fp32 tile), while the next chunk loads
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dp[e] = ds2[e] * gp[e];
+      const uint4 dq = packq8(dp);
+      *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
+      {
+        float dpr[8];
+        unpack8(dq, dpr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) adbl[e] += dpr[e];
+      }
       __syncthreads();
-      prefetch();
+      // prefetch the next chunk while the MFMAs run
+      if (!RECOMP) prefetch();
       if (w < 4) {
+        // D[ci][row] = sum_co Wl[co][ci] dpre[row][co]: A = Wl^T (transposed LDS read), B = dpre rows
         f32x16_t acc = zero16();
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk)
-          acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
+        for (int kk = 0; kk < 8; ++kk) {
+          const int rlo = kk * 16 + 8 * h + q;
+          const int col = w * 32 + tc;
+          const bf16x8 fa = cat_tr(lds_tr(ws, swz256e(rlo, col)), lds_tr(ws, swz256e(rlo + 4, col)));
+          acc = mfma32(fa, lds_frag(dt, swz256(r, kk * 2 + h)), acc);
+        }
 #pragma unroll
         for (int g = 0; g < 4; ++g)
           *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
               make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
       }
+      // dWl[co][ci] += sum_row dpre[row][co] h1[row][ci]   (both operands transposed LDS reads)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int rlo = ks * 16 + 8 * h + q;
+        const bf16x8 fa = cat_tr(lds_tr(dt, swz256e(rlo, wco + tc)), lds_tr(dt, swz256e(rlo + 4, wco + tc)));
+        const bf16x8 fb0 = cat_tr(lds_tr(ht, swz256e(rlo, wci + tc)), lds_tr(ht, swz256e(rlo + 4, wci + tc)));
+        const bf16x8 fb1 =
+            cat_tr(lds_tr(ht, swz256e(rlo, wci + 32 + tc)), lds_tr(ht, swz256e(rlo + 4, wci + 32 + tc)));
+        aw0 = mfma32(fa, fb0, aw0);
+        aw1 = mfma32(fa, fb1, aw1);
+      }
       __syncthreads();
-      const float4 pa = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
-      const float4 pb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
-      const float pv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
+      const float4 ya = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
+      const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
+      const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
+      float o[8], sa = 0.f, sc = 0.f;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pr[e] = pv[e] + bb[e];
-    } else {
-      unpack8(n_pr, pr);
-    }
-    float gp[8];
-    {
-      const f32x2 xi[4] = {(f32x2){pr[0], pr[1]}, (f32x2){pr[2], pr[3]}, (f32x2){pr[4], pr[5]},
-                           (f32x2){pr[6], pr[7]}};
-      f32x2 go[4];
-      gelu2_fast_n<4, true>(xi, go);
+      for (int e = 0; e < 8; ++e) {
+        o[e] = okc ? bfround(ds2[e] + yv[e]) : 0.f;
+        const float dxh = o[e] * ga1[e];
+        sa += dxh;
+        sc += dxh * xh1[e];
+        adg1[e] += o[e] * xh1[e];
+        adb1[e] += o[e];
+      }
+      if (okc) *reinterpret_cast<uint4*>(dh1 + offc) = packq8(o);
+      // LN1 partial of (sample, position pair): 16 lanes per row, rows j and j+1 share the sample
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        gp[2 * e] = go[e].x;
-        gp[2 * e + 1] = go[e].y;
+      for (int m = 1; m <= 16; m <<= 1) {
+        sa += __shfl_xor(sa, m, 64);
+        sc += __shfl_xor(sc, m, 64);
+      }
+      if ((lane & 31) == 0 && bcur < b1) {
+        sums1[((size_t)bcur * TS1 + pair) * 2] = sa;
+        sums1[((size_t)bcur * TS1 + pair) * 2 + 1] = sc;
       }
     }
+    // [L, C] affine gradients: sum the 16 rows of each position through LDS, one add per element
+    const int l0 = pair * 2;
+    float* accs[4] = {adg2, adb2, adg1, adb1};
+    float* dsts[4] = {dg2, db2, dg1, db1};
 #pragma unroll
-    for (int e = 0; e < 8; ++e) dp[e] = ds2[e] * gp[e];
-    const uint4 dq = packq8(dp);
-    *reinterpret_cast<uint4*>(dt + swz256(j, ch)) = dq;
-    {
-      float dpr[8];
-      unpack8(dq, dpr);
+    for (int a = 0; a < 4; ++a) {
+      __syncthreads();
 #pragma unroll
-      for (int e = 0; e < 8; ++e) adbl[e] += dpr[e];
-    }
-    __syncthreads();
-    // prefetch the next chunk while the MFMAs run
-    if (!RECOMP) prefetch();
-    if (w < 4) {
-      // D[ci][row] = sum_co Wl[co][ci] dpre[row][co]: A = Wl^T (transposed LDS read), B = dpre rows
-      f32x16_t acc = zero16();
+      for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = accs[a][e];
+      __syncthreads();
+      if (tid < 2 * CH) {
+        const int par = tid >> 7, c = tid & (CH - 1);
+        float v = 0.f;
 #pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int rlo = kk * 16 + 8 * h + q;
-        const int col = w * 32 + tc;
-        const bf16x8 fa = cat_tr(lds_tr(ws, swz256e(rlo, col)), lds_tr(ws, swz256e(rlo + 4, col)));
-        acc = mfma32(fa, lds_frag(dt, swz256(r, kk * 2 + h)), acc);
+        for (int k = 0; k < 16; ++k) v += yt[(2 * k + par) * CH + c];
+        if (l0 + par < L) atomicAdd(dsts[a] + (size_t)(l0 + par) * CH + c, v);
       }
-#pragma unroll
-      for (int g = 0; g < 4; ++g)
-        *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
-            make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
     }
-    // dWl[co][ci] += sum_row dpre[row][co] h1[row][ci]   (both operands transposed LDS reads)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int rlo = ks * 16 + 8 * h + q;
-      const bf16x8 fa = cat_tr(lds_tr(dt, swz256e(rlo, wco + tc)), lds_tr(dt, swz256e(rlo + 4, wco + tc)));
-      const bf16x8 fb0 = cat_tr(lds_tr(ht, swz256e(rlo, wci + tc)), lds_tr(ht, swz256e(rlo + 4, wci + tc)));
-      const bf16x8 fb1 =
-          cat_tr(lds_tr(ht, swz256e(rlo, wci + 32 + tc)), lds_tr(ht, swz256e(rlo + 4, wci + 32 + tc)));
-      aw0 = mfma32(fa, fb0, aw0);
-      aw1 = mfma32(fa, fb1, aw1);
-    }
-    __syncthreads();
-    const float4 ya = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
-    const float4 yb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
-    const float yv[8] = {ya.x, ya.y, ya.z, ya.w, yb.x, yb.y, yb.z, yb.w};
-    float o[8], sa = 0.f, sc = 0.f;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      o[e] = okc ? bfround(ds2[e] + yv[e]) : 0.f;
-      const float dxh = o[e] * ga1[e];
-      sa += dxh;
-      sc += dxh * xh1[e];
-      adg1[e] += o[e] * xh1[e];
-      adb1[e] += o[e];
-    }
-    if (okc) *reinterpret_cast<uint4*>(dh1 + offc) = packq8(o);
-    // LN1 partial of (sample, position pair): 16 lanes per row, rows j and j+1 share the sample
-#pragma unroll
-    for (int m = 1; m <= 16; m <<= 1) {
-      sa += __shfl_xor(sa, m, 64);
-      sc += __shfl_xor(sc, m, 64);
-    }
-    if ((lane & 31) == 0 && bcur < b1) {
-      sums1[((size_t)bcur * TS1 + blockIdx.x) * 2] = sa;
-      sums1[((size_t)bcur * TS1 + blockIdx.x) * 2 + 1] = sc;
-    }
-  }
-  // [L, C] affine gradients: sum the 16 rows of each position through LDS, one add per element
-  const int l0 = blockIdx.x * 2;
-  float* accs[4] = {adg2, adb2, adg1, adb1};
-  float* dsts[4] = {dg2, db2, dg1, db1};
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    __syncthreads();
-#pragma unroll
-    for (int e = 0; e < 8; ++e) yt[j * CH + ch * 8 + e] = accs[a][e];
-    __syncthreads();
-    if (tid < 2 * CH) {
-      const int par = tid >> 7, c = tid & (CH - 1);
-      float v = 0.f;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) v += yt[(2 * k + par) * CH + c];
-      if (l0 + par < L) atomicAdd(dsts[a] + (size_t)(l0 + par) * CH + c, v);
-    }
+    __syncthreads();                                // yt reads done before the next pair's MFMA writes
   }
   // local-MLP bias: column sums over all rows
   __syncthreads();
@@ -1337,13 +1341,16 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
                      consts, dgb_zero, st1f, B, L, eps);
   const int pairs = (L + 1) / 2;
-  int nsplit = wg_per_cu > 0 ? (wg_per_cu * num_cus() + pairs - 1) / pairs
-                             : (num_cus() + pairs - 1) / pairs;     // at least one workgroup per CU
+  const int target = (wg_per_cu > 0 ? wg_per_cu : 1) * num_cus();
+  int nsplit = (target + pairs - 1) / pairs;        // at least one workgroup per CU
   if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
   if (nsplit < 1) nsplit = 1;
+  // long sequences: one workgroup walks several position pairs (its dWl partial is flushed once; at
+  // L = 4096 one workgroup per pair made 33 M float atomics on the 16 K dWl elements)
+  const int gx = pairs < target ? pairs : target;
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
   auto* k = bl != nullptr ? ln2_linear_bwd_kernel<true> : ln2_linear_bwd_kernel<false>;
-  hipLaunchKernelGGL(k, dim3(pairs, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
+  hipLaunchKernelGGL(k, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
                      (const bf16_t*)s2, g2, (const bf16_t*)pre_l, bl, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
                      consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, gb, B, L);
   return pbx_launch_status();

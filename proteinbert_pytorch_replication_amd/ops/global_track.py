@@ -28,6 +28,16 @@ _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_local_head2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+
+
+def local_head_parts(B: int, L: int, dev) -> int:
+    """Partial-gradient rows of the local-head kernel (``csrc/glob.hip`` pbx_local_head2): one per
+    workgroup of the MFMA form (2 workgroups per CU walk the positions), else one per position."""
+    Bp = (B + 31) // 32 * 32
+    if 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (16 * 32 + 96) * 4 > 163840:
+        return L
+    return min(L, 2 * torch.cuda.get_device_properties(dev).multi_processor_count)
 _lib.register("pbx_go_head", [_P, _P, _P, _P, ctypes.c_long, ctypes.c_long, _P, _P, _P, _I, _I, _P])
 
 _lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
@@ -229,14 +239,18 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         r1, r2 = e(B), e(B)
         g1_bf, g2_bf = e(B, G, dt=BF16), e(B, G, dt=BF16)
         pregl, gb = (e(B, NGL), e(B, NGL)) if NGL else (None, torch.zeros((B, 0), dtype=F32, device=dev))
-        vp = vpart.contiguous()
+        vp, TVk = vpart.contiguous(), TV
+        if TV >= 16:
+            # long sequences: the attention-pool tile partials are summed by the whole chip first (the
+            # fused kernel has only B / 16 workgroups; at L = 4096 each would stream 64 tile rows)
+            vp, TVk = vp.sum(dim=1, keepdim=True), 1
         gc, gbc = g.contiguous(), g_bf.contiguous()
 
         def launch():
             _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
                                             fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
                                             gb if NGL else None),
-                      B, G, NGL, TV, K, LN_EPS, _s(dev))
+                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
 
         if aux and dev.type == "cuda":
             # outputs were allocated on the main stream above; the aux stream starts after the main
@@ -408,11 +422,12 @@ class HeadsLossFn(torch.autograd.Function):
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
         dh = torch.empty_like(h)
-        dwo_part = torch.empty((L, V, C), dtype=F32, device=dev)
-        dbo_part = torch.empty((L, V), dtype=F32, device=dev)
-        _lib.call("pbx_local_head", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
+        P = local_head_parts(B, L, dev)
+        dwo_part = torch.empty((P, V, C), dtype=F32, device=dev)
+        dbo_part = torch.empty((P, V), dtype=F32, device=dev)
+        _lib.call("pbx_local_head2", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
                   y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(),
-                  dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, st)
+                  dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, P, st)
         # the last global block may still run on its aux stream: the local head above overlapped it
         streams.wait_ready(g2, g2_bf)
         z = mm32(g2_bf, bf16_of(wa).t())

@@ -10,11 +10,12 @@ from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("B", [6, 100, 200, 512, 640])
-def test_heads_loss_matches_torch(B):
+@pytest.mark.parametrize("B,L", [(6, 24), (100, 24), (200, 24), (512, 24), (640, 24), (6, 1100), (40, 2000)])
+def test_heads_loss_matches_torch(B, L):
+    """L > 2 x CUs: each local-head workgroup walks several positions (its dWo partial sums them)."""
     from proteinbert_pytorch_replication_amd.ops.global_track import HeadsLossFn
     torch.manual_seed(B)
-    L, A, G = 24, 96, 256
+    A, G = 96, 256
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=G, key_dim=64, num_heads=4,
                     num_blocks=1, device="cuda", backend="hip")
     h = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16).requires_grad_(True)
