@@ -82,7 +82,12 @@ class ProteinBERTForTokenClassification(_FinetuneBase):
 
     def forward(self, x: Inputs) -> torch.Tensor:
         h, g = self._encode(x)
-        logits = F.linear(self.dropout(h.float()), self.head.weight, self.head.bias)        # [B, L, K]
+        from ..ops import finetune_head
+        if finetune_head.supported(h, self.n_classes) and isinstance(self.dropout, nn.Identity):
+            # bf16 GEMM on the encoder output + streaming weight-gradient kernel (ops/finetune_head.py)
+            logits = finetune_head.TokenHeadFn.apply(h, self.head.weight, self.head.bias)
+        else:
+            logits = F.linear(self.dropout(h.float()), self.head.weight, self.head.bias)    # [B, L, K]
         if self.global_head is not None:
             logits = logits + self.global_head(g.float()).unsqueeze(1)
         return logits.permute(0, 2, 1)                                                   # [B, K, L]

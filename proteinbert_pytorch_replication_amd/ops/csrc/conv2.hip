@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
     const uint4 pnq = *reinterpret_cast<const uint4*>(ot + swz256(row, c));
     const uint4 pwq = *reinterpret_cast<const uint4*>(smem + swz256(row, c));
     const size_t off = ((size_t)b * L + pos0 + row) * CH + c * 8;
-    if (ok) {
+    if (ok && pre_n != nullptr) {                  // null: no backward will read them (inference)
       *reinterpret_cast<uint4*>(pre_n + off) = pnq;
       *reinterpret_cast<uint4*>(pre_w + off) = pwq;
     }

@@ -1060,11 +1060,10 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
   float* tab = red + 2 * PB * CH;                          // [nb][4]: mean rstd m1 m2
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int j = tid >> 4, ch = tid & 15;
-  const int l0 = blockIdx.x * PB, l = l0 + j;
-  const bool okl = l < L;
   const int nbg = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
   const int nb = b1 - b0;
+  float* dacc = tab + 4 * nb;                              // [nb][CH] dgb partial over the walked tiles
   const float inv_n = 1.0f / (float)(L * CH);
   for (int i = w; i < nb; i += 8) {
     float mean, rstd, m1, m2;
@@ -1077,53 +1076,64 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     wave_bwd_consts(sums1 + (size_t)(b0 + i) * TS1 * 2, TS1, inv_n, m1, m2);
     if (lane == 0) { tab[4 * i] = mean; tab[4 * i + 1] = rstd; tab[4 * i + 2] = m1; tab[4 * i + 3] = m2; }
   }
-  float ga[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (okl) load_f8(g1 + (size_t)l * CH + ch * 8, ga);
-  // loads from a clamped valid row (masked at use): a select on the load becomes a branch around
-  // it, and the wait for it a vmcnt(0)
-  const size_t coff = (size_t)min(l, L - 1) * CH + ch * 8;
-  uint4 n_dh = *reinterpret_cast<const uint4*>(dh1 + (size_t)min(b0, B - 1) * L * CH + coff);
-  uint4 n_s = *reinterpret_cast<const uint4*>(s1 + (size_t)min(b0, B - 1) * L * CH + coff);
-  __syncthreads();
-  for (int b = b0; b < b1; ++b) {
-    const float* tb = tab + 4 * (b - b0);
-    const float mean = tb[0], rstd = tb[1], m1 = tb[2], m2 = tb[3];
-    float* rb = red + ((b - b0) & 1) * PB * CH;
-    float dv[8], sv[8], o[8];
-    unpack8(n_dh, dv);
-    unpack8(n_s, sv);
-    if (gb != nullptr) {          // late gb: s1 + gb[b]
-      float gv[8];
-      load_f8(gb + (size_t)b * CH + ch * 8, gv);
+  for (int i = tid; i < nb * CH; i += 512) dacc[i] = 0.f;
+  // a workgroup walks position tiles blockIdx.x, + gridDim.x, ... (long sequences): its dgb partial
+  // sums them in LDS and is flushed once (one atomic per (sample, channel) and workgroup)
+  const int TP = (L + PB - 1) / PB;
+  int it = 0;                                              // red double-buffer parity across tiles
+  for (int px = blockIdx.x; px < TP; px += gridDim.x) {
+    const int l = px * PB + j;
+    const bool okl = l < L;
+    float ga[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (okl) load_f8(g1 + (size_t)l * CH + ch * 8, ga);
+    // loads from a clamped valid row (masked at use): a select on the load becomes a branch around
+    // it, and the wait for it a vmcnt(0)
+    const size_t coff = (size_t)min(l, L - 1) * CH + ch * 8;
+    uint4 n_dh = *reinterpret_cast<const uint4*>(dh1 + (size_t)min(b0, B - 1) * L * CH + coff);
+    uint4 n_s = *reinterpret_cast<const uint4*>(s1 + (size_t)min(b0, B - 1) * L * CH + coff);
+    __syncthreads();
+    for (int b = b0; b < b1; ++b, ++it) {
+      const float* tb = tab + 4 * (b - b0);
+      const float mean = tb[0], rstd = tb[1], m1 = tb[2], m2 = tb[3];
+      float* rb = red + (it & 1) * PB * CH;
+      float dv[8], sv[8], o[8];
+      unpack8(n_dh, dv);
+      unpack8(n_s, sv);
+      if (gb != nullptr) {          // late gb: s1 + gb[b]
+        float gv[8];
+        load_f8(gb + (size_t)b * CH + ch * 8, gv);
 #pragma unroll
-      for (int e = 0; e < 8; ++e) sv[e] += gv[e];
-    }
-    const size_t noff = (size_t)min(b + 1, B - 1) * L * CH + coff;
-    n_dh = *reinterpret_cast<const uint4*>(dh1 + noff);
-    n_s = *reinterpret_cast<const uint4*>(s1 + noff);
+        for (int e = 0; e < 8; ++e) sv[e] += gv[e];
+      }
+      const size_t noff = (size_t)min(b + 1, B - 1) * L * CH + coff;
+      n_dh = *reinterpret_cast<const uint4*>(dh1 + noff);
+      n_s = *reinterpret_cast<const uint4*>(s1 + noff);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = okl ? rstd * (dv[e] * ga[e] - m1 - (sv[e] - mean) * rstd * m2) : 0.f;
-    const uint4 qv = packq8(o);
-    if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + (size_t)l * CH + ch * 8) = qv;
-    // dgb column sums: the wave's 4 rows by shuffles, one [128] partial per wave, 8 adds per channel
-    unpack8(qv, o);
+      for (int e = 0; e < 8; ++e) o[e] = okl ? rstd * (dv[e] * ga[e] - m1 - (sv[e] - mean) * rstd * m2) : 0.f;
+      const uint4 qv = packq8(o);
+      if (okl) *reinterpret_cast<uint4*>(ds1 + (size_t)b * L * CH + (size_t)l * CH + ch * 8) = qv;
+      // dgb column sums: the wave's 4 rows by shuffles, one [128] partial per wave, 8 adds per channel
+      unpack8(qv, o);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      o[e] += __shfl_xor(o[e], 16, 64);
-      o[e] += __shfl_xor(o[e], 32, 64);
-    }
-    if (lane < 16) {
-      *reinterpret_cast<float4*>(rb + w * CH + ch * 8) = make_float4(o[0], o[1], o[2], o[3]);
-      *reinterpret_cast<float4*>(rb + w * CH + ch * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
-    }
-    __syncthreads();   // (double buffer: the next sample writes the other half)
-    if (tid < CH) {
-      float a = 0.f;
+      for (int e = 0; e < 8; ++e) {
+        o[e] += __shfl_xor(o[e], 16, 64);
+        o[e] += __shfl_xor(o[e], 32, 64);
+      }
+      if (lane < 16) {
+        *reinterpret_cast<float4*>(rb + w * CH + ch * 8) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(rb + w * CH + ch * 8 + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      }
+      __syncthreads();   // (double buffer: the next sample writes the other half)
+      if (tid < CH) {
+        float a = 0.f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a += rb[k * CH + tid];
-      atomicAdd(dgb + (size_t)b * CH + tid, a);
+        for (int k = 0; k < 8; ++k) a += rb[k * CH + tid];
+        dacc[(b - b0) * CH + tid] += a;
+      }
     }
   }
+  __syncthreads();
+  for (int i = tid; i < nb * CH; i += 512) atomicAdd(dgb + (size_t)(b0 + i / CH) * CH + i % CH, dacc[i]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1370,9 +1380,14 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
 PBX_EXPORT int pbx_ln1_finalizex(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
                                  const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, const float* gb,
                                  const float* st1f, int B, int L, float eps, hipStream_t st) {
-  dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
+  // at most 16 position tiles across x (a workgroup walks the rest), ~2 workgroups per CU overall
+  const int tp = (L + PB - 1) / PB;
+  const int gx = tp < 16 ? tp : 16;
+  int gy = (2 * num_cus() + gx - 1) / gx;
+  gy = gy < 1 ? 1 : (gy > B ? B : gy);
+  dim3 grid(gx, gy);
   const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
-  const int lds = 2 * PB * CH * 4 + nbmax * 16;
+  const int lds = 2 * PB * CH * 4 + nbmax * 16 + nbmax * CH * 4;
   if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
   hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,

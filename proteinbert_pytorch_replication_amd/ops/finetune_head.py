@@ -1,0 +1,54 @@
+"""Per-residue fine-tuning head on MI355X (BASELINE cfg 5).
+
+``logits = h Wᵀ + b`` over ``[B*L, 128]`` bf16 encoder rows and K <= 16 classes: the forward is one
+bf16 hipBLASLt GEMM (22 us at B*L = 262,144 vs 75 us for the fp32 ``F.linear`` on an upcast copy);
+the weight gradient, a 262,144-long reduction that hipBLASLt ran at 230-410 us, is the streaming
+kernel in ``csrc/finetune.hip`` (fp32 accumulation, deterministic slab reduction).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from . import global_track  # noqa: F401  (registers pbx_colsum_add)
+
+_P, _I, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
+_lib.register("pbx_token_head_wgrad", [_P, _P, _P, _L, _I, _I, _P])
+
+
+def supported(h: torch.Tensor, n_classes: int) -> bool:
+    return h.is_cuda and h.dtype == torch.bfloat16 and h.shape[-1] == 128 and n_classes <= 16
+
+
+class TokenHeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, bias):
+        B, L, C = h.shape
+        h2 = h.contiguous().view(B * L, C)
+        logits = torch.mm(h2, weight.to(torch.bfloat16).t()).float() + bias
+        ctx.save_for_backward(h2, weight)
+        ctx.shape = (B, L)
+        return logits.view(B, L, -1)
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        h2, weight = ctx.saved_tensors
+        B, L = ctx.shape
+        K = weight.shape[0]
+        g = dlogits.reshape(B * L, K).float().contiguous()
+        dh = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dh = torch.mm(g.to(torch.bfloat16), weight.to(torch.bfloat16)).view(B, L, -1)
+        if ctx.needs_input_grad[1]:
+            M = B * L
+            P = max(1, min(2 * torch.cuda.get_device_properties(h2.device).multi_processor_count, (M + 15) // 16))
+            slab = torch.empty((P, K, h2.shape[1]), dtype=torch.float32, device=h2.device)
+            st = _lib.stream_ptr(h2.device)
+            _lib.call("pbx_token_head_wgrad", h2.data_ptr(), g.data_ptr(), slab.data_ptr(), M, K, P, st)
+            dw = torch.zeros_like(weight)
+            _lib.call("pbx_colsum_add", slab.data_ptr(), P, K * h2.shape[1], dw.data_ptr(), None, st)
+        if ctx.needs_input_grad[2]:
+            db = g.sum(dim=0)
+        return dh, dw, db

@@ -108,12 +108,15 @@ def conv_tile(L: int) -> int:
 
 
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, BM, stream, colsum=None) -> None:
-    """``gb`` None (v3 only): s1 without the broadcast vector, ``colsum`` [B, T, 128] its tile channel sums."""
+    """``gb`` None (v3 only): s1 without the broadcast vector, ``colsum`` [B, T, 128] its tile channel sums;
+    ``pre_n``/``pre_w`` None (v3 only): the pre-activations are not stored (no backward)."""
     if CONV_IMPL == "v3":
         _lib.call("pbx_conv_fwd3x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
-                  _p(gb), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), _p(colsum), B, L, KS,
+                  _p(gb), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), _p(colsum), B, L, KS,
                   dil, BM, stream)
     else:
+        if pre_n is None:
+            pre_n, pre_w = torch.empty_like(x), torch.empty_like(x)
         _lib.call("pbx_conv_fwd", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
                   gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil,
                   BM, stream)
@@ -222,8 +225,11 @@ class LocalBlockFn(torch.autograd.Function):
             wpw, wtw = pack_conv(ww)
         wl_b = bf16_of(wl)
         late = late_gb_enabled()
-        pre_n = torch.empty_like(x)
-        pre_w = torch.empty_like(x)
+        # inference / frozen-encoder forwards keep no backward state: the conv pre-activations, the MLP
+        # pre-activation and the pool's GELU' fragments are not written at all
+        need_bwd = any(ctx.needs_input_grad)
+        pre_n = torch.empty_like(x) if need_bwd else None
+        pre_w = torch.empty_like(x) if need_bwd else None
         s1 = torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
         cs1 = st1f = None
@@ -237,7 +243,7 @@ class LocalBlockFn(torch.autograd.Function):
         else:
             gb = gb.detach().float().contiguous()
             conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
-        pre_l = torch.empty_like(x) if PRE_L == "store" else None
+        pre_l = torch.empty_like(x) if PRE_L == "store" and need_bwd else None
         s2 = torch.empty_like(x)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_linear_fwdx", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
@@ -249,7 +255,6 @@ class LocalBlockFn(torch.autograd.Function):
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
         # the GELU' fragments only serve a backward pass: inference / frozen-encoder forwards skip them
-        need_bwd = any(ctx.needs_input_grad)
         ctx.pool_v2 = attn_pool_v2(NJ) and need_bwd
         if ctx.pool_v2:
             # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]

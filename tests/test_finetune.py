@@ -82,3 +82,27 @@ def test_hip_encoder_finetune_matches_torch_encoder():
     tl, _ = train_step(m2, [(X, y)], torch.nn.CrossEntropyLoss(ignore_index=-100), opt, {}, True, 1.0, "cuda")
     assert tl == tl
     assert enc.proteinBERT_blocks[0].local_narrow_conv_layer[0].weight.grad.abs().sum() > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,K", [(3, 1000, 8), (5, 333, 13), (64, 512, 3)])
+def test_token_head_kernel_matches_fp32(B, L, K):
+    """ops/finetune_head.py: bf16 GEMM forward + csrc/finetune.hip weight-gradient kernel vs fp32."""
+    from proteinbert_pytorch_replication_amd.ops.finetune_head import TokenHeadFn
+    torch.manual_seed(K)
+    h = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16).requires_grad_(True)
+    w = (torch.randn(K, 128, device="cuda") * 0.1).requires_grad_(True)
+    b = torch.randn(K, device="cuda").requires_grad_(True)
+    dl = torch.randn(B, L, K, device="cuda")
+    out = TokenHeadFn.apply(h, w, b)
+    (out * dl).sum().backward()
+    hr = h.detach().float().requires_grad_(True)
+    wr, br = w.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    ref = torch.nn.functional.linear(hr, wr, br)
+    (ref * dl).sum().backward()
+    torch.cuda.synchronize()
+    rel = lambda a, r: ((a.float() - r).norm() / r.norm()).item()  # noqa: E731
+    assert rel(out, ref) < 1e-2
+    assert rel(w.grad, wr.grad) < 1e-5          # fp32 accumulation over the B*L rows
+    assert rel(b.grad, br.grad) < 1e-5
+    assert rel(h.grad, hr.grad) < 1e-2
