@@ -1,7 +1,7 @@
 # Round-end style check: full GPU test suite, smoke, headline bench and the other BASELINE configs.
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/full_gpu_tests.log 2>&1 || { tail -40 gpurun_out/full_gpu_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/full_gpu_tests.log 2>&1 || { tail -40 gpurun_out/full_gpu_tests.log; exit 1; }
 tail -3 gpurun_out/full_gpu_tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/full_smoke.log 2>&1 || { tail -20 gpurun_out/full_smoke.log; exit 1; }
 timeout -k 10 300 python -u bench.py > gpurun_out/full_bench_l512.json 2> gpurun_out/full_bench_l512.err || exit 1
