@@ -815,7 +815,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const float* __restrict__ consts,
     bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
     float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl,
-    const float* __restrict__ gb, int B, int L) {
+    const float* __restrict__ gb, float* __restrict__ dwl_slab, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16 [32][128]
@@ -1038,12 +1038,20 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     for (int k = 0; k < 32; ++k) a += yt[k * CH + tid];
     atomicAdd(dbl + tid, a);
   }
-  // local-MLP weight: D[co][ci], lane -> ci (128 contiguous bytes per half-wave)
+  // local-MLP weight: D[co][ci], lane -> ci (128 contiguous bytes per half-wave).  dwl_slab: this
+  // workgroup's partial goes to its own slab row (folded by one column-sum pass) instead of 16 K float
+  // atomics on the same 16 K addresses from every workgroup
+  float* dw = dwl_slab != nullptr ? dwl_slab + (size_t)(blockIdx.y * gridDim.x + blockIdx.x) * CH * CH : dwl;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int co = wco + (i & 3) + 8 * (i >> 2) + 4 * h;
-    atomicAdd(dwl + (size_t)co * CH + wci + r, aw0[i]);
-    atomicAdd(dwl + (size_t)co * CH + wci + 32 + r, aw1[i]);
+    if (dwl_slab != nullptr) {
+      dw[(size_t)co * CH + wci + r] = aw0[i];
+      dw[(size_t)co * CH + wci + 32 + r] = aw1[i];
+    } else {
+      atomicAdd(dw + (size_t)co * CH + wci + r, aw0[i]);
+      atomicAdd(dw + (size_t)co * CH + wci + 32 + r, aw1[i]);
+    }
   }
 }
 
@@ -1218,6 +1226,8 @@ int persistent_grid(int tiles, int per_cu) {
 }
 }  // namespace
 
+extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st);
+
 static bool ln_attrs_set = false;
 static void set_ln_attrs() {
   if (ln_attrs_set) return;
@@ -1345,7 +1355,7 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
                                    const void* wl, float* consts, void* dh1, float* sums1, float* dg2, float* db2,
                                    float* dg1, float* db1, float* dwl, float* dbl, float* dgb_zero,
                                    const float* gb, const float* st1f, int B, int L, float eps, int wg_per_cu,
-                                   hipStream_t st) {
+                                   float* dwl_slab, int slab_rows, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
@@ -1360,9 +1370,17 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
   const int gx = pairs < target ? pairs : target;
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
   auto* k = bl != nullptr ? ln2_linear_bwd_kernel<true> : ln2_linear_bwd_kernel<false>;
+  // dWl partials: one slab row per workgroup when the caller's slab is large enough, else atomics
+  const int nwg = gx * nsplit;
+  float* slab = dwl_slab != nullptr && nwg <= slab_rows ? dwl_slab : nullptr;
   hipLaunchKernelGGL(k, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
                      (const bf16_t*)s2, g2, (const bf16_t*)pre_l, bl, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
-                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, gb, B, L);
+                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, gb, slab, B, L);
+  if (slab != nullptr) {
+    const int rc = pbx_launch_status();
+    if (rc != 0) return rc;
+    return pbx_colsum_add(slab, nwg, CH * CH, dwl, nullptr, st);
+  }
   return pbx_launch_status();
 }
 
@@ -1372,7 +1390,8 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
   return pbx_ln2_linear_bwd2(dh2, s2, st2, sums2, TS2, g2, pre_l, nullptr, s1, st1, T1, BM1, g1, be1, wl, consts,
-                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, nullptr, nullptr, B, L, eps, 0, st);
+                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, nullptr, nullptr, B, L, eps, 0,
+                             nullptr, 0, st);
 }
 
 // dgb ([B, 128] fp32) is accumulated into

@@ -202,8 +202,8 @@ __global__ void __launch_bounds__(512) pc_ln_linear_bwd_kernel(
     const float4* __restrict__ stats, const float* __restrict__ g1, const float* __restrict__ be1,
     const bf16_t* __restrict__ wl, const float* __restrict__ bl, const float* __restrict__ g2,
     bf16_t* __restrict__ ds1, float* __restrict__ dgbp, float* __restrict__ dg2, float* __restrict__ db2,
-    float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl, int B,
-    int L) {
+    float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl,
+    float* __restrict__ dwl_slab, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;
   unsigned char* ht = smem + 32768;
@@ -373,11 +373,18 @@ __global__ void __launch_bounds__(512) pc_ln_linear_bwd_kernel(
       atomicAdd(dsts[a] + tid, v);
     }
   }
+  // dwl_slab: one slab row per workgroup (folded by a column-sum pass), not 16 K contended atomics
+  float* dw = dwl_slab != nullptr ? dwl_slab + (size_t)blockIdx.x * CH * CH : dwl;
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int co = wco + (i & 3) + 8 * (i >> 2) + 4 * h;
-    atomicAdd(dwl + (size_t)co * CH + wci + r, aw0[i]);
-    atomicAdd(dwl + (size_t)co * CH + wci + 32 + r, aw1[i]);
+    if (dwl_slab != nullptr) {
+      dw[(size_t)co * CH + wci + r] = aw0[i];
+      dw[(size_t)co * CH + wci + 32 + r] = aw1[i];
+    } else {
+      atomicAdd(dw + (size_t)co * CH + wci + r, aw0[i]);
+      atomicAdd(dw + (size_t)co * CH + wci + 32 + r, aw1[i]);
+    }
   }
 }
 
@@ -399,6 +406,8 @@ int pc_grid(long items) {
 }
 }  // namespace
 
+extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st);
+
 // s1/h2 [B, L, 128] bf16; g1/be1/g2/be2/bl [128] fp32; wl [128, 128] bf16 (torch Linear layout);
 // stats [B*L] float4 (mean1, rstd1, mean2, rstd2)
 PBX_EXPORT int pbx_pc_ln_linear_fwd(const void* s1, const float* g1, const float* be1, const void* wl, const float* bl,
@@ -418,12 +427,19 @@ PBX_EXPORT int pbx_pc_ln_linear_bwd(const void* dh2a, const void* dh2b, const vo
                                     const void* stats,
                                     const float* g1, const float* be1, const void* wl, const float* bl, const float* g2,
                                     void* ds1, float* dgbp, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
-                                    float* dbl, int B, int L, hipStream_t st) {
+                                    float* dbl, float* dwl_slab, int slab_rows, int B, int L, hipStream_t st) {
   if (B <= 0 || L <= 0) return (int)hipErrorInvalidValue;
   const long items = (long)B * ((L + TR - 1) / TR);
   const int lds = 32768 + 2 * TR * 256 + TR * YS * 4;
-  hipLaunchKernelGGL(pc_ln_linear_bwd_kernel, dim3(pc_grid(items)), dim3(512), lds, st, (const bf16_t*)dh2a,
+  const int grid = pc_grid(items);
+  float* slab = dwl_slab != nullptr && grid <= slab_rows ? dwl_slab : nullptr;
+  hipLaunchKernelGGL(pc_ln_linear_bwd_kernel, dim3(grid), dim3(512), lds, st, (const bf16_t*)dh2a,
                      (const bf16_t*)dh2b, (const bf16_t*)dh2c, (const bf16_t*)s1, (const float4*)stats, g1, be1, (const bf16_t*)wl, bl, g2,
-                     (bf16_t*)ds1, dgbp, dg2, db2, dg1, db1, dwl, dbl, B, L);
+                     (bf16_t*)ds1, dgbp, dg2, db2, dg1, db1, dwl, dbl, slab, B, L);
+  if (slab != nullptr) {
+    const int rc = pbx_launch_status();
+    if (rc != 0) return rc;
+    return pbx_colsum_add(slab, grid, CH * CH, dwl, nullptr, st);
+  }
   return pbx_launch_status();
 }

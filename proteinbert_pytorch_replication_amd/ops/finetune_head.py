@@ -27,7 +27,7 @@ class TokenHeadFn(torch.autograd.Function):
     def forward(ctx, h, weight, bias):
         B, L, C = h.shape
         h2 = h.contiguous().view(B * L, C)
-        logits = torch.mm(h2, weight.to(torch.bfloat16).t()).float() + bias
+        logits = torch.addmm(bias.float(), h2, weight.to(torch.bfloat16).t(), out_dtype=torch.float32)
         ctx.save_for_backward(h2, weight)
         ctx.shape = (B, L)
         return logits.view(B, L, -1)

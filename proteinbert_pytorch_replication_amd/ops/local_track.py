@@ -47,7 +47,7 @@ _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, 
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P])  # ..wl, consts, dh1, sums1, dg2..dbl, dgb
 _lib.register("pbx_ln2_linear_bwd2", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P,
-                                      _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P])
+                                      _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _I, _P, _I, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
@@ -144,6 +144,25 @@ def attn_bwd_waves(L: int) -> int:
 
 def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
+
+
+_DWL_SLAB: Dict[int, torch.Tensor] = {}
+DWL_SLAB = os.environ.get("PBX_DWL_SLAB", "1") == "1"
+
+
+def dwl_slab(dev: torch.device) -> Tuple[Optional[int], int]:
+    """(pointer, rows) of a per-device [2 x CUs, 128, 128] fp32 scratch slab for the local-MLP weight
+    gradient partials of the LayerNorm/MLP backward kernels (one row per workgroup, folded by one
+    column-sum launch; the kernels fall back to float atomics when it is absent or too small).  The
+    kernels run on one stream in order, so one slab per device is reused by every block."""
+    if not DWL_SLAB:
+        return None, 0
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _DWL_SLAB.get(idx)
+    if s is None:
+        s = torch.empty((2 * _num_cus(dev), CH, CH), dtype=torch.float32, device=dev)
+        _DWL_SLAB[idx] = s
+    return s.data_ptr(), s.shape[0]
 
 
 def _num_cus(dev: torch.device) -> int:
@@ -321,7 +340,7 @@ class LocalBlockFn(torch.autograd.Function):
                   g2.data_ptr(), pre_ptr, bl_ptr, s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, LN2_WG_PER_CU, stream)
+                  dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, LN2_WG_PER_CU, *dwl_slab(dev), stream)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
         _lib.call("pbx_ln1_finalizex", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),

@@ -26,12 +26,12 @@ import torch
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
 from .global_track import BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, mm32, addmm_into
-from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, pack_conv, _grad_dst, _wgrad
+from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_pc_ln_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
-                                       _P, _I, _I, _P])
+                                       _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_pa_fused_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 
@@ -179,7 +179,7 @@ class PaperBlockFn(torch.autograd.Function):
                   s1.data_ptr(), stats.data_ptr(),
                   g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(),
                   dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
-                  dbl.data_ptr(), B, L, stream)
+                  dbl.data_ptr(), *dwl_slab(dev), B, L, stream)
         dgb = dgbp.sum(dim=1)
         if streams.GLOBAL_ENABLED:
             streams.fork(dev, "global")

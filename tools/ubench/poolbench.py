@@ -78,7 +78,7 @@ for recomp in (False, True):
         us = timeit(lambda: _lib.call("pbx_ln2_linear_bwd2", P(dh2), P(s2), P(st2), P(sums2), T2, P(g2),
                                       None if recomp else P(pre_l), P(bl) if recomp else None, P(x), P(st1), T1,
                                       128, P(g1), P(be1), P(wl), P(consts), P(dh1), P(sums1), *[P(t) for t in acc],
-                                      P(dwl), P(dbl), P(dgb), None, None, B, L, 1e-5, wgcu, st))
+                                      P(dwl), P(dbl), P(dgb), None, None, B, L, 1e-5, wgcu, None, 0, st))
         print(f"ln2_linear_bwd recompute={recomp} wg/cu={wgcu}: {us:8.1f} us", flush=True)
 ds1 = torch.empty_like(x)
 us = timeit(lambda: _lib.call("pbx_ln1_finalize", P(dh1), P(x), P(st1), T1, 128, P(sums1), TS1, P(g1), P(ds1),
