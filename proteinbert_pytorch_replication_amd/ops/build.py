@@ -55,8 +55,12 @@ def _run(cmd: List[str], verbose: bool) -> None:
 
 
 def hip_flags() -> List[str]:
+    # -fno-slp-vectorize: the SLP vectoriser packs adjacent scalar f32 ops into v_pk_*_f32, which cost
+    # more than their scalar halves beside in-flight MFMAs on gfx950; explicitly packed code (f32x2
+    # GELU cores of the VALU-bound pool epilogue) stays packed.  +1.4 % on the step, same-box A/B
+    # (tools/gpu_scalar_ab.sh, profiles/r2_v8_scalar_ab.txt).
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-            "-ffp-contract=fast", "-Wno-unused-result", "-I", CSRC]
+            "-ffp-contract=fast", "-fno-slp-vectorize", "-Wno-unused-result", "-I", CSRC]
 
 
 def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:

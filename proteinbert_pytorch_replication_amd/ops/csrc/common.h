@@ -112,6 +112,51 @@ __device__ __forceinline__ f32x2 gelu_grad2_fast(f32x2 x) {
   return __builtin_elementwise_fma(x * 0.3989422804014327f, e, sh + 0.5f);
 }
 
+// Scalar form of the interleaved cores below: the same A&S stages on 2N independent scalars, one
+// v_fma_f32 per value per stage.  Beside in-flight MFMAs a v_pk_*_f32 costs far more than its two
+// scalar halves (MI355X_MICROARCH.md constants table), and these cores run in the shadow of the MFMAs
+// of the next tile.  (Needs -fno-slp-vectorize, or the SLP vectoriser packs the halves again.)
+template <int N, int MODE>   // MODE 0: GELU, 1: GELU', 2: both (g and gd)
+__device__ __forceinline__ void gelu_scalar_n(const f32x2* x, f32x2* g, f32x2* gd) {
+  constexpr int M = 2 * N;
+  float xs[M], ax[M], t[M], e[M], pl[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    xs[i] = (i & 1) ? x[i >> 1].y : x[i >> 1].x;
+    ax[i] = fabsf(xs[i]);
+    t[i] = fmaf(ax[i], 0.23164190f, 1.0f);
+    e[i] = (xs[i] * -0.72134752044448170f) * xs[i];
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    t[i] = __builtin_amdgcn_rcpf(t[i]);
+    e[i] = __builtin_amdgcn_exp2f(e[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], -0.5307027145f, 0.7265760135f);
+#pragma unroll
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], -0.7107068705f);
+#pragma unroll
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], 0.142248368f);
+#pragma unroll
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], -0.127414796f);
+#pragma unroll
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(pl[i] * t[i], e[i], 0.5f);   // h
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    float gv = 0.f, dv = 0.f;
+    if (MODE != 1) gv = fmaf(ax[i], pl[i], xs[i] * 0.5f);
+    if (MODE != 0) dv = fmaf(xs[i] * 0.3989422804014327f, e[i], copysignf(pl[i], xs[i]) + 0.5f);
+    if (i & 1) {
+      if (MODE != 1) g[i >> 1].y = gv;
+      if (MODE != 0) gd[i >> 1].y = dv;
+    } else {
+      if (MODE != 1) g[i >> 1].x = gv;
+      if (MODE != 0) gd[i >> 1].x = dv;
+    }
+  }
+}
+
 // N independent pairs evaluated stage by stage (every stage of all N before the next): the
 // one-pair forms above compile to a serial dependency chain with an s_nop between dependent packed
 // ops; N interleaved chains fill those slots and the transcendental latencies.
@@ -120,6 +165,11 @@ __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
 #ifdef PBX_ABL_NOGELU   // ablation builds only (tools/ubench/build_flags.sh): the cost of the GELU chains
 #pragma unroll
   for (int i = 0; i < N; ++i) out[i] = x[i] * 0.5f;
+  return;
+#endif
+#ifdef PBX_SCALAR_GELU
+  if (GRAD) gelu_scalar_n<N, 1>(x, nullptr, out);
+  else gelu_scalar_n<N, 0>(x, out, nullptr);
   return;
 #endif
   f32x2 ax[N], t[N], e[N], pl[N];
@@ -168,6 +218,10 @@ __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd
     g[i] = x[i] * 0.5f;
     gd[i] = x[i] * 0.25f;
   }
+  return;
+#endif
+#ifdef PBX_SCALAR_GELU
+  gelu_scalar_n<N, 2>(x, g, gd);
   return;
 #endif
   f32x2 ax[N], t[N], e[N], pl[N];

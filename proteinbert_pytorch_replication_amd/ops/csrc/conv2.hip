@@ -170,8 +170,10 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       gi[e] = (f32x2){pn[2 * e], pn[2 * e + 1]};
       gi[4 + e] = (f32x2){pw[2 * e], pw[2 * e + 1]};
     }
-    gelu2_fast_n<4, false>(gi, go);
-    gelu2_fast_n<4, false>(gi + 4, go + 4);
+    // scalar A&S stages (gelu_scalar_n): this epilogue runs beside the other waves' MFMAs, where the
+    // packed form measured 3 % slower on the kernel (tools/gpu_scalar_ab.sh)
+    gelu_scalar_n<4, 0>(gi, go, nullptr);
+    gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
     float o[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {

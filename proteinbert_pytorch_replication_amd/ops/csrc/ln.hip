@@ -568,6 +568,9 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
         for (int s = 0; s < 2; ++s) {
           const int rlo = 16 * s + 4 * h + q;
           const bf16x8 f = cat_tr(lds_tr(gt, rlo * GT_STRIDE + tc * 2), lds_tr(gt, (rlo + 8) * GT_STRIDE + tc * 2));
+#ifdef PBX_ABL_NOGSTORE   // ablation builds only: the cost of the GELU' fragment stores (B > 0 always)
+          if (B < 0)
+#endif
           gdst[((size_t)pt * NJT * 2 + jt * 2 + s) * 64] = f;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
