@@ -235,10 +235,19 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // data gradient: D[ci][pos] = sum_conv sum_tap sum_co W[co][ci][tap] * dpre_conv[pos - shift][co]
+//
+// LNIN (reference semantics): the kernel's `ds1` argument is dh1, the gradient at the LayerNorm-1 OUTPUT,
+// and the LN1 backward runs here, in the prologue (halo rows included) and again in the epilogue:
+//   ds1 = rstd1 (dh1 g1 - m1 - xhat1 m2),  xhat1 = (s1 - mean1) rstd1,   c1[b] = (mean1, rstd1, m1, m2)
+// (pbx_ln1_consts), and the epilogue adds the tile's sum_l ds1 into dgb[b] (gradient of the broadcast
+// global->local vector, modules.py:208-211).  This replaces the separate LN1-finalize pass, which read
+// dh1 and s1 and wrote ds1 only for this kernel to read it back (3 x [B, L, 128] bf16 per block).
+template <bool LNIN>
 __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
-    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ pre_n, const bf16_t* __restrict__ pre_w,
-    const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
+    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ s1, const float* __restrict__ g1,
+    const float* __restrict__ c1, float* __restrict__ dgb, const bf16_t* __restrict__ pre_n,
+    const bf16_t* __restrict__ pre_w, const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw,
+    bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = (L + BM - 1) / BM;
   const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
@@ -258,6 +267,16 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   fr[0] = fw[lane];
   fr[1] = fw[256 + lane];
   fr[2] = fw[512 + lane];
+  float4 lnc = make_float4(0.f, 0.f, 0.f, 0.f);      // (mean1, rstd1, m1, m2) of sample b
+  if (LNIN) lnc = *reinterpret_cast<const float4*>(c1 + (size_t)b * 4);
+  // LN1 backward of one 8-channel chunk: g = dh1 on entry, ds1 on exit (sq: s1 chunk, ga: g1 chunk)
+  auto ln1_bwd8 = [&](float* g, const uint4& sq, const float4& ga0, const float4& ga1) {
+    float sv[8];
+    unpack8(sq, sv);
+    const float gam[8] = {ga0.x, ga0.y, ga0.z, ga0.w, ga1.x, ga1.y, ga1.z, ga1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] = lnc.y * (g[e] * gam[e] - lnc.z - (sv[e] - lnc.x) * lnc.y * lnc.w);
+  };
 
   // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
 #pragma unroll 1
@@ -268,7 +287,8 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     unsigned char* tile = c ? aw : an;
     const int nch = (BM + 2 * halo) * 16;
     for (int base = tid; base < nch; base += 2 * 512) {
-      uint4 gq[2], pq[2];
+      uint4 gq[2], pq[2], sq[2];
+      float4 ga[2][2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int idx = base + i * 512;
@@ -277,6 +297,13 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         const size_t off = sbase + (size_t)pos * CH + (idx & 15) * 8;
         gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
         pq[i] = ok ? *reinterpret_cast<const uint4*>(pre + off) : make_uint4(0u, 0u, 0u, 0u);
+        if (LNIN) {
+          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+          const float* gp = g1 + (size_t)min(max(pos, 0), L - 1) * CH + (idx & 15) * 8;
+          sq[i] = ok ? *reinterpret_cast<const uint4*>(s1 + off) : make_uint4(0u, 0u, 0u, 0u);
+          ga[i][0] = ok ? *reinterpret_cast<const float4*>(gp) : z;
+          ga[i][1] = ok ? *reinterpret_cast<const float4*>(gp + 4) : z;
+        }
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -286,6 +313,7 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         const int pos = pos0 - halo + j;
         float g[8], pv[8], o[8];
         unpack8(gq[i], g);
+        if (LNIN) ln1_bwd8(g, sq[i], ga[i][0], ga[i][1]);
         unpack8(pq[i], pv);
 #pragma unroll
         for (int e = 0; e < 8; e += 2) {
@@ -353,6 +381,7 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
       }
   }
   __syncthreads();
+  float dgs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // LNIN: this thread's sum_l ds1 (chunk tid & 15)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = tid + 512 * i;
@@ -361,12 +390,39 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     const size_t off = sbase + (size_t)(pos0 + row) * CH + c * 8;
     float gv[8], o[8];
     unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
+    if (LNIN) {
+      const float* gp = g1 + (size_t)(pos0 + row) * CH + c * 8;
+      ln1_bwd8(gv, *reinterpret_cast<const uint4*>(s1 + off), *reinterpret_cast<const float4*>(gp),
+               *reinterpret_cast<const float4*>(gp + 4));
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dgs[e] += gv[e];
+    }
     const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c));
     const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c + 1));
     const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
     *reinterpret_cast<uint4*>(dx + off) = packq8(o);
+  }
+  if (LNIN) {
+    // lanes l, l^16, l^32, l^48 own the same chunk; then the 8 waves through LDS (ft is free now)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      dgs[e] += __shfl_xor(dgs[e], 16, 64);
+      dgs[e] += __shfl_xor(dgs[e], 32, 64);
+    }
+    __syncthreads();                              // every thread is done reading ft
+    if (lane < 16) {
+      *reinterpret_cast<float4*>(ft + w * CH + lane * 8) = make_float4(dgs[0], dgs[1], dgs[2], dgs[3]);
+      *reinterpret_cast<float4*>(ft + w * CH + lane * 8 + 4) = make_float4(dgs[4], dgs[5], dgs[6], dgs[7]);
+    }
+    __syncthreads();
+    if (tid < CH) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) a += ft[k * CH + tid];
+      atomicAdd(dgb + (size_t)b * CH + tid, a);
+    }
   }
 }
 
@@ -399,7 +455,8 @@ static void set_conv3_attrs() {
   if (conv3_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<256, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   conv3_attrs_set = true;
 }
 
@@ -439,9 +496,24 @@ PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* p
   const int lds = dgrad3_lds(KS, dil);
   if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
   const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_dgrad3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1, (const bf16_t*)pre_n,
-                     (const bf16_t*)pre_w, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n,
-                     (bf16_t*)dpre_w, L, KS, dil);
+  hipLaunchKernelGGL(conv_dgrad3_kernel<false>, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1, nullptr,
+                     nullptr, nullptr, nullptr, (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn,
+                     (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
+  return pbx_launch_status();
+}
+
+// reference semantics: dh1 (gradient at the LN1 output) in, the LN1 backward fused (see conv_dgrad3_kernel);
+// c1: [B][4] from pbx_ln1_consts; dgb [B][128] fp32 is accumulated into
+PBX_EXPORT int pbx_conv_dgrad3_ln(const void* dh1, const void* s1, const float* g1, const float* c1, float* dgb,
+                                  const void* pre_n, const void* pre_w, const void* ftn, const void* ftw, void* dx,
+                                  void* dpre_n, void* dpre_w, int B, int L, int KS, int dil, hipStream_t st) {
+  set_conv3_attrs();
+  const int lds = dgrad3_lds(KS, dil);
+  if (lds > 163840 || dil < 1 || KS < 2 || lds < 8 * CH * 4) return (int)hipErrorInvalidValue;
+  const int T = (L + BM - 1) / BM;
+  hipLaunchKernelGGL(conv_dgrad3_kernel<true>, dim3(B * T), dim3(512), lds, st, (const bf16_t*)dh1,
+                     (const bf16_t*)s1, g1, c1, dgb, (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn,
+                     (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
   return pbx_launch_status();
 }
 

@@ -1148,6 +1148,27 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// Per-sample LayerNorm-1 backward constants for the conv data gradient that builds ds1 itself
+// (pbx_conv_dgrad3_ln): c[b] = (mean1, rstd1, m1, m2), m1 = mean(dxhat), m2 = mean(dxhat xhat) from the
+// LN1 partials of the LN2/MLP backward.  One wave per sample.
+__global__ void __launch_bounds__(256) ln1_consts_kernel(const float* __restrict__ st1, int T1, int BM1,
+                                                         const float* __restrict__ sums1, int TS1,
+                                                         const float* __restrict__ st1f, float* __restrict__ consts,
+                                                         int B, int L, float eps) {
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  float mean, rstd, m1, m2;
+  if (st1f != nullptr) {
+    mean = st1f[2 * b];
+    rstd = st1f[2 * b + 1];
+  } else {
+    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+  }
+  wave_bwd_consts(sums1 + (size_t)b * TS1 * 2, TS1, 1.0f / (float)(L * CH), m1, m2);
+  if ((threadIdx.x & 63) == 0) *reinterpret_cast<float4*>(consts + (size_t)b * 4) = make_float4(mean, rstd, m1, m2);
+}
+
+// ------------------------------------------------------------------------------------------------
 // token embedding: forward gather to bf16, backward per-token segmented sum
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restrict__ tok, const float* __restrict__ E,
                                                         bf16_t* __restrict__ out, long rows) {
@@ -1414,6 +1435,14 @@ PBX_EXPORT int pbx_ln1_finalizex(const void* dh1, const void* s1, const float* s
   set_ln_attrs();
   hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
                      BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, gb, st1f, B, L, eps);
+  return pbx_launch_status();
+}
+
+// consts: [B][4] fp32 (mean1, rstd1, m1, m2) for pbx_conv_dgrad3_ln; st1f nullable (late gb)
+PBX_EXPORT int pbx_ln1_consts(const float* st1, int T1, int BM1, const float* sums1, int TS1, const float* st1f,
+                              float* consts, int B, int L, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(ln1_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st1, T1, BM1, sums1, TS1, st1f, consts, B,
+                     L, eps);
   return pbx_launch_status();
 }
 

@@ -35,6 +35,8 @@ _lib.register("pbx_conv_fwd3x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I,
 _lib.register("pbx_ln_linear_fwdx", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln1_finalizex", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_dgrad3_ln", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_ln1_consts", [_P, _I, _I, _P, _I, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
@@ -94,6 +96,17 @@ LN2_WG_PER_CU = int(os.environ.get("PBX_LN2_WGCU", "0"))
 # SLOWER on the B=512 L=512 step (same-box A/B, high- or normal-priority aux stream: the 32 global-track
 # workgroups find no CU with free LDS beside the convolution's), so it is opt-in.
 LATE_GB = os.environ.get("PBX_LATE_GB", "0") == "1"
+# LayerNorm-1 backward inside the conv data gradient (csrc/conv2.hip conv_dgrad3_kernel<true>): the
+# kernel reads dh1, s1 and g1 and builds ds1 itself (halo rows included) instead of a separate finalize
+# pass writing ds1 for it.  Measured 1.5-3 % SLOWER on the B=512 L=512 step (same-box A/B, 3 rounds,
+# profiles/r2_v8_ln1_fuse_ab.txt): the data-gradient prologue is load-latency bound and now carries
+# 2.5x the bytes per round trip, which costs more than the 40 us finalize pass it replaces.  Opt-in.
+LN1_FUSE = os.environ.get("PBX_LN1_FUSE", "0") == "1"
+
+
+def ln1_fused(gb_late) -> bool:
+    """LN1 backward fused into the conv data gradient: v3 convs, s1 holding the broadcast vector."""
+    return LN1_FUSE and CONV_IMPL == "v3" and gb_late is None
 
 
 def late_gb_enabled() -> bool:
@@ -341,19 +354,31 @@ class LocalBlockFn(torch.autograd.Function):
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
                   dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, LN2_WG_PER_CU, *dwl_slab(dev), stream)
-        # LN1 finalize (ds1) + gradient of the broadcast global->local vector
-        ds1 = torch.empty_like(x)
-        _lib.call("pbx_ln1_finalizex", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
-                  TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), _p(gb_late), _p(st1f), B, L, LN_EPS, stream)
-        if streams.GLOBAL_ENABLED:
-            # the previous block's global-track backward (next autograd node, aux stream) needs only
-            # dgb: let it start here, beside the conv data gradient below
-            streams.fork(dev, "global")
-        # convolutions
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
-        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
+        if ln1_fused(gb_late):
+            # LN1 backward (ds1) + gradient of the broadcast global->local vector inside the conv data
+            # gradient; only the per-sample constants are a separate (one wave per sample) launch
+            c1 = torch.empty((B, 4), dtype=torch.float32, device=dev)
+            _lib.call("pbx_ln1_consts", st1.data_ptr(), T1, BM1, sums1.data_ptr(), TS1, _p(st1f), c1.data_ptr(),
+                      B, L, LN_EPS, stream)
+            _lib.call("pbx_conv_dgrad3_ln", dh1.data_ptr(), s1.data_ptr(), g1.data_ptr(), c1.data_ptr(),
+                      dgb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
+                      dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, stream)
+            if streams.GLOBAL_ENABLED:
+                streams.fork(dev, "global")
+        else:
+            # LN1 finalize (ds1) + gradient of the broadcast global->local vector
+            ds1 = torch.empty_like(x)
+            _lib.call("pbx_ln1_finalizex", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1,
+                      sums1.data_ptr(), TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), _p(gb_late), _p(st1f),
+                      B, L, LN_EPS, stream)
+            if streams.GLOBAL_ENABLED:
+                # the previous block's global-track backward (next autograd node, aux stream) needs only
+                # dgb: let it start here, beside the conv data gradient below
+                streams.fork(dev, "global")
+            conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)

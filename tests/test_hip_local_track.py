@@ -69,9 +69,10 @@ def test_local_block_forward(L, B, late, monkeypatch):
                                                  (200, 3, "recompute", 2, False), (4096, 1, "recompute", 0, False),
                                                  (300, 40, "recompute", 2, False), (512, 2, "store", 0, True),
                                                  (300, 5, "recompute", 0, True), (4096, 1, "store", 0, True)])
-def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch):
+def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch, fuse=False):
     from proteinbert_pytorch_replication_amd.ops import local_track as lt
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
+    monkeypatch.setattr(lt, "LN1_FUSE", fuse)          # LN1 backward inside the conv data gradient
     monkeypatch.setattr(lt, "PRE_L", pre_l)            # MLP pre-activation stored, or recomputed in backward
     monkeypatch.setattr(lt, "LN2_WG_PER_CU", wgcu)
     monkeypatch.setattr(lt, "LATE_GB", late)
@@ -101,6 +102,12 @@ def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch):
     for n, a, b in zip(names, got, ref):
         e = rel(a, b)
         assert e < 3e-2, f"{n}: rel err {e:.3e}"
+
+
+@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1)])
+def test_local_block_backward_fused_ln1(L, B, monkeypatch):
+    """LN1 backward inside the conv data gradient (opt-in PBX_LN1_FUSE=1)."""
+    test_local_block_backward(L, B, "store", 0, False, monkeypatch, fuse=True)
 
 
 def test_embedding_kernels():
