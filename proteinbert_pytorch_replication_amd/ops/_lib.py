@@ -29,6 +29,7 @@ _SIGS = {
     "pbx_adam_flat": [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P],
     "pbx_sumsq_flat": [_P, _I64, _P, _P, _P],
     "pbx_clip_scale_flat": [_P, _I64, _P, _F32, _P],
+    "pbx_nonfinite_flag": [_P, _I64, _P, _P, _P],
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -117,6 +117,22 @@ class FusedAdam(torch.optim.Optimizer):
         return loss
 
     @torch.no_grad()
+    def set_nonfinite_skip(self) -> torch.Tensor:
+        """Device flag (int32 [1]): 1 when any arena gradient is NaN / Inf; the update then leaves
+        parameters and moments unchanged.  No host sync (two HIP launches on a GPU)."""
+        a = self.arena
+        if _hip_ok(a.grad):
+            from ..ops import _lib
+            if getattr(self, "_nf_ws", None) is None:
+                self._nf_ws = torch.empty(1025, dtype=torch.int32, device=a.grad.device)
+            _lib.call("pbx_nonfinite_flag", a.grad.data_ptr(), a.numel, self._nf_ws.data_ptr(),
+                      self._nf_ws[1024:].data_ptr(), _lib.stream_ptr(a.grad.device))
+            self.skip_flag = self._nf_ws[1024:]
+        else:
+            self.skip_flag = (~torch.isfinite(a.grad).all()).to(torch.int32).reshape(1)
+        return self.skip_flag
+
+    @torch.no_grad()
     def clip_grad_norm_(self, max_norm: float) -> torch.Tensor:
         """Global L2 grad-norm clip over the arena (after DP reduction); returns the pre-clip norm."""
         a = self.arena

@@ -78,7 +78,7 @@ class PretrainStep:
             # all-reduced grads (bucketed DP): every rank takes the same decision, no host sync.
             # ZeroFusedAdam reduces inside step() and replaces this local flag by a group-wide
             # decision over the reduced shards (parallel/zero.py)
-            opt.skip_flag = (~torch.isfinite(opt.arena.grad.sum())).to(torch.int32).reshape(1)
+            opt.set_nonfinite_skip()
         opt.step()
         return loss.detach()
 

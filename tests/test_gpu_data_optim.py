@@ -48,6 +48,23 @@ def test_fused_adam_skip_flag():
     assert torch.all(p.detach() < 1.0)
 
 
+@pytest.mark.parametrize("n", [1, 7, 4096, 300001])
+def test_nonfinite_flag_kernel(n):
+    """pbx_nonfinite_flag: 1 iff any gradient element is NaN / Inf (every position, tail included)."""
+    p = torch.nn.Parameter(torch.zeros(n, device="cuda"))
+    fa = FusedAdam([p], lr=0.1)
+    p.grad.copy_(torch.randn(n, device="cuda") * 1e30)          # huge but finite: not flagged
+    assert int(fa.set_nonfinite_skip().item()) == 0
+    for bad in (float("inf"), float("-inf"), float("nan")):
+        for pos in sorted({0, n // 2, n - 1}):
+            g = torch.randn(n, device="cuda")
+            g[pos] = bad
+            p.grad.copy_(g)
+            assert int(fa.set_nonfinite_skip().item()) == 1, (bad, pos)
+    p.grad.zero_()
+    assert int(fa.set_nonfinite_skip().item()) == 0
+
+
 def test_clip_grad_norm_gpu():
     p = torch.nn.Parameter(torch.zeros(5000, device="cuda"))
     fa = FusedAdam([p], lr=0.1)
