@@ -36,6 +36,20 @@ constexpr int BM = 128;               // positions per workgroup
 constexpr int FRAG = 64 * 8;          // bf16 per packed fragment (64 lanes x 8)
 constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging tile
 
+// Workgroup -> (sample, tile) id.  The dispatcher deals workgroups to the 8 XCDs round-robin by id
+// (blockIdx % 8 labels the blocks that share an XCD's L2), so the bijective remap
+// (cdna_hip_programming.md T1) gives each XCD a contiguous run of tiles: neighbouring tiles of one
+// sample, whose +-20-row halos overlap, then read those rows through the same L2.  +0.5 % on the step,
+// 6/6 same-box rounds (profiles/r2_v8_xcd_remap_ab.txt); -DPBX_NO_XCD_REMAP builds the identity map.
+__device__ __forceinline__ int tile_id() {
+#ifndef PBX_NO_XCD_REMAP
+  const int n = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = n >> 3, r = n & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+#else
+  return blockIdx.x;
+#endif
+}
+
 // Packed fragment index (in fragments) of (tap k, K-block kb of 16, M-block mb of 32); lane offset
 // added by the reader.  Forward: M = output channel, K = input channel.  Dgrad: M = input channel,
 // K = output channel.
@@ -53,7 +67,8 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
   constexpr int TOT = TBM * 256;                              // bytes of one [TBM][128] bf16 tile
   const int T = (L + TBM - 1) / TBM;
-  const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
+  const int tid0 = tile_id();
+  const int b = tid0 / T, t = tid0 - (tid0 / T) * T;
   const int pos0 = t * TBM;
   const int half = KS >> 1;
   const int halo = half * dil;
@@ -250,7 +265,8 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = (L + BM - 1) / BM;
-  const int b = blockIdx.x / T, t = blockIdx.x - (blockIdx.x / T) * T;
+  const int tid0 = tile_id();
+  const int b = tid0 / T, t = tid0 - (tid0 / T) * T;
   const int pos0 = t * BM;
   const int half = KS >> 1;
   const int halo_n = half, halo_w = half * dil;
