@@ -74,6 +74,8 @@ def main():
     L = a.seq_len or mcfg.sequences_length
     B = a.batch or cfg.train.batch_size
     torch.manual_seed(a.seed)
+    if a.impl == "hip" and dev.type != "cuda":
+        a.impl = "torch"            # CPU rehearsal (gloo ranks): the fused kernels need a GPU
     backend = "hip" if a.impl == "hip" else "torch"
     model = ProteinBERT(sequences_length=L, num_annotations=mcfg.num_annotations, local_dim=mcfg.local_dim,
                         global_dim=mcfg.global_dim, key_dim=mcfg.key_dim, num_heads=mcfg.num_heads,
