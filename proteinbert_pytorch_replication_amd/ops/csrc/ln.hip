@@ -55,34 +55,41 @@ __device__ __forceinline__ void stage_weight(unsigned char* dst, const bf16_t* _
 // The caller passes in-bounds pointers (rows clamped); `ok` only masks the values, so every load is
 // unconditional and all 24 of them are in flight together (a load under a divergent branch costs
 // one exposed memory round trip per branch).
+// KB: channel chunks whose loads are in flight together (8: one round trip, ~160 VGPRs of operands;
+// 4: two round trips at half the registers, for the high-occupancy pool variant)
+template <int KB = 8>
 __device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict__ src, const float* __restrict__ gam,
                                              const float* __restrict__ bet, float mean, float rstd, bool ok,
                                              int h, bf16_t* __restrict__ out) {
-  uint4 sq[8];
-  float4 ga[8][2], ba[8][2];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const int ci = kk * 16 + 8 * h;
-    sq[kk] = *reinterpret_cast<const uint4*>(src + ci);
-    ga[kk][0] = *reinterpret_cast<const float4*>(gam + ci);
-    ga[kk][1] = *reinterpret_cast<const float4*>(gam + ci + 4);
-    ba[kk][0] = *reinterpret_cast<const float4*>(bet + ci);
-    ba[kk][1] = *reinterpret_cast<const float4*>(bet + ci + 4);
+  for (int k0 = 0; k0 < 8; k0 += KB) {
+  uint4 sq[KB];
+  float4 ga[KB][2], ba[KB][2];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int ci = (k0 + k) * 16 + 8 * h;
+    sq[k] = *reinterpret_cast<const uint4*>(src + ci);
+    ga[k][0] = *reinterpret_cast<const float4*>(gam + ci);
+    ga[k][1] = *reinterpret_cast<const float4*>(gam + ci + 4);
+    ba[k][0] = *reinterpret_cast<const float4*>(bet + ci);
+    ba[k][1] = *reinterpret_cast<const float4*>(bet + ci + 4);
   }
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
+  for (int k = 0; k < KB; ++k) {
+    const int kk = k0 + k;
     const int ci = kk * 16 + 8 * h;
     float sv[8], v[8];
-    unpack8(sq[kk], sv);
-    const float g[8] = {ga[kk][0].x, ga[kk][0].y, ga[kk][0].z, ga[kk][0].w,
-                        ga[kk][1].x, ga[kk][1].y, ga[kk][1].z, ga[kk][1].w};
-    const float be[8] = {ba[kk][0].x, ba[kk][0].y, ba[kk][0].z, ba[kk][0].w,
-                         ba[kk][1].x, ba[kk][1].y, ba[kk][1].z, ba[kk][1].w};
+    unpack8(sq[k], sv);
+    const float g[8] = {ga[k][0].x, ga[k][0].y, ga[k][0].z, ga[k][0].w,
+                        ga[k][1].x, ga[k][1].y, ga[k][1].z, ga[k][1].w};
+    const float be[8] = {ba[k][0].x, ba[k][0].y, ba[k][0].z, ba[k][0].w,
+                         ba[k][1].x, ba[k][1].y, ba[k][1].z, ba[k][1].w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ok ? (sv[e] - mean) * rstd * g[e] + be[e] : 0.f;
     const uint4 q = packq8(v);
     if (ok && out != nullptr) *reinterpret_cast<uint4*>(out + ci) = q;
     f[kk] = __builtin_bit_cast(bf16x8, q);
+  }
   }
 }
 
@@ -496,7 +503,10 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
 constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
 constexpr int GT_BYTES = 32 * GT_STRIDE;
 
-template <int NWAVE, int NI>   // NI: GELU pairs interleaved per core call (4: one half-tile, 8: a tile, 16: both)
+// NP: 32-position MFMA tiles per work item: 2 (64 positions, each Wv fragment read from LDS feeds two
+// MFMAs; ~248 VGPRs, two waves per SIMD) or 1 (32 positions; <= 168 VGPRs, three waves per SIMD, 12
+// waves per workgroup; vpart then has one row per 32-position tile)
+template <int NWAVE, int NI, int NP = 2>   // NI: GELU pairs interleaved per core call (4: one half-tile, 8: a tile, 16: both)
 __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
@@ -509,33 +519,41 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
   unsigned char* gt = smem + NJ * 256 + w * GT_BYTES;               // this wave's transpose tile
   const int NW = blockDim.x >> 6;
   const int T2 = (L + BML - 1) / BML;
-  const int TW = (L + 63) / 64;
+  const int TW64 = (L + 63) / 64;
+  const int TW = NP == 2 ? TW64 : 2 * TW64;        // work items per sample
   const int NJT = NJ / 32;
   const long items = (long)B * TW;
   stage_weight(ws, wv, NJ);
   __syncthreads();
   for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW) {
     const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos0 = tw * 64;
+    const int pos0 = tw * 32 * NP;
     float mean, rstd;
     wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
     bf16x8 hf0[8], hf1[8];
     {
-      const int pa = pos0 + r, pb = pos0 + 32 + r;
-      const int ca = min(pa, L - 1), cb = min(pb, L - 1);
-      const size_t ra = ((size_t)b * L + ca) * CH, rb = ((size_t)b * L + cb) * CH;
-      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
-      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
+      const int pa = pos0 + r;
+      const int ca = min(pa, L - 1);
+      const size_t ra = ((size_t)b * L + ca) * CH;
+      ln_row_frags<NP == 2 ? 8 : 4>(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h,
+                                     h2 + ra);
+      if constexpr (NP == 2) {
+        const int pb = pos0 + 32 + r;
+        const int cb = min(pb, L - 1);
+        const size_t rb = ((size_t)b * L + cb) * CH;
+        ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
+      }
     }
     float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
-    // fragment base of this item's two 32-position tiles: [b][2 tw + pt][jt][s][lane]
-    bf16x8* gdst = gfrag + ((size_t)b * 2 * TW + 2 * tw) * NJT * 2 * 64 + lane;
+    // fragment base of this item's 32-position tiles: [b][2 ceil(L/64)][jt][s][lane]
+    bf16x8* gdst = gfrag + ((size_t)b * 2 * TW64 + NP * tw) * NJT * 2 * 64 + lane;
     auto epi = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
       f32x2 sv = {0.f, 0.f};
-      // GELU / GELU' of both 32x32 tiles: NI pairs per interleaved core call
-      f32x2 gdall[16];
+      // GELU / GELU' of the item's 32x32 tiles: NI pairs per interleaved core call
+      constexpr int NPAIR = 8 * NP;
+      f32x2 gdall[NPAIR];
 #pragma unroll
-      for (int c8 = 0; c8 < 16; c8 += NI) {
+      for (int c8 = 0; c8 < NPAIR; c8 += NI) {
         f32x2 xv[NI], gv[NI], gd[NI];
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
@@ -551,7 +569,7 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
         }
       }
 #pragma unroll
-      for (int pt = 0; pt < 2; ++pt) {
+      for (int pt = 0; pt < NP; ++pt) {
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           // positions 8g + 4h .. +3 of column j = r -> Gt[r][8g + 4h]
@@ -590,7 +608,7 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         c0 = mfma32(hf0[kk], wf[kk], c0);
-        c1 = mfma32(hf1[kk], wf[kk], c1);
+        if constexpr (NP == 2) c1 = mfma32(hf1[kk], wf[kk], c1);
       }
       if (jt + 1 < NJT) {
 #pragma unroll
@@ -1262,6 +1280,8 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<12, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<12, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -1338,12 +1358,14 @@ PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g
   set_ln_attrs();
   if (NJ % 64 != 0 || NJ * 256 + (nw & 15) * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
   // nw (low 4 bits) = 8: two waves per SIMD, 4 GELU pairs per core call; 4: one wave per SIMD with
-  // 8 independent pairs per core call (or 16 when nw = 4 | 16 << 4) for ILP
-  const int ni = nw >> 4 ? nw >> 4 : ((nw & 15) == 8 ? 4 : 8);
+  // 8 independent pairs per core call (or 16 when nw = 4 | 16 << 4) for ILP; 12: 32-position items,
+  // three waves per SIMD (vpart: one row per 32-position tile, 2 ceil(L/64) rows per sample)
+  const int ni = nw >> 4 ? nw >> 4 : ((nw & 15) == 8 ? 4 : (nw & 15) == 12 ? 2 : 8);
   nw &= 15;
-  if (nw != 4 && nw != 8) return (int)hipErrorInvalidValue;
-  auto* k = nw == 8 ? ln_attn_fwd2_kernel<8, 4> : (ni == 16 ? ln_attn_fwd2_kernel<4, 16> : ln_attn_fwd2_kernel<4, 8>);
-  const long items2 = (long)B * ((L + 63) / 64);
+  if (nw != 4 && nw != 8 && nw != 12) return (int)hipErrorInvalidValue;
+  auto* k = nw == 12 ? (ni == 4 ? ln_attn_fwd2_kernel<12, 4, 1> : ln_attn_fwd2_kernel<12, 2, 1>)
+          : nw == 8 ? ln_attn_fwd2_kernel<8, 4> : (ni == 16 ? ln_attn_fwd2_kernel<4, 16> : ln_attn_fwd2_kernel<4, 8>);
+  const long items2 = (long)B * ((L + 63) / 64) * (nw == 12 ? 2 : 1);
   long wg2 = (items2 + nw - 1) / nw;
   if (wg2 > num_cus()) wg2 = num_cus();
   hipLaunchKernelGGL(k, dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,

@@ -75,6 +75,9 @@ ATTN_POOL = os.environ.get("PBX_ATTN_POOL", "v2")
 
 
 # pool-v2 forward launch: waves per workgroup | GELU pairs per interleaved core call << 4
+# (12: 32-position items, three waves per SIMD, vpart rows per 32 positions; measured equal to slightly
+# slower than 8 on the B=512 L=512 step, profiles/r2_v8_pool_32pos_ab.txt: more waves do not help a
+# kernel whose SIMDs are already issue-bound on the GELU / GELU' VALU work)
 ATTN_FWD2_CFG = int(os.environ.get("PBX_ATTN_FWD2", "8"), 0)
 
 
@@ -284,10 +287,14 @@ class LocalBlockFn(torch.autograd.Function):
         NJ = wv_bf16.shape[0]
         nwf = attn_fwd_waves(L)
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
-        h2 = torch.empty_like(x)
-        vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
         # the GELU' fragments only serve a backward pass: inference / frozen-encoder forwards skip them
         ctx.pool_v2 = attn_pool_v2(NJ) and need_bwd
+        BMV = 64                                # positions per vpart row
+        if ctx.pool_v2 and ATTN_FWD2_CFG & 15 == 12:
+            BMV = 32                            # 32-position work items: one vpart row each
+        TVR = (L + 63) // 64 * (64 // BMV)
+        h2 = torch.empty_like(x)
+        vpart = torch.empty((B, TVR, NJ), dtype=torch.float32, device=dev)
         if ctx.pool_v2:
             # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
             gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
@@ -302,7 +309,7 @@ class LocalBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l if pre_l is not None else bl, s2, st2, hsave, wtn,
                               wtw, wl_b, wv_bf16, g1, be1, g2, gb if late else None, st1f)
         ctx.pre_l_stored = pre_l is not None
-        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, 64)
+        ctx.meta = (B, L, KS, dil, BM1, T1, T2, NJ, BMV)
         ctx.set_materialize_grads(False)
         ctx.params = params
         return h2, vpart
@@ -327,6 +334,8 @@ class LocalBlockFn(torch.autograd.Function):
             # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
             dvpart = dvpart[:, 0, :].float().contiguous()
             BMV = (L + 31) // 32 * 32
+        elif dvpart.shape[1] != TV:
+            dvpart = dvpart[:, :TV]             # 32-position items: a trailing all-padding tile row
         dvpart = dvpart.float().contiguous()
         # attention pool + LN2 partials
         nwb = attn_bwd_waves(L)

@@ -110,6 +110,15 @@ def test_local_block_backward_fused_ln1(L, B, monkeypatch):
     test_local_block_backward(L, B, "store", 0, False, monkeypatch, fuse=True)
 
 
+@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (300, 5), (64, 4), (4096, 1)])
+def test_local_block_backward_pool_32pos_items(L, B, monkeypatch):
+    """Pool forward with 32-position work items at three waves per SIMD (PBX_ATTN_FWD2=12): one vpart
+    row per 32 positions, GELU' fragments in the same layout as the 64-position form."""
+    from proteinbert_pytorch_replication_amd.ops import local_track as lt
+    monkeypatch.setattr(lt, "ATTN_FWD2_CFG", 12)
+    test_local_block_backward(L, B, "store", 0, False, monkeypatch)
+
+
 def test_embedding_kernels():
     from proteinbert_pytorch_replication_amd.ops.local_track import EmbedFn
     torch.manual_seed(0)

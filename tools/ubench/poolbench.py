@@ -55,7 +55,7 @@ be2 = torch.zeros(L, C, device=dev)
 wv = (torch.randn(NJ, C, device=dev) * 0.05).to(bf)
 h2 = torch.empty_like(x)
 TV = (L + 63) // 64
-vpart = torch.empty(B, TV, NJ, device=dev)
+vpart = torch.empty(B, TV * (2 if lt.ATTN_FWD2_CFG & 15 == 12 else 1), NJ, device=dev)   # 12: rows per 32 positions
 gfrag = torch.empty(B, 2 * TV, NJ * 32, device=dev, dtype=bf)
 us = timeit(lambda: _lib.call("pbx_ln_attn_fwd2", P(s2), P(st2), P(g2), P(be2), P(wv), P(h2), P(vpart), P(gfrag),
                               B, L, NJ, lt.ATTN_FWD2_CFG, 1e-5, st))
