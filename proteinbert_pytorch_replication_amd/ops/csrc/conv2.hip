@@ -331,11 +331,15 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         unpack8(gq[i], g);
         if (LNIN) ln1_bwd8(g, sq[i], ga[i][0], ga[i][1]);
         unpack8(pq[i], pv);
+        // GELU' of the 8 values as interleaved scalar A&S stages (gelu_scalar_n, as in the forward)
+        f32x2 pp[4], gd[4];
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          const f32x2 dd = gelu_grad2((f32x2){pv[e], pv[e + 1]}) * (f32x2){g[e], g[e + 1]};
-          o[e] = dd.x;
-          o[e + 1] = dd.y;
+        for (int e = 0; e < 4; ++e) pp[e] = (f32x2){pv[2 * e], pv[2 * e + 1]};
+        gelu_scalar_n<4, 1>(pp, nullptr, gd);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[2 * e] = gd[e].x * g[2 * e];
+          o[2 * e + 1] = gd[e].y * g[2 * e + 1];
         }
         const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
         if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
