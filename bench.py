@@ -9,6 +9,11 @@ GO multi-hot annotations generated and corrupted on the device every step.
     python bench.py --gpus N --steps K --warmup W
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU, RCCL)
 
+Run as plain ``python bench.py --gpus N`` (N > 1, no WORLD_SIZE in the environment), the script
+starts the N ranks itself -- ``torch.distributed.run`` as a CHILD process, launched before this
+process touches the GPU -- and exits with the child's status.  Under a launcher, WORLD_SIZE must
+equal ``--gpus`` or the run fails (exit 2) instead of measuring a different world.
+
 A timed step = synthetic batch generation + corruption, forward, loss,
 backward, bucketed RCCL all-reduce (N>1) and the fused Adam update.
 Rank 0 prints ONE JSON line; the time is the max over ranks.
@@ -63,11 +68,37 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(n: int) -> int:
+    """Start ``n`` ranks of this script under torch.distributed.run (a child process: nothing here has
+    initialised the GPU) and return its exit status."""
+    import subprocess
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", os.environ.get("MASTER_PORT", str(_free_port())),
+           os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     a = parse()
+    if a.gpus < 1:
+        print("error: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(self_launch(a.gpus))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus:
+        print(f"error: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to measure a different world size",
+              file=sys.stderr)
+        sys.exit(2)
     info = pdist.init_distributed()
-    if info.world_size != a.gpus and not (a.gpus == 1 and info.world_size == 1):
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={info.world_size}", file=sys.stderr)
     dev = info.device
     cfg = get_preset(a.preset or ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else "cfg2_paper_l512"))
     mcfg = cfg.model
@@ -87,7 +118,8 @@ def main():
     ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb) if info.distributed else None
     if ddp is not None:
         ddp.broadcast_parameters(model)
-    dtype = torch.float32 if a.impl == "faithful" else torch.bfloat16
+    # bf16 activations on the GPU; the CPU rehearsal path (gloo ranks, BASELINE cfg 1) computes in fp32
+    dtype = torch.float32 if (a.impl == "faithful" or dev.type != "cuda") else torch.bfloat16
     step = PretrainStep(model, opt, ddp, compute_dtype=dtype)
     if a.impl == "faithful":
         # reference computation as written: literal Q/K/softmax attention, fp32, eager
@@ -124,15 +156,22 @@ def main():
                "higher_is_better": True, "scaling": "weak",
                "vs_baseline": round(value / PAPER_IMPLIED_SEQ_PER_S, 2),
                "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-               "data": "synthetic (on-device UniRef90-shaped sequences + 8943-dim GO multi-hot, random-init weights)",
+               "data": _data_label(dev),
                "config": {"model": f"ProteinBERT paper config: {mcfg.num_blocks} blocks, d_local={mcfg.local_dim}, "
                                    f"d_global={mcfg.global_dim}, key_dim={mcfg.key_dim}, heads={mcfg.num_heads}, "
                                    f"annotations={mcfg.num_annotations}, semantics={a.semantics}",
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
                           "impl": a.impl, "hip_graph": graphed},
+               "world_size": n, "backend": info.backend if n > 1 else "single",
                "final_loss": round(final_loss, 5)}
         print(json.dumps(out), flush=True)
     pdist.destroy()
+
+
+def _data_label(dev) -> str:
+    where = "generated on the device by HIP kernels" if dev.type == "cuda" else "generated on the host CPU"
+    return (f"synthetic: UniRef90-shaped sequences + 8943-dim GO multi-hot, {where} and corrupted every step; "
+            "random-init weights")
 
 
 def _timed(one, a, info, dev):
@@ -190,8 +229,10 @@ def finetune_bench(a, info, encoder, L, B, mcfg):
         out = {"metric": "sequences/sec (whole node) ProteinBERT fine-tune (frozen encoder + per-residue "
                          f"{a.classes}-state head) L={L}", "value": round(value, 2), "unit": "sequences/s",
                "n_gpus": n, "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(1000 * dt / a.steps, 3),
-               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
-               "data": "synthetic (on-device tokens, random per-residue labels, random-init weights)",
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "bf16" if dev.type == "cuda" else "fp32",
+               "data": _data_label(dev).replace("GO multi-hot", "GO multi-hot, random per-residue labels"),
+               "world_size": n,
                "config": {"model": f"ProteinBERT paper config encoder (frozen) + Linear({mcfg.local_dim}+"
                                    f"{mcfg.global_dim} -> {a.classes}) per residue",
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",

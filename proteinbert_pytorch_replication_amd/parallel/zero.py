@@ -24,7 +24,7 @@ import torch
 import torch.distributed as dist
 
 from ..train.arena import ALIGN
-from ..train.optim import FusedAdam, _hip_ok
+from ..train.optim import FusedAdam, _hip_ok, adam_update_host, skip_requested
 
 
 class ZeroFusedAdam(FusedAdam):
@@ -91,8 +91,18 @@ class ZeroFusedAdam(FusedAdam):
             # value on any rank lands in some rank's reduced shard, so decide from the shards and
             # agree over the group (MAX) - every rank skips together, no NaN reaches the all-gather
             n = self.hi - self.lo
-            bad = (~torch.isfinite(self._gshard[:n].sum())).to(torch.int32).reshape(1) if n > 0 \
-                else torch.zeros(1, dtype=torch.int32, device=self._gshard.device)
+            bad = torch.zeros(1, dtype=torch.int32, device=self._gshard.device)
+            if n > 0:
+                # exact per-element test (a shard sum of large finite values could overflow to Inf);
+                # the same pbx_nonfinite_flag kernel as the non-ZeRO path on a GPU
+                if _hip_ok(self._gshard):
+                    from ..ops import _lib
+                    ws = torch.empty(1025, dtype=torch.int32, device=self._gshard.device)
+                    _lib.call("pbx_nonfinite_flag", self._gshard.data_ptr(), n, ws.data_ptr(), ws[1024:].data_ptr(),
+                              _lib.stream_ptr(self._gshard.device))
+                    bad = ws[1024:].clone()
+                else:
+                    bad.fill_(0 if bool(torch.isfinite(self._gshard[:n]).all()) else 1)
             if self.world > 1:
                 dist.all_reduce(bad, op=dist.ReduceOp.MAX, group=self.pg)
             self.skip_flag = bad
@@ -111,21 +121,8 @@ class ZeroFusedAdam(FusedAdam):
                 _lib.call("pbx_adam_flat", p.data_ptr(), g.data_ptr(), m.data_ptr(), v.data_ptr(), _lib.ptr(sh), n,
                           self._hp_dev.data_ptr(), _lib.ptr(self.skip_flag), self._step_dev.data_ptr(),
                           _lib.stream_ptr(a.data.device))
-            else:
-                lr, b1, b2, eps, wd, bc1, bc2s, gs = self._hparam_values()
-                gg = g * gs
-                if wd != 0:
-                    gg = gg + wd * p
-                m_new = m * b1 + (1 - b1) * gg
-                v_new = v * b2 + (1 - b2) * gg * gg
-                p_new = p - (lr / bc1) * m_new / (v_new.sqrt() / bc2s + eps)
-                if self.skip_flag is not None:
-                    keep = self.skip_flag == 0
-                    m_new, v_new, p_new = (torch.where(keep, m_new, m), torch.where(keep, v_new, v),
-                                           torch.where(keep, p_new, p))
-                m.copy_(m_new)
-                v.copy_(v_new)
-                p.copy_(p_new)
+            elif not skip_requested(self.skip_flag):
+                adam_update_host(self, p, g, m, v)
         self._all_gather()
         return loss
 

@@ -97,24 +97,18 @@ class FusedAdam(torch.optim.Optimizer):
                       self.exp_avg_sq.data_ptr(), _lib.ptr(self.shadow), a.numel, self._hp_dev.data_ptr(),
                       _lib.ptr(self.skip_flag), self._step_dev.data_ptr(), _lib.stream_ptr(a.data.device))
         else:
-            lr, b1, b2, eps, wd, bc1, bc2s, gs = self._hparam_values()
-            g = a.grad * gs
-            if wd != 0:
-                g = g + wd * a.data
-            m_new = self.exp_avg * b1 + (1 - b1) * g
-            v_new = self.exp_avg_sq * b2 + (1 - b2) * g * g
-            p_new = a.data - (lr / bc1) * m_new / (v_new.sqrt() / bc2s + eps)
-            if self.skip_flag is not None:
-                keep = self.skip_flag == 0
-                m_new = torch.where(keep, m_new, self.exp_avg)
-                v_new = torch.where(keep, v_new, self.exp_avg_sq)
-                p_new = torch.where(keep, p_new, a.data)
-            self.exp_avg.copy_(m_new)
-            self.exp_avg_sq.copy_(v_new)
-            a.data.copy_(p_new)
-            if self.shadow is not None:
-                self.shadow.copy_(a.data)
+            self._step_host(a)
         return loss
+
+    def _step_host(self, a: FlatArena) -> None:
+        """CPU update: one in-place pass of PyTorch's fused CPU Adam kernel over the flat arena (same
+        update as the HIP kernel: L2 weight decay, bias corrections at ``step_count``).  The skip
+        decision is a host bool here (a CPU tensor read, no device sync)."""
+        if skip_requested(self.skip_flag):
+            return
+        adam_update_host(self, a.data, a.grad, self.exp_avg, self.exp_avg_sq)
+        if self.shadow is not None:
+            self.shadow.copy_(a.data)
 
     @torch.no_grad()
     def set_nonfinite_skip(self) -> torch.Tensor:
@@ -129,7 +123,13 @@ class FusedAdam(torch.optim.Optimizer):
                       self._nf_ws[1024:].data_ptr(), _lib.stream_ptr(a.grad.device))
             self.skip_flag = self._nf_ws[1024:]
         else:
-            self.skip_flag = (~torch.isfinite(a.grad).all()).to(torch.int32).reshape(1)
+            # exact per-element test in one BLAS pass: grad . 0 is NaN iff some element is NaN / Inf (every
+            # finite product is exactly 0, so large finite gradients cannot overflow it, unlike a sum)
+            z = getattr(self, "_zero_vec", None)
+            if z is None or z.numel() != a.grad.numel() or z.dtype != a.grad.dtype:
+                z = self._zero_vec = torch.zeros_like(a.grad)
+            bad = not bool(torch.isfinite(torch.dot(a.grad, z)))
+            self.skip_flag = torch.tensor([1 if bad else 0], dtype=torch.int32)
         return self.skip_flag
 
     @torch.no_grad()
@@ -189,6 +189,21 @@ class FusedAdam(torch.optim.Optimizer):
             steps = int(float(s["step"]))
         self.step_count = steps
         self.sync_step_counter()
+
+
+def skip_requested(flag: Optional[torch.Tensor]) -> bool:
+    return flag is not None and bool(flag.reshape(-1)[0].item())
+
+
+def adam_update_host(opt: FusedAdam, p: torch.Tensor, g: torch.Tensor, m: torch.Tensor, v: torch.Tensor) -> None:
+    """In-place Adam on flat host tensors with ``opt``'s hyper-parameters (torch's fused CPU kernel)."""
+    lr, b1, b2, eps, wd, _, _, gs = opt._hparam_values()
+    grad = g if gs == 1.0 else g * gs
+    if getattr(opt, "_host_step", None) is None:
+        opt._host_step = torch.zeros((), dtype=torch.float32)
+    opt._host_step.fill_(float(max(1, opt.step_count)))
+    torch._fused_adam_([p], [grad], [m], [v], [], [opt._host_step], amsgrad=False, lr=lr, beta1=b1, beta2=b2,
+                       weight_decay=wd, eps=eps, maximize=False)
 
 
 def make_optimizer(model: torch.nn.Module, lr: float = 2e-4, betas=(0.9, 0.999), eps: float = 1e-8,

@@ -38,3 +38,29 @@ def test_bench_two_ranks_cpu_gloo():
     assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
     # whole-job aggregate: N * B * steps / (max-over-ranks seconds)
     assert abs(d["value"] - 2 * 2 * 1000.0 / d["ms_per_step"]) / d["value"] < 0.02
+
+
+def test_bench_self_launches_ranks_cpu_gloo():
+    """Plain ``python bench.py --gpus 2`` (no launcher): the script starts the two ranks itself and reports
+    the real world size (the round driver may call it either way)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(OMP_NUM_THREADS="2", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--batch", "2", "--seq-len", "32"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo"
+    assert d["config"]["parallelism"] == "dp2" and d["config"]["global_batch"] == 4
+    assert d["dtype"] == "fp32" and "host" in d["data"]      # CPU rehearsal is labelled as such
+
+
+def test_bench_rejects_world_size_mismatch():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "1", "--warmup", "0",
+           "--batch", "2", "--seq-len", "32"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
+    assert not _json_lines(r.stdout)
