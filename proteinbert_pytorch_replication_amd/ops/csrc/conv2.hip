@@ -3,13 +3,9 @@
 // Reference: ProteinBERT/modules.py:124-147 (Conv1d C->C, k=9, dilation 1 and 5, padding "same",
 // each + GELU) and :205-212 (x + narrow + wide + broadcast(global->local), LayerNorm over (L, C)).
 //
-// Why a second form (conv.hip holds the LDS-weight-ring kernels): there, every workgroup stages all
-// 590 KB of both convs' weights through LDS (global -> VGPR -> ds_write -> barrier -> ds_read) for
-// only 256 positions; per weight step the LDS spends about as many cycles on those writes plus the
-// fragment reads as the MFMAs take, a barrier separates every step, and the 141 KB footprint allows
-// one workgroup per CU (MFMA busy ~25 %, profiles/r1_hip_v5_*).
-//
-// Here the weights are re-packed once per step (pbx_pack_conv_frag, 2 x 295 KB bf16) into the exact
+// Why weights are streamed (the round-1 form staged all 590 KB of both convs' weights through LDS:
+// global -> VGPR -> ds_write -> barrier -> ds_read for only 256 positions, a barrier every weight
+// step and one workgroup per CU, MFMA busy ~25 %, profiles/r1_hip_v5_*): here the weights are re-packed once per step (pbx_pack_conv_frag, 2 x 295 KB bf16) into the exact
 // per-lane order of a v_mfma_f32_32x32x16_bf16 A operand, so one wave loads a whole 32x16 fragment
 // with ONE coalesced 1-KB global_load_dwordx4 (an L2 hit: every XCD keeps the 0.6 MB resident).
 // Only the activation tile lives in LDS; the main loop has no barrier and no LDS writes, each wave
@@ -55,14 +51,14 @@ __device__ __forceinline__ int tile_id() {
 // K = output channel.
 __device__ __forceinline__ int frag_index(int k, int kb, int mb) { return (k * 8 + kb) * 4 + mb; }
 
-// TBM = positions per workgroup: 128 (two workgroups per CU, <= 128 VGPRs) or 256 (one workgroup per
-// CU, 8 accumulators per wave: every weight fragment fetched from L2 feeds 8 MFMAs instead of 4)
-template <int TBM, int MINB>
-__global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
+// TBM = 128 positions per workgroup: two workgroups per CU at <= 128 VGPRs (a 256-position form, one
+// workgroup per CU with every weight fragment feeding 8 MFMAs, measured slower in the full step)
+__global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
     bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
-    float* __restrict__ stats, float* __restrict__ colsum, int L, int KS, int dil) {
+    float* __restrict__ stats, int L, int KS, int dil) {
+  constexpr int TBM = BM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
   constexpr int TOT = TBM * 256;                              // bytes of one [TBM][128] bf16 tile
@@ -89,10 +85,7 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   fr[0] = fw[lane];
   fr[1] = fw[256 + lane];
   fr[2] = fw[512 + lane];
-  // gb == nullptr ("late gb"): s1 is stored without the broadcast global->local vector, which its
-  // consumers add (the global track of the previous block may still be running beside this kernel)
-  if (tid < 3 * CH)
-    bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : (gb != nullptr ? gb[(size_t)b * CH + tid - 2 * CH] : 0.f);
+  if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
   stage_chunks(
       XR * 16,
       [&](int idx) {
@@ -159,7 +152,6 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
   // plain (sum, sum of squares) of the stored bf16 values -- per row, masked once -- merged to
   // (mean, M2) by one thread at the end (the per-thread / per-lane Chan merges cost a division each)
   f32x2 s2v = {0.f, 0.f};                          // (sum, sum of squares)
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // channel sums of this thread's rows
   const float4 g0 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8);
   const float4 g1 = *reinterpret_cast<const float4*>(bsm + 2 * CH + (tid & 15) * 8 + 4);
   const f32x2 gbp[4] = {(f32x2){g0.x, g0.y}, (f32x2){g0.z, g0.w}, (f32x2){g1.x, g1.y}, (f32x2){g1.z, g1.w}};
@@ -207,37 +199,13 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
       rs += (f32x2){pv.x + pv.y, pv.x * pv.x + pv.y * pv.y};
     }
     s2v += ok ? rs : (f32x2){0.f, 0.f};
-    if (colsum != nullptr) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) csum[e] += ok ? orr[e] : 0.f;
-    }
   }
   float* scratch = bsm + 3 * CH;                  // 8 waves x (sum, sum of squares)
   {
     const float sa = wave_reduce_sum(s2v.x), sq = wave_reduce_sum(s2v.y);
     if (lane == 0) { scratch[2 * w] = sa; scratch[2 * w + 1] = sq; }
   }
-  float* cpart = reinterpret_cast<float*>(ot);    // [8 waves][128] channel partials (ot is free after the loop)
-  if (colsum != nullptr) {
-    // lanes l, l^16, l^32, l^48 share the 8-channel chunk (l & 15)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      csum[e] += __shfl_xor(csum[e], 16, 64);
-      csum[e] += __shfl_xor(csum[e], 32, 64);
-    }
-    __syncthreads();                              // every wave is done reading the ot tile
-    if (lane < 16) {
-      *reinterpret_cast<float4*>(cpart + w * CH + lane * 8) = make_float4(csum[0], csum[1], csum[2], csum[3]);
-      *reinterpret_cast<float4*>(cpart + w * CH + lane * 8 + 4) = make_float4(csum[4], csum[5], csum[6], csum[7]);
-    }
-  }
   __syncthreads();
-  if (colsum != nullptr && tid < CH) {
-    float a = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a += cpart[i * CH + tid];
-    colsum[((size_t)b * T + t) * CH + tid] = a;
-  }
   if (tid == 0) {
     float sa = 0.f, sq = 0.f;
 #pragma unroll
@@ -250,17 +218,10 @@ __global__ void __launch_bounds__(512, MINB) conv_fwd3_kernel(
 
 // ------------------------------------------------------------------------------------------------
 // data gradient: D[ci][pos] = sum_conv sum_tap sum_co W[co][ci][tap] * dpre_conv[pos - shift][co]
-//
-// LNIN (reference semantics): the kernel's `ds1` argument is dh1, the gradient at the LayerNorm-1 OUTPUT,
-// and the LN1 backward runs here, in the prologue (halo rows included) and again in the epilogue:
-//   ds1 = rstd1 (dh1 g1 - m1 - xhat1 m2),  xhat1 = (s1 - mean1) rstd1,   c1[b] = (mean1, rstd1, m1, m2)
-// (pbx_ln1_consts), and the epilogue adds the tile's sum_l ds1 into dgb[b] (gradient of the broadcast
-// global->local vector, modules.py:208-211).  This replaces the separate LN1-finalize pass, which read
-// dh1 and s1 and wrote ds1 only for this kernel to read it back (3 x [B, L, 128] bf16 per block).
-template <bool LNIN>
+// (Running the LayerNorm-1 backward inside this kernel's prologue instead of the separate finalize pass
+// measured 1.5-3 % slower on the step: the prologue is load-latency bound, profiles/r2_v8_ln1_fuse_ab.txt.)
 __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
-    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ s1, const float* __restrict__ g1,
-    const float* __restrict__ c1, float* __restrict__ dgb, const bf16_t* __restrict__ pre_n,
+    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ pre_n,
     const bf16_t* __restrict__ pre_w, const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw,
     bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -283,16 +244,6 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   fr[0] = fw[lane];
   fr[1] = fw[256 + lane];
   fr[2] = fw[512 + lane];
-  float4 lnc = make_float4(0.f, 0.f, 0.f, 0.f);      // (mean1, rstd1, m1, m2) of sample b
-  if (LNIN) lnc = *reinterpret_cast<const float4*>(c1 + (size_t)b * 4);
-  // LN1 backward of one 8-channel chunk: g = dh1 on entry, ds1 on exit (sq: s1 chunk, ga: g1 chunk)
-  auto ln1_bwd8 = [&](float* g, const uint4& sq, const float4& ga0, const float4& ga1) {
-    float sv[8];
-    unpack8(sq, sv);
-    const float gam[8] = {ga0.x, ga0.y, ga0.z, ga0.w, ga1.x, ga1.y, ga1.z, ga1.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) g[e] = lnc.y * (g[e] * gam[e] - lnc.z - (sv[e] - lnc.x) * lnc.y * lnc.w);
-  };
 
   // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
 #pragma unroll 1
@@ -303,8 +254,7 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     unsigned char* tile = c ? aw : an;
     const int nch = (BM + 2 * halo) * 16;
     for (int base = tid; base < nch; base += 2 * 512) {
-      uint4 gq[2], pq[2], sq[2];
-      float4 ga[2][2];
+      uint4 gq[2], pq[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int idx = base + i * 512;
@@ -313,13 +263,6 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         const size_t off = sbase + (size_t)pos * CH + (idx & 15) * 8;
         gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
         pq[i] = ok ? *reinterpret_cast<const uint4*>(pre + off) : make_uint4(0u, 0u, 0u, 0u);
-        if (LNIN) {
-          const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-          const float* gp = g1 + (size_t)min(max(pos, 0), L - 1) * CH + (idx & 15) * 8;
-          sq[i] = ok ? *reinterpret_cast<const uint4*>(s1 + off) : make_uint4(0u, 0u, 0u, 0u);
-          ga[i][0] = ok ? *reinterpret_cast<const float4*>(gp) : z;
-          ga[i][1] = ok ? *reinterpret_cast<const float4*>(gp + 4) : z;
-        }
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -329,7 +272,6 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         const int pos = pos0 - halo + j;
         float g[8], pv[8], o[8];
         unpack8(gq[i], g);
-        if (LNIN) ln1_bwd8(g, sq[i], ga[i][0], ga[i][1]);
         unpack8(pq[i], pv);
         // GELU' of the 8 values as interleaved scalar A&S stages (gelu_scalar_n, as in the forward)
         f32x2 pp[4], gd[4];
@@ -401,7 +343,6 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
       }
   }
   __syncthreads();
-  float dgs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};   // LNIN: this thread's sum_l ds1 (chunk tid & 15)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int idx = tid + 512 * i;
@@ -410,39 +351,12 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     const size_t off = sbase + (size_t)(pos0 + row) * CH + c * 8;
     float gv[8], o[8];
     unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
-    if (LNIN) {
-      const float* gp = g1 + (size_t)(pos0 + row) * CH + c * 8;
-      ln1_bwd8(gv, *reinterpret_cast<const uint4*>(s1 + off), *reinterpret_cast<const float4*>(gp),
-               *reinterpret_cast<const float4*>(gp + 4));
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dgs[e] += gv[e];
-    }
     const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c));
     const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c + 1));
     const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
     *reinterpret_cast<uint4*>(dx + off) = packq8(o);
-  }
-  if (LNIN) {
-    // lanes l, l^16, l^32, l^48 own the same chunk; then the 8 waves through LDS (ft is free now)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      dgs[e] += __shfl_xor(dgs[e], 16, 64);
-      dgs[e] += __shfl_xor(dgs[e], 32, 64);
-    }
-    __syncthreads();                              // every thread is done reading ft
-    if (lane < 16) {
-      *reinterpret_cast<float4*>(ft + w * CH + lane * 8) = make_float4(dgs[0], dgs[1], dgs[2], dgs[3]);
-      *reinterpret_cast<float4*>(ft + w * CH + lane * 8 + 4) = make_float4(dgs[4], dgs[5], dgs[6], dgs[7]);
-    }
-    __syncthreads();
-    if (tid < CH) {
-      float a = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) a += ft[k * CH + tid];
-      atomicAdd(dgb + (size_t)b * CH + tid, a);
-    }
   }
 }
 
@@ -473,40 +387,24 @@ int dgrad3_lds(int KS, int dil) {
 static bool conv3_attrs_set = false;
 static void set_conv3_attrs() {
   if (conv3_attrs_set) return;
-  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<128, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<256, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   conv3_attrs_set = true;
 }
 
-// LayerNorm partials in `stats` are per tbm-position tile: [B][ceil(L/tbm)][2] (tbm = 128 or 256).  fwn/fww: forward
-// fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels.
-// gb may be null ("late gb": s1 without the broadcast vector); colsum (nullable): [B][ceil(L/tbm)][128]
-// channel sums of the stored s1 per tile, for the exact LayerNorm statistics once gb is known
-PBX_EXPORT int pbx_conv_fwd3x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, float* colsum, int B,
-                              int L, int KS, int dil, int tbm, hipStream_t st) {
-  set_conv3_attrs();
-  if (tbm != 128 && tbm != 256) return (int)hipErrorInvalidValue;
-  const int lds = fwd3_lds(KS, dil, tbm);
-  if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
-  const int T = (L + tbm - 1) / tbm;
-  if (tbm == 256)
-    hipLaunchKernelGGL((conv_fwd3_kernel<256, 2>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
-                       (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
-                       (bf16_t*)s1, stats, colsum, L, KS, dil);
-  else
-    hipLaunchKernelGGL((conv_fwd3_kernel<128, 4>), dim3(B * T), dim3(512), lds, st, (const bf16_t*)x,
-                       (const bf16x8*)fwn, (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w,
-                       (bf16_t*)s1, stats, colsum, L, KS, dil);
-  return pbx_launch_status();
-}
-
+// LayerNorm partials in `stats` are per 128-position tile: [B][ceil(L/128)][2].  fwn/fww: forward
+// fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels; gb [B][128] fp32.
+// pre_n / pre_w may be null (inference: no backward reads them).
 PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
-                             int dil, int tbm, hipStream_t st) {
-  return pbx_conv_fwd3x(x, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, nullptr, B, L, KS, dil, tbm, st);
+                             int dil, hipStream_t st) {
+  set_conv3_attrs();
+  const int lds = fwd3_lds(KS, dil, BM);
+  if (lds > 163840 || dil < 1 || KS < 2 || gb == nullptr) return (int)hipErrorInvalidValue;
+  const int T = (L + BM - 1) / BM;
+  hipLaunchKernelGGL(conv_fwd3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
+                     (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
+  return pbx_launch_status();
 }
 
 PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* pre_w, const void* ftn,
@@ -516,24 +414,9 @@ PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* p
   const int lds = dgrad3_lds(KS, dil);
   if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
   const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_dgrad3_kernel<false>, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1, nullptr,
-                     nullptr, nullptr, nullptr, (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn,
-                     (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
-  return pbx_launch_status();
-}
-
-// reference semantics: dh1 (gradient at the LN1 output) in, the LN1 backward fused (see conv_dgrad3_kernel);
-// c1: [B][4] from pbx_ln1_consts; dgb [B][128] fp32 is accumulated into
-PBX_EXPORT int pbx_conv_dgrad3_ln(const void* dh1, const void* s1, const float* g1, const float* c1, float* dgb,
-                                  const void* pre_n, const void* pre_w, const void* ftn, const void* ftw, void* dx,
-                                  void* dpre_n, void* dpre_w, int B, int L, int KS, int dil, hipStream_t st) {
-  set_conv3_attrs();
-  const int lds = dgrad3_lds(KS, dil);
-  if (lds > 163840 || dil < 1 || KS < 2 || lds < 8 * CH * 4) return (int)hipErrorInvalidValue;
-  const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_dgrad3_kernel<true>, dim3(B * T), dim3(512), lds, st, (const bf16_t*)dh1,
-                     (const bf16_t*)s1, g1, c1, dgb, (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn,
-                     (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
+  hipLaunchKernelGGL(conv_dgrad3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1,
+                     (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn, (const bf16x8*)ftw,
+                     (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
   return pbx_launch_status();
 }
 

@@ -1,0 +1,308 @@
+// In-tree MFMA GEMMs for the small / skinny library-shaped products of ProteinBERT:
+// the [B, 8943] x [8943, 512] GO-input and GO-output products, their weight gradients (a K = B
+// reduction) and the global-track weight gradients dW = dU^T X.  hipBLASLt ran these at 10-66 us
+// per call (profiles/r2_v8_concurrent_steps.txt); they are M,N <= 9k, K <= 9k, bf16 operands with
+// fp32 accumulation.
+//
+//   C[M][N] (+)= sum_k op(A)[m][k] op(B)[k][n]
+//   TA = 0: A[m][k] = A[m * lda + k]     TA = 1: A[m][k] = A[k * lda + m]
+//   TB = 0: B[k][n] = B[k * ldb + n]     TB = 1: B[k][n] = B[n * ldb + k]
+//
+// Tile 128 x 128 per workgroup (4 waves, 64 x 64 each = 2 x 2 v_mfma_f32_32x32x16_bf16 tiles), K in
+// chunks of 128.  Both operands are staged through LDS as 256-B-row swizzled tiles (mfma.h swz256):
+// the operand whose K runs along memory is stored [m|n][k] and read by rows (ds_read_b128); the other
+// is stored [k][m|n] and read transposed (ds_read_b64_tr_b16), so every layout is one coalesced 16-B
+// global load per lane and conflict-free LDS reads.  The next K chunk is loaded into registers while
+// the current one is in the MFMAs.  Split-K (grid.z) writes fp32 partial slabs that pbx_gemm_reduce
+// sums in a fixed order: every result is deterministic (no float atomics).
+//
+// EPI_GO: the GO-annotation head of the reference loss fused into the GEMM epilogue
+// (ProteinBERT/modules.py:286-293, utils.py:294): z = acc + bias, p = sigmoid(z), BCE(p, y) with
+// PyTorch's log clamp (>= -100), weighted by w[b] / (B A); writes dz = dL/dz (bf16, the operand of
+// the backward GEMMs), per-(row tile, column) partial sums of dz (the bias gradient, folded by the
+// caller) and per-workgroup loss partials.  z itself is never stored.
+#include "mfma.h"
+
+using namespace pbx;
+typedef unsigned short bf16_t;
+
+namespace {
+constexpr int BT = 128;   // tile rows / cols
+constexpr int BK = 128;   // K chunk
+constexpr int TILE = BT * 256;   // bytes of one staged operand tile
+
+enum { EPI_STORE = 0, EPI_GO = 1 };
+
+struct GoArgs {
+  const float* bias;      // [N]
+  const float* y;         // [M][ldy] targets
+  long ldy;
+  const float* wrow;      // per-row weight (w[b]) ...
+  const float* wfull;     // ... or a full [M][ldy] weight (one of the two)
+  bf16_t* dz;             // [M][lddz]
+  long lddz;
+  float* dbias_part;      // [ceil(M / BT)][N]
+  float* loss_part;       // [gridDim.x * gridDim.y]
+  float inv_mn;           // 1 / (M N)
+};
+
+// One operand tile (rows r0.., K chunk k0..) into LDS.  KMAJ: K runs along memory (A row / B col) ->
+// LDS [row][k]; else -> LDS [k][row].  ALIGNED: 16-B vector loads (ld % 8 == 0, 16-B base).
+template <bool KMAJ, bool ALIGNED>
+struct Stager {
+  uint4 v[8];   // 2048 16-B chunks per tile / 256 threads
+  __device__ __forceinline__ void load(const bf16_t* __restrict__ p, long ld, int rows, int K, int r0, int k0) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      const int a = idx >> 4, c = (idx & 15) * 8;   // LDS row a, 8-element chunk c
+      // KMAJ: row = r0 + a, k = k0 + c.. ; else: k = k0 + a, row = r0 + c..
+      const int row = KMAJ ? r0 + a : r0 + c;
+      const int kk = KMAJ ? k0 + c : k0 + a;
+      if (ALIGNED) {
+        const bool ok = KMAJ ? (row < rows && kk < K) : (kk < K && row < rows);
+        // the chunk is entirely valid or entirely outside (rows / K multiples of 8 on this path)
+        v[i] = ok ? *reinterpret_cast<const uint4*>(p + (KMAJ ? (size_t)row * ld + kk : (size_t)kk * ld + row))
+                  : make_uint4(0u, 0u, 0u, 0u);
+      } else {
+        unsigned short e[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int rr = KMAJ ? row : row + j, kj = KMAJ ? kk + j : kk;
+          e[j] = (rr < rows && kj < K) ? p[KMAJ ? (size_t)rr * ld + kj : (size_t)kj * ld + rr] : (unsigned short)0;
+        }
+        v[i] = make_uint4(e[0] | (unsigned)e[1] << 16, e[2] | (unsigned)e[3] << 16, e[4] | (unsigned)e[5] << 16,
+                          e[6] | (unsigned)e[7] << 16);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* t) const {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int idx = threadIdx.x + 256 * i;
+      *reinterpret_cast<uint4*>(t + swz256(idx >> 4, idx & 15)) = v[i];
+    }
+  }
+};
+
+// MFMA operand fragment of row/col block `blk` (32 wide) at k-step kk from a staged tile
+template <bool KMAJ>
+__device__ __forceinline__ bf16x8 frag(const unsigned char* t, int blk, int kk, int r, int h, int q, int tc) {
+  if (KMAJ) return lds_frag(t, swz256(blk * 32 + r, kk * 2 + h));
+  const int rlo = kk * 16 + 8 * h + q;
+  const int col = blk * 32 + tc;
+  return cat_tr(lds_tr(t, swz256e(rlo, col)), lds_tr(t, swz256e(rlo + 4, col)));
+}
+
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_reduce_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
+__global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B,
+                                                      long ldb, float* __restrict__ C, long ldc, int M, int N, int K,
+                                                      int kchunks_per_split, int accumulate, GoArgs go) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + TILE;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
+  const int nkc = (K + BK - 1) / BK;
+  const int kc0 = blockIdx.z * kchunks_per_split;
+  const int kc1 = min(nkc, kc0 + kchunks_per_split);
+  constexpr bool AK = TA == 0, BKM = TB == 1;     // K runs along memory
+  Stager<AK, AL_A> sa;
+  Stager<BKM, AL_B> sb;
+  f32x16_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = zero16();
+  if (kc0 < kc1) {
+    sa.load(A, lda, M, K, m0, kc0 * BK);
+    sb.load(B, ldb, N, K, n0, kc0 * BK);
+  }
+  for (int kc = kc0; kc < kc1; ++kc) {
+    __syncthreads();                       // previous chunk's fragments consumed
+    sa.store(As);
+    sb.store(Bs);
+    __syncthreads();
+    if (kc + 1 < kc1) {                    // next chunk in flight during the MFMAs
+      sa.load(A, lda, M, K, m0, (kc + 1) * BK);
+      sb.load(B, ldb, N, K, n0, (kc + 1) * BK);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const bf16x8 a0 = frag<AK>(As, wm * 2, kk, r, h, q, tc), a1 = frag<AK>(As, wm * 2 + 1, kk, r, h, q, tc);
+      const bf16x8 b0 = frag<BKM>(Bs, wn * 2, kk, r, h, q, tc), b1 = frag<BKM>(Bs, wn * 2 + 1, kk, r, h, q, tc);
+      acc[0][0] = mfma32(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32(a1, b1, acc[1][1]);
+    }
+  }
+  // D layout: lane (r, h), register e -> row (e & 3) + 8 (e >> 2) + 4 h, column r of each 32 x 32 tile
+  if constexpr (EPI == EPI_STORE) {
+    float* dst = C + (size_t)blockIdx.z * M * ldc;   // split-K slab (z > 0 only when gridDim.z > 1)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = n0 + wn * 64 + j * 32 + r;
+        if (n >= N) continue;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m < M) {
+            float* c = dst + (size_t)m * ldc + n;
+            *c = accumulate ? *c + acc[i][j][e] : acc[i][j][e];
+          }
+        }
+      }
+  } else {
+    // GO head: one thread per (row, column); the column's bias gradient over this tile's 128 rows is
+    // summed through LDS (two wm halves), the loss over the whole tile
+    float* red = reinterpret_cast<float*>(smem);     // reuse the staging tiles: [2][128] dbias + 4
+    __syncthreads();
+    float lsum = 0.f;
+    float dcol[2] = {0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + r;
+      const bool okn = n < N;
+      const float bc = okn ? go.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+          if (m >= M) continue;
+          if (!okn) {                                // zero pad columns: dz feeds 16-B padded loads
+            if (n < go.lddz) go.dz[(size_t)m * go.lddz + n] = 0;
+            continue;
+          }
+          const float zz = acc[i][j][e] + bc;
+          const float p = 1.0f / (1.0f + __expf(-zz));
+          const float yy = go.y[(size_t)m * go.ldy + n];
+          const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.0f - p), -100.f);
+          const float wgt = go.wrow != nullptr ? go.wrow[m] : go.wfull[(size_t)m * go.ldy + n];
+          lsum += wgt * -(yy * lp + (1.0f - yy) * l1p) * go.inv_mn;
+          const float pq = p * (1.0f - p);
+          const float g = wgt * go.inv_mn * (p - yy) * pq / fmaxf(pq, 1e-12f);
+          const bf16_t gb = f2bf(g);
+          go.dz[(size_t)m * go.lddz + n] = gb;
+          dcol[j] += bf2f(gb);
+        }
+    }
+    // column sums: lanes r and r + 32 hold the same column (h halves), then the two wm halves
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dcol[j] += __shfl_xor(dcol[j], 32, 64);
+    if (h == 0) {
+      red[wm * 128 + wn * 64 + r] = dcol[0];
+      red[wm * 128 + wn * 64 + 32 + r] = dcol[1];
+    }
+    __syncthreads();
+    if (tid < BT) {
+      const int n = n0 + tid;
+      if (n < N) go.dbias_part[(size_t)blockIdx.y * N + n] = red[tid] + red[128 + tid];
+    }
+    __syncthreads();
+    const float lt = block_sum256(lsum, red + 256);
+    if (tid == 0) go.loss_part[blockIdx.y * gridDim.x + blockIdx.x] = lt;
+  }
+}
+
+// C[m][n] (+)= sum_z slab[z][m][n]  (fixed order)
+__global__ void __launch_bounds__(256) gemm_reduce_kernel(const float* __restrict__ slab, int S, float* __restrict__ C,
+                                                          long ldc, int M, int N, int accumulate) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n4 = (N + 3) / 4;
+  if (idx >= (long)M * n4) return;
+  const int m = (int)(idx / n4), n = (int)(idx - (idx / n4) * n4) * 4;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int z = 0; z < S; ++z) {
+    const float* p = slab + ((size_t)z * M + m) * N + n;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[e] += n + e < N ? p[e] : 0.f;
+  }
+  float* c = C + (size_t)m * ldc + n;
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    if (n + e < N) c[e] = accumulate ? c[e] + s[e] : s[e];
+}
+
+template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
+int launch(const void* A, long lda, const void* B, long ldb, float* C, long ldc, int M, int N, int K, int splitk,
+           int accumulate, const GoArgs& go, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_kernel<TA, TB, AL_A, AL_B, EPI>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * TILE);
+    attr = true;
+  }
+  const int nkc = (K + BK - 1) / BK;
+  const int per = (nkc + splitk - 1) / splitk;
+  const int sk = (nkc + per - 1) / per;   // no empty splits
+  dim3 grid((N + BT - 1) / BT, (M + BT - 1) / BT, sk);
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, AL_A, AL_B, EPI>), grid, dim3(256), 2 * TILE, st, (const bf16_t*)A, lda,
+                     (const bf16_t*)B, ldb, C, ldc, M, N, K, per, accumulate, go);
+  return pbx_launch_status();
+}
+
+template <int TA, int TB, int EPI>
+int dispatch_al(bool aa, bool ab, const void* A, long lda, const void* B, long ldb, float* C, long ldc, int M, int N,
+                int K, int splitk, int accumulate, const GoArgs& go, hipStream_t st) {
+  if (aa && ab) return launch<TA, TB, true, true, EPI>(A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  if (aa) return launch<TA, TB, true, false, EPI>(A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  if (ab) return launch<TA, TB, false, true, EPI>(A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  return launch<TA, TB, false, false, EPI>(A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+}
+
+// 16-B vector loads are legal when the base is 16-B aligned and the leading dimension and the extent
+// along the contiguous axis are multiples of 8 elements (a chunk is then wholly in or out of range),
+// or the caller guarantees the contiguous axis is zero-padded to a multiple of 8 (`padded`)
+bool aligned(const void* p, long ld, int contig_extent, bool padded) {
+  return ((size_t)p & 15) == 0 && ld % 8 == 0 && (padded || contig_extent % 8 == 0);
+}
+}  // namespace
+
+// C (+)= op(A) op(B); splitk > 1: C must be a [splitk][M][N] fp32 scratch slab (ldc = N), then
+// pbx_gemm_reduce folds it.  ta / tb: 0 / 1 as in the header comment.  pad bit 0 / 1: A / B is
+// zero-padded along its contiguous axis to a multiple of 8 elements (16-B loads may read the pad).
+PBX_EXPORT int pbx_gemm(const void* A, long lda, int ta, const void* B, long ldb, int tb, float* C, long ldc, int M, int N,
+                        int K, int splitk, int accumulate, int pad, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || splitk < 1 || (splitk > 1 && ldc != N)) return (int)hipErrorInvalidValue;
+  const GoArgs go{};
+  const bool aa = aligned(A, lda, ta == 0 ? K : M, pad & 1), ab = aligned(B, ldb, tb == 1 ? K : N, pad & 2);
+  if (ta == 0 && tb == 0) return dispatch_al<0, 0, EPI_STORE>(aa, ab, A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  if (ta == 0 && tb == 1) return dispatch_al<0, 1, EPI_STORE>(aa, ab, A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  if (ta == 1 && tb == 0) return dispatch_al<1, 0, EPI_STORE>(aa, ab, A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+  return dispatch_al<1, 1, EPI_STORE>(aa, ab, A, lda, B, ldb, C, ldc, M, N, K, splitk, accumulate, go, st);
+}
+
+PBX_EXPORT int pbx_gemm_reduce(const float* slab, int S, float* C, long ldc, int M, int N, int accumulate,
+                               hipStream_t st) {
+  const long n = (long)M * ((N + 3) / 4);
+  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slab, S, C, ldc, M, N,
+                     accumulate);
+  return pbx_launch_status();
+}
+
+// Fused GO head (reference semantics): x [M = B][K = G] bf16 row-major, w [N = A][K] bf16 (the head
+// weight's bf16 mirror), bias [A] fp32, y [B][ldy] fp32 targets, weights per row (wrow) or full
+// (wfull, [B][ldy]).  Outputs: dz [B][lddz] bf16 (columns A .. lddz zeroed), dbias_part
+// [ceil(B / 128)][A], loss_part [ceil(B / 128) ceil(A / 128)] (each already divided by B A).
+PBX_EXPORT int pbx_go_head_fused(const void* x, long ldx, const void* w, long ldw, const float* bias, const float* y,
+                                 long ldy, const float* wrow, const float* wfull, void* dz, long lddz, float* dbias_part,
+                                 float* loss_part, int M, int N, int K, hipStream_t st) {
+  if (M <= 0 || N <= 0 || K <= 0 || (wrow == nullptr) == (wfull == nullptr)) return (int)hipErrorInvalidValue;
+  GoArgs go{bias, y, ldy, wrow, wfull, (bf16_t*)dz, lddz, dbias_part, loss_part, 1.0f / ((float)M * (float)N)};
+  const bool aa = aligned(x, ldx, K, false), ab = aligned(w, ldw, K, false);
+  return dispatch_al<0, 1, EPI_GO>(aa, ab, x, ldx, w, ldw, nullptr, 0, M, N, K, 1, 0, go, st);
+}

@@ -131,8 +131,7 @@ __device__ __forceinline__ void sample_stats(float* sh, const float* __restrict_
 __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1, const float* __restrict__ g1,
     const float* __restrict__ be1, const bf16_t* __restrict__ wl, const float* __restrict__ bl,
-    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, const float* __restrict__ gb,
-    const float* __restrict__ cs1, float* __restrict__ st1f, int B, int L, float eps) {
+    bf16_t* __restrict__ pre_l, bf16_t* __restrict__ s2, float* __restrict__ st2, int B, int L, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* ht = smem + 32768;                                  // h1 tile bf16, PB x 256 B
@@ -149,20 +148,12 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
   const int nb = b1 - b0;
   float* part = tab + 2 * nb;
   stage_weight(ws, wl, CH);
-  // gb != nullptr ("late gb"): s1 was stored without the broadcast global->local vector; the
-  // statistics of s1 + gb come from the s1 tile partials, their channel sums cs1 and gb
   for (int i = w; i < nb; i += 8) {
     float mean, rstd;
-    const int bi = b0 + i;
-    if (gb != nullptr)
-      wave_ln_stats_gb(st1 + (size_t)bi * T1 * 2, T1, BM1, L, cs1 + (size_t)bi * T1 * CH, gb + (size_t)bi * CH, eps,
-                       mean, rstd);
-    else
-      wave_ln_stats(st1 + (size_t)bi * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
+    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
     if (lane == 0) {
       tab[2 * i] = mean;
       tab[2 * i + 1] = rstd;
-      if (st1f != nullptr && blockIdx.x == 0) { st1f[2 * bi] = mean; st1f[2 * bi + 1] = rstd; }
     }
   }
   float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bb[8];
@@ -178,12 +169,6 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const float mean = tab[2 * i], rstd = tab[2 * i + 1];
     float sv[8], h1[8];
     unpack8(nxt, sv);
-    if (gb != nullptr) {
-      float gv[8];
-      load_f8(gb + (size_t)b * CH + ch * 8, gv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) sv[e] += gv[e];
-    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) h1[e] = okl ? (sv[e] - mean) * rstd * gam[e] + bet[e] : 0.f;
     *reinterpret_cast<uint4*>(ht + swz256(j, ch)) = packq8(h1);
@@ -217,7 +202,7 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const uint4 oq = packq8(o);
     if (okl) {
       const size_t off = ((size_t)b * L + l) * CH + ch * 8;
-      if (pre_l != nullptr) *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);   // null: recomputed
+      if (pre_l != nullptr) *reinterpret_cast<uint4*>(pre_l + off) = packq8(pre);   // null: no backward
       *reinterpret_cast<uint4*>(s2 + off) = oq;
     }
     // (sum, sum of squares) of the stored values, reduced over the wave into the LDS partial table
@@ -247,18 +232,6 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = m;
     st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
   }
-}
-
-// 8 chained MFMAs: D[j][pos] (A = Wv rows jt*32.., B = h2 fragments) or D[pos][j] (swapped)
-template <bool POS_ROWS>
-__device__ __forceinline__ f32x16_t wv_chain(const unsigned char* ws, const bf16x8* hf, int jt, int r, int h) {
-  f32x16_t acc = zero16();
-#pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const bf16x8 wf = lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h));
-    acc = POS_ROWS ? mfma32(hf[kk], wf, acc) : mfma32(wf, hf[kk], acc);
-  }
-  return acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -336,160 +309,11 @@ __global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
-// attention pool backward + LayerNorm-2 backward partials.
-// dP[j][pos] = dv[b][t][j] * GELU'(Wv[j] . h2[pos]) ; dh2 = dh2_in + Wv^T dP  (dP never leaves
-// registers: the 32x32 accumulator of the recompute is the B operand of the second MFMA).
-// Work items are 32-position wave tiles taken by each wave independently (no workgroup barrier
-// after the Wv staging, so the waves of a CU drift apart and one wave's loads overlap another's
-// MFMAs), and the LN2 partials are written per wave tile: sums2[b][ceil(L/32)][2].
-template <int MAXT>   // 512: 8 waves at <= 256 VGPRs; 256: 4 waves (one per SIMD) at <= 512 VGPRs
-__global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
-    const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
-    const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, int NJ,
-    float eps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int q = tr_q(lane), tc = tr_c(lane);
-  const int NW = blockDim.x >> 6;
-  const int T2 = (L + BML - 1) / BML;
-  const int TW = (L + 31) / 32;
-  const int TV = (L + BMV - 1) / BMV;
-  const int NJT = NJ / 32;
-  const long items = (long)B * TW;
-  const long stride = (long)gridDim.x * NW;
-  auto load_rows = [&](long item, bf16x8* f) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos = tw * 32 + r;
-    const bool ok = pos < L;
-    const bf16_t* src = h2 + ((size_t)b * L + min(pos, L - 1)) * CH;     // clamped, unconditional loads
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const uint4 v = *reinterpret_cast<const uint4*>(src + kk * 16 + 8 * h);
-      f[kk] = __builtin_bit_cast(bf16x8, ok ? v : make_uint4(0u, 0u, 0u, 0u));
-    }
-  };
-  stage_weight(ws, wv, NJ);
-  __syncthreads();
-  for (long item = (long)blockIdx.x * NW + w; item < items; item += stride) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos0 = tw * 32;
-    const int pos = pos0 + r;
-    const bool okb = pos < L;
-    const size_t rowoff = ((size_t)b * L + pos) * CH;
-    bf16x8 hf[8];
-    load_rows(item, hf);
-    f32x16_t y[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    // this tile's attention-gradient row dv[NJ] -> the wave's LDS slot (2 loads per lane, once per
-    // tile, instead of 4 dependent global loads per 32-column block inside the loop)
-    const float* dvg = dvpart + ((size_t)b * TV + pos0 / BMV) * NJ;
-    float* dv = reinterpret_cast<float*>(ws + NJ * 256) + w * NJ;
-    for (int i = lane * 4; i < NJ; i += 256) *reinterpret_cast<float4*>(dv + i) = *reinterpret_cast<const float4*>(dvg + i);
-    __builtin_amdgcn_wave_barrier();
-    // positions beyond L get nonzero dP (GELU'(0) = 1/2) but only feed their own output columns,
-    // which are neither stored nor counted in the LN partials
-    auto proc = [&](const f32x16_t& d1, int jt) {
-      float dp[16];
-#pragma unroll
-      for (int hq = 0; hq < 4; ++hq) {
-        // rows 8 hq + 4 h .. +3 of this column block: dv read from the wave's LDS slot per group
-        float dvv[4];
-        load_f4(dv + jt * 32 + 8 * hq + 4 * h, dvv);
-        f32x2 xv[2], gv[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) xv[i] = (f32x2){d1[4 * hq + 2 * i], d1[4 * hq + 2 * i + 1]};
-        gelu2_fast_n<2, true>(xv, gv);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          dp[4 * hq + 2 * i] = gv[i].x * dvv[2 * i];
-          dp[4 * hq + 2 * i + 1] = gv[i].y * dvv[2 * i + 1];
-        }
-      }
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const bf16x8 fb = pack8(dp + 8 * s);
-        const int rlo = jt * 32 + 16 * s + 4 * h + q;
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const int col = ct * 32 + tc;
-          const bf16x8 fa = cat_tr(lds_tr(ws, swz256e(rlo, col)), lds_tr(ws, swz256e(rlo + 8, col)));
-          y[ct] = mfma32(fa, fb, y[ct]);
-        }
-      }
-    };
-    if (MAXT > 256) {
-      // 8 waves (<= 256 VGPRs): one recompute tile in flight; the other wave of the SIMD covers
-      // the chain latency
-      for (int jt = 0; jt < NJT; ++jt) proc(wv_chain<false>(ws, hf, jt, r, h), jt);
-    } else {
-      f32x16_t d0 = wv_chain<false>(ws, hf, 0, r, h);
-      for (int jt = 0; jt < NJT; jt += 2) {
-        const f32x16_t d1 = wv_chain<false>(ws, hf, jt + 1, r, h);
-        proc(d0, jt);
-        if (jt + 2 < NJT) d0 = wv_chain<false>(ws, hf, jt + 2, r, h);
-        proc(d1, jt + 1);
-      }
-    }
-    // Y[ci][pos]; LN2 backward partials of this wave tile
-    float mean, rstd;
-    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    float sa = 0.f, sc = 0.f;
-    {
-      // all operand loads first (clamped row, unconditional), then the math and masked stores
-      const int pc = min(pos, L - 1);
-      const size_t roff = ((size_t)b * L + pc) * CH;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        uint2 dq[4], sq[4];
-        float4 gq[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ci0 = ct * 32 + 8 * i + 4 * h;
-          dq[i] = dh2_in != nullptr ? *reinterpret_cast<const uint2*>(dh2_in + roff + ci0) : make_uint2(0u, 0u);
-          sq[i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
-          gq[i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
-        }
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int i = g;
-          const int ci0 = ct * 32 + 8 * g + 4 * h;
-          float din[4], sv[4], o[4];
-          unpack4(dq[i], din);
-          unpack4(sq[i], sv);
-          const float gg[4] = {gq[i].x, gq[i].y, gq[i].z, gq[i].w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o[e] = bfround(din[e] + y[ct][4 * g + e]);
-            const float xh = (sv[e] - mean) * rstd;
-            const float dxh = o[e] * gg[e];
-            sa += okb ? dxh : 0.f;
-            sc += okb ? dxh * xh : 0.f;
-          }
-          if (okb) *reinterpret_cast<uint2*>(dh2 + rowoff + ci0) = packq4(o);
-        }
-        // one channel tile's operands in flight at a time (hoisting all four needs 128 VGPRs)
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    sa = wave_reduce_sum(sa);
-    sc = wave_reduce_sum(sc);
-    if (lane == 0) {
-      sums2[((size_t)b * TW + tw) * 2] = sa;
-      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // Attention pool with the GELU derivative stored by the forward (v2).
 //
-// The backward of the pool needs GELU'(h2 Wv) at every (position, value column): the v1 backward
-// recomputes the [32 x 512] projection per tile (128 MFMAs) and evaluates GELU' (2 transcendentals
-// per element) just to multiply it by dv.  Here the forward evaluates GELU and GELU' from ONE shared
+// The backward of the pool needs GELU'(h2 Wv) at every (position, value column): recomputing it costs
+// the [32 x 512] projection per tile (128 MFMAs) plus GELU' (2 transcendentals per element), all to
+// multiply it by dv (the round-1 form; 1.6 % slower on the step).  Here the forward evaluates GELU and GELU' from ONE shared
 // erf/exp core, column-sums GELU as before and writes GELU' as bf16 in the exact per-lane order of
 // the backward's MFMA B operand (`gfrag`: [B][2 ceil(L/64)][NJ/32][2][64 lanes][8], one coalesced
 // 1-KB store / load per wave-instruction); the backward is then 128 MFMAs per 32-position tile fed
@@ -503,10 +327,9 @@ __global__ void __launch_bounds__(MAXT) attn_bwd_kernel(
 constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
 constexpr int GT_BYTES = 32 * GT_STRIDE;
 
-// NP: 32-position MFMA tiles per work item: 2 (64 positions, each Wv fragment read from LDS feeds two
-// MFMAs; ~248 VGPRs, two waves per SIMD) or 1 (32 positions; <= 168 VGPRs, three waves per SIMD, 12
-// waves per workgroup; vpart then has one row per 32-position tile)
-template <int NWAVE, int NI, int NP = 2>   // NI: GELU pairs interleaved per core call (4: one half-tile, 8: a tile, 16: both)
+// Work item: 64 positions (two 32-position MFMA tiles; each Wv fragment read from LDS feeds two MFMAs;
+// ~248 VGPRs, two waves per SIMD).  NI: GELU pairs interleaved per core call.
+template <int NWAVE, int NI>
 __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
@@ -520,7 +343,8 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
   const int NW = blockDim.x >> 6;
   const int T2 = (L + BML - 1) / BML;
   const int TW64 = (L + 63) / 64;
-  const int TW = NP == 2 ? TW64 : 2 * TW64;        // work items per sample
+  const int TW = TW64;                              // work items per sample
+  constexpr int NP = 2;                             // 32-position MFMA tiles per work item
   const int NJT = NJ / 32;
   const long items = (long)B * TW;
   stage_weight(ws, wv, NJ);
@@ -535,9 +359,9 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
       const int pa = pos0 + r;
       const int ca = min(pa, L - 1);
       const size_t ra = ((size_t)b * L + ca) * CH;
-      ln_row_frags<NP == 2 ? 8 : 4>(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h,
+      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h,
                                      h2 + ra);
-      if constexpr (NP == 2) {
+      {
         const int pb = pos0 + 32 + r;
         const int cb = min(pb, L - 1);
         const size_t rb = ((size_t)b * L + cb) * CH;
@@ -608,7 +432,7 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
 #pragma unroll
       for (int kk = 0; kk < 8; ++kk) {
         c0 = mfma32(hf0[kk], wf[kk], c0);
-        if constexpr (NP == 2) c1 = mfma32(hf1[kk], wf[kk], c1);
+        c1 = mfma32(hf1[kk], wf[kk], c1);
       }
       if (jt + 1 < NJT) {
 #pragma unroll
@@ -793,7 +617,7 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
                                                          const float* __restrict__ sums2, int TS2,
                                                          const float* __restrict__ st1, int T1, int BM1,
                                                          float* __restrict__ consts, float* __restrict__ zero128,
-                                                         const float* __restrict__ st1f, int B, int L, float eps) {
+                                                         int B, int L, float eps) {
   const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (b >= B) return;
   // zero row b of the [B, 128] accumulator the LN1 finalize adds into (saves a fill launch per block)
@@ -802,12 +626,7 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
   float mean2, rstd2, m1, m2, mean1, rstd1;
   wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BM2, L, CH, eps, mean2, rstd2);
   wave_bwd_consts(sums2 + (size_t)b * TS2 * 2, TS2, 1.0f / (float)(L * CH), m1, m2);
-  if (st1f != nullptr) {          // final (mean, rstd) of LN1 written by the forward (late gb)
-    mean1 = st1f[2 * b];
-    rstd1 = st1f[2 * b + 1];
-  } else {
-    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
-  }
+  wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
   if ((threadIdx.x & 63) == 0) {
     float4* c = reinterpret_cast<float4*>(consts + (size_t)b * 8);
     c[0] = make_float4(mean2, rstd2, m1, m2);
@@ -824,19 +643,15 @@ __global__ void __launch_bounds__(256) ln2_consts_kernel(const float* __restrict
 // affine gradients therefore accumulate in registers over every sample the workgroup sees and are
 // written once (no cross-workgroup reduction when nsplit == 1); dWl sums 32 x nsamples rows per
 // workgroup before its one atomic flush.  LN1 partials: sums1[b][pair][2].
-//
-// RECOMP: the MLP pre-activation is not read from memory but recomputed on MFMA from the h1 tile the
-// kernel builds anyway (pre = h1 Wl^T + bl, fp32): the forward then skips its [B, L, 128] pre_l store
-// and this kernel one [B, L, 128] read, for one 32x128x128 MFMA pass and two barriers per chunk.
-template <bool RECOMP>
+// (Recomputing the MLP pre-activation here instead of reading the forward's pre_l measured slower.)
 __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const bf16_t* __restrict__ dh2, const bf16_t* __restrict__ s2, const float* __restrict__ g2,
-    const bf16_t* __restrict__ pre_l, const float* __restrict__ bl, const bf16_t* __restrict__ s1,
+    const bf16_t* __restrict__ pre_l, const bf16_t* __restrict__ s1,
     const float* __restrict__ g1, const float* __restrict__ be1, const bf16_t* __restrict__ wl,
     const float* __restrict__ consts,
     bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
     float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl,
-    const float* __restrict__ gb, float* __restrict__ dwl_slab, int B, int L) {
+    float* __restrict__ dwl_slab, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16 [32][128]
@@ -850,8 +665,6 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
   const int nsplit = gridDim.y;
   const int b0 = (int)((long)B * blockIdx.y / nsplit), b1 = (int)((long)B * (blockIdx.y + 1) / nsplit);
   stage_weight(ws, wl, CH);
-  float bb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (RECOMP) load_f8(bl + ch * 8, bb);
   float adbl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // dWl accumulators: wave w owns co tile (w >> 1) and ci tiles 2 (w & 1) + {0, 1}; they sum over every
   // pair the workgroup walks (long sequences: fewer workgroups than pairs, so fewer dWl flushes)
@@ -874,13 +687,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     bool ok = okl && bs < b1;
     size_t off = (size_t)bs * L * CH + coff;
     uint4 n_dh = ldq(dh2 + off, ok), n_s2 = ldq(s2 + off, ok), n_s1 = ldq(s1 + off, ok);
-    uint4 n_pr = RECOMP ? make_uint4(0u, 0u, 0u, 0u) : ldq(pre_l + off, ok);
-    // late gb: s1 + gb[sample] (the forward stored s1 without the broadcast vector)
-    float4 n_g0 = make_float4(0.f, 0.f, 0.f, 0.f), n_g1 = n_g0;
-    if (gb != nullptr && bs < b1) {
-      n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
-      n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
-    }
+    uint4 n_pr = ldq(pre_l + off, ok);
     float4 n_c0 = make_float4(0.f, 1.f, 0.f, 0.f), n_c1 = make_float4(0.f, 1.f, 0.f, 0.f);
     if (bs < b1) {
       n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
@@ -895,11 +702,6 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       unpack8(n_dh, dh);
       unpack8(n_s2, sv2);
       unpack8(n_s1, sv1);
-      {
-        const float gv[8] = {n_g0.x, n_g0.y, n_g0.z, n_g0.w, n_g1.x, n_g1.y, n_g1.z, n_g1.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sv1[e] += gv[e];
-      }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xh2 = (sv2[e] - mean2) * rstd2;
@@ -916,41 +718,14 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
         off = (size_t)bs * L * CH + coff;
         n_dh = ldq(dh2 + off, ok);
         n_s2 = ldq(s2 + off, ok);
-        if (!RECOMP) n_pr = ldq(pre_l + off, ok);
+        n_pr = ldq(pre_l + off, ok);
         n_s1 = ldq(s1 + off, ok);
         if (bs < b1) {
           n_c0 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8);
           n_c1 = *reinterpret_cast<const float4*>(consts + (size_t)bs * 8 + 4);
-          if (gb != nullptr) {
-            n_g0 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8);
-            n_g1 = *reinterpret_cast<const float4*>(gb + (size_t)bs * CH + ch * 8 + 4);
-          }
         }
       };
-      if (RECOMP) {
-        // pre[row][co] = sum_ci h1[row][ci] Wl[co][ci] + bl[co]: the forward's MFMA, from the same
-        // bf16 h1 tile (waves 0-3, D[co][row] into the fp32 tile), while the next chunk loads
-        __syncthreads();
-        prefetch();
-        if (w < 4) {
-          f32x16_t acc = zero16();
-#pragma unroll
-          for (int kk = 0; kk < 8; ++kk)
-            acc = mfma32(lds_frag(ws, swz256(w * 32 + r, kk * 2 + h)), lds_frag(ht, swz256(r, kk * 2 + h)), acc);
-#pragma unroll
-          for (int g = 0; g < 4; ++g)
-            *reinterpret_cast<float4*>(yt + r * YS + w * 32 + 8 * g + 4 * h) =
-                make_float4(acc[4 * g], acc[4 * g + 1], acc[4 * g + 2], acc[4 * g + 3]);
-        }
-        __syncthreads();
-        const float4 pa = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8);
-        const float4 pb = *reinterpret_cast<const float4*>(yt + j * YS + ch * 8 + 4);
-        const float pv[8] = {pa.x, pa.y, pa.z, pa.w, pb.x, pb.y, pb.z, pb.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) pr[e] = pv[e] + bb[e];
-      } else {
-        unpack8(n_pr, pr);
-      }
+      unpack8(n_pr, pr);
       float gp[8];
       {
         const f32x2 xi[4] = {(f32x2){pr[0], pr[1]}, (f32x2){pr[2], pr[3]}, (f32x2){pr[4], pr[5]},
@@ -975,7 +750,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
       }
       __syncthreads();
       // prefetch the next chunk while the MFMAs run
-      if (!RECOMP) prefetch();
+      prefetch();
       if (w < 4) {
         // D[ci][row] = sum_co Wl[co][ci] dpre[row][co]: A = Wl^T (transposed LDS read), B = dpre rows
         f32x16_t acc = zero16();
@@ -1083,7 +858,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
 __global__ void __launch_bounds__(512) ln1_finalize_kernel(
     const bf16_t* __restrict__ dh1, const bf16_t* __restrict__ s1, const float* __restrict__ st1, int T1, int BM1,
     const float* __restrict__ sums1, int TS1, const float* __restrict__ g1, bf16_t* __restrict__ ds1,
-    float* __restrict__ dgb, const float* __restrict__ gb, const float* __restrict__ st1f, int B, int L, float eps) {
+    float* __restrict__ dgb, int B, int L, float eps) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* red = reinterpret_cast<float*>(smem);            // 2 x [PB][CH] (double-buffered)
   float* tab = red + 2 * PB * CH;                          // [nb][4]: mean rstd m1 m2
@@ -1096,12 +871,7 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
   const float inv_n = 1.0f / (float)(L * CH);
   for (int i = w; i < nb; i += 8) {
     float mean, rstd, m1, m2;
-    if (st1f != nullptr) {
-      mean = st1f[2 * (b0 + i)];
-      rstd = st1f[2 * (b0 + i) + 1];
-    } else {
-      wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
-    }
+    wave_ln_stats(st1 + (size_t)(b0 + i) * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
     wave_bwd_consts(sums1 + (size_t)(b0 + i) * TS1 * 2, TS1, inv_n, m1, m2);
     if (lane == 0) { tab[4 * i] = mean; tab[4 * i + 1] = rstd; tab[4 * i + 2] = m1; tab[4 * i + 3] = m2; }
   }
@@ -1128,12 +898,6 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
       float dv[8], sv[8], o[8];
       unpack8(n_dh, dv);
       unpack8(n_s, sv);
-      if (gb != nullptr) {          // late gb: s1 + gb[b]
-        float gv[8];
-        load_f8(gb + (size_t)b * CH + ch * 8, gv);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) sv[e] += gv[e];
-      }
       const size_t noff = (size_t)min(b + 1, B - 1) * L * CH + coff;
       n_dh = *reinterpret_cast<const uint4*>(dh1 + noff);
       n_s = *reinterpret_cast<const uint4*>(s1 + noff);
@@ -1165,29 +929,6 @@ __global__ void __launch_bounds__(512) ln1_finalize_kernel(
   for (int i = tid; i < nb * CH; i += 512) atomicAdd(dgb + (size_t)(b0 + i / CH) * CH + i % CH, dacc[i]);
 }
 
-// ------------------------------------------------------------------------------------------------
-// Per-sample LayerNorm-1 backward constants for the conv data gradient that builds ds1 itself
-// (pbx_conv_dgrad3_ln): c[b] = (mean1, rstd1, m1, m2), m1 = mean(dxhat), m2 = mean(dxhat xhat) from the
-// LN1 partials of the LN2/MLP backward.  One wave per sample.
-__global__ void __launch_bounds__(256) ln1_consts_kernel(const float* __restrict__ st1, int T1, int BM1,
-                                                         const float* __restrict__ sums1, int TS1,
-                                                         const float* __restrict__ st1f, float* __restrict__ consts,
-                                                         int B, int L, float eps) {
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= B) return;
-  float mean, rstd, m1, m2;
-  if (st1f != nullptr) {
-    mean = st1f[2 * b];
-    rstd = st1f[2 * b + 1];
-  } else {
-    wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean, rstd);
-  }
-  wave_bwd_consts(sums1 + (size_t)b * TS1 * 2, TS1, 1.0f / (float)(L * CH), m1, m2);
-  if ((threadIdx.x & 63) == 0) *reinterpret_cast<float4*>(consts + (size_t)b * 4) = make_float4(mean, rstd, m1, m2);
-}
-
-// ------------------------------------------------------------------------------------------------
-// token embedding: forward gather to bf16, backward per-token segmented sum
 __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restrict__ tok, const float* __restrict__ E,
                                                         bf16_t* __restrict__ out, long rows) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -1274,18 +1015,11 @@ static bool ln_attrs_set = false;
 static void set_ln_attrs() {
   if (ln_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<512>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd_kernel<256>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<4, 16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<12, 4, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<12, 2, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
 }
@@ -1296,27 +1030,18 @@ static int ln_groups(int B, int L) {
   return g < 1 ? 1 : (g > B ? B : g);
 }
 
-// gb/cs1 (nullable, "late gb"): s1 lacks the broadcast vector gb [B, 128]; cs1 = conv_fwd3x channel
-// sums.  st1f (nullable): final LN1 (mean, rstd) per sample, for the backward kernels.
-PBX_EXPORT int pbx_ln_linear_fwdx(const void* s1, const float* st1, int T1, int BM1, const float* g1,
-                                  const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
-                                  float* st2, const float* gb, const float* cs1, float* st1f, int B, int L, float eps,
-                                  hipStream_t st) {
+// pre_l (nullable): the MLP pre-activation for the backward (inference forwards skip it)
+PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int BM1, const float* g1,
+                                 const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
+                                 float* st2, int B, int L, float eps, hipStream_t st) {
   dim3 grid((L + PB - 1) / PB, ln_groups(B, L));
   const int nbmax = (B + (int)grid.y - 1) / (int)grid.y;
   const int lds = 32768 + PB * 256 + PB * YS * 4 + nbmax * 18 * 4;
   if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
   hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
-                     (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, gb, cs1, st1f, B, L, eps);
+                     (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
   return pbx_launch_status();
-}
-
-PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int BM1, const float* g1,
-                                 const float* be1, const void* wl, const float* bl, void* pre_l, void* s2,
-                                 float* st2, int B, int L, float eps, hipStream_t st) {
-  return pbx_ln_linear_fwdx(s1, st1, T1, BM1, g1, be1, wl, bl, pre_l, s2, st2, nullptr, nullptr, nullptr, B, L, eps,
-                            st);
 }
 
 // nw: waves per workgroup; vpart is [B][ceil(L / 64)][NJ] (one row per 64-position wave tile)
@@ -1333,42 +1058,19 @@ PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2
 }
 
 // dvpart rows follow the forward tiling (bmv positions, a multiple of 32); sums2 is [B][ceil(L / 32)][2]
-PBX_EXPORT int pbx_attn_bwd(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
-                            const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
-                            int NJ, int nw, float eps, hipStream_t st) {
-  set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + nw * NJ * 4 > 163840 || nw < 1 || nw > 8 || bmv % 32 != 0)
-    return (int)hipErrorInvalidValue;
-  const long items = (long)B * ((L + 31) / 32);
-  long wgl = (items + nw - 1) / nw;
-  if (wgl > num_cus()) wgl = num_cus();
-  const int wgs = (int)wgl;
-  hipLaunchKernelGGL(nw > 4 ? attn_bwd_kernel<512> : attn_bwd_kernel<256>, dim3(wgs), dim3(64 * nw),
-                     NJ * 256 + nw * NJ * 4, st, (const bf16_t*)h2,
-                     (const bf16_t*)s2,
-                     st2, g2, (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, NJ,
-                     eps);
-  return pbx_launch_status();
-}
-
-// v2 pool: also writes gfrag (bf16 GELU' fragments, B * 2 ceil(L/64) * NJ * 32 elements)
+// v2 pool: also writes gfrag (bf16 GELU' fragments, B * 2 ceil(L/64) * NJ * 32 elements).  8 waves per
+// workgroup (two per SIMD), 4 GELU pairs per interleaved core call; measured against 4 waves x 8 / 16
+// pairs and 12 waves of 32-position items (profiles/r2_v8_pool_32pos_ab.txt): equal or slower.
 PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
-                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, int nw, float eps,
+                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, float eps,
                                 hipStream_t st) {
   set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 + (nw & 15) * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
-  // nw (low 4 bits) = 8: two waves per SIMD, 4 GELU pairs per core call; 4: one wave per SIMD with
-  // 8 independent pairs per core call (or 16 when nw = 4 | 16 << 4) for ILP; 12: 32-position items,
-  // three waves per SIMD (vpart: one row per 32-position tile, 2 ceil(L/64) rows per sample)
-  const int ni = nw >> 4 ? nw >> 4 : ((nw & 15) == 8 ? 4 : (nw & 15) == 12 ? 2 : 8);
-  nw &= 15;
-  if (nw != 4 && nw != 8 && nw != 12) return (int)hipErrorInvalidValue;
-  auto* k = nw == 12 ? (ni == 4 ? ln_attn_fwd2_kernel<12, 4, 1> : ln_attn_fwd2_kernel<12, 2, 1>)
-          : nw == 8 ? ln_attn_fwd2_kernel<8, 4> : (ni == 16 ? ln_attn_fwd2_kernel<4, 16> : ln_attn_fwd2_kernel<4, 8>);
-  const long items2 = (long)B * ((L + 63) / 64) * (nw == 12 ? 2 : 1);
+  constexpr int nw = 8;
+  if (NJ % 64 != 0 || NJ * 256 + nw * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
+  const long items2 = (long)B * ((L + 63) / 64);
   long wg2 = (items2 + nw - 1) / nw;
   if (wg2 > num_cus()) wg2 = num_cus();
-  hipLaunchKernelGGL(k, dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
+  hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
                      (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag, B, L,
                      NJ, eps);
   return pbx_launch_status();
@@ -1393,21 +1095,19 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
 
 // dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics).
 // consts: [B][8] fp32 workspace; sums1: [B][ceil(L/2)][2] LN1 partials (TS1 = ceil(L/2)).
-// bl != nullptr: recompute the MLP pre-activation (pre_l unused, may be null); wg_per_cu: workgroups
-// per CU to aim the (position pair, sample split) grid at (0: one)
-PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
-                                   const float* g2, const void* pre_l, const float* bl, const void* s1,
-                                   const float* st1, int T1, int BM1, const float* g1, const float* be1,
-                                   const void* wl, float* consts, void* dh1, float* sums1, float* dg2, float* db2,
-                                   float* dg1, float* db1, float* dwl, float* dbl, float* dgb_zero,
-                                   const float* gb, const float* st1f, int B, int L, float eps, int wg_per_cu,
-                                   float* dwl_slab, int slab_rows, hipStream_t st) {
+// dwl_slab (nullable): [slab_rows][128][128] scratch for per-workgroup dWl partials (else atomics).
+PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
+                                  const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
+                                  int BM1, const float* g1, const float* be1, const void* wl, float* consts,
+                                  void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
+                                  float* dbl, float* dgb_zero, int B, int L, float eps, float* dwl_slab, int slab_rows,
+                                  hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
-                     consts, dgb_zero, st1f, B, L, eps);
+                     consts, dgb_zero, B, L, eps);
   const int pairs = (L + 1) / 2;
-  const int target = (wg_per_cu > 0 ? wg_per_cu : 1) * num_cus();
+  const int target = num_cus();
   int nsplit = (target + pairs - 1) / pairs;        // at least one workgroup per CU
   if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
   if (nsplit < 1) nsplit = 1;
@@ -1415,13 +1115,12 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
   // L = 4096 one workgroup per pair made 33 M float atomics on the 16 K dWl elements)
   const int gx = pairs < target ? pairs : target;
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
-  auto* k = bl != nullptr ? ln2_linear_bwd_kernel<true> : ln2_linear_bwd_kernel<false>;
   // dWl partials: one slab row per workgroup when the caller's slab is large enough, else atomics
   const int nwg = gx * nsplit;
   float* slab = dwl_slab != nullptr && nwg <= slab_rows ? dwl_slab : nullptr;
-  hipLaunchKernelGGL(k, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
-                     (const bf16_t*)s2, g2, (const bf16_t*)pre_l, bl, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
-                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, gb, slab, B, L);
+  hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
+                     (const bf16_t*)s2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
+                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, slab, B, L);
   if (slab != nullptr) {
     const int rc = pbx_launch_status();
     if (rc != 0) return rc;
@@ -1430,21 +1129,10 @@ PBX_EXPORT int pbx_ln2_linear_bwd2(const void* dh2, const void* s2, const float*
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
-                                  const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
-                                  int BM1, const float* g1, const float* be1, const void* wl, float* consts,
-                                  void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
-                                  float* dbl, float* dgb_zero, int B, int L, float eps, hipStream_t st) {
-  return pbx_ln2_linear_bwd2(dh2, s2, st2, sums2, TS2, g2, pre_l, nullptr, s1, st1, T1, BM1, g1, be1, wl, consts,
-                             dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, dgb_zero, nullptr, nullptr, B, L, eps, 0,
-                             nullptr, 0, st);
-}
-
 // dgb ([B, 128] fp32) is accumulated into
-// gb (nullable): late-gb s1 (add gb[b]); st1f (nullable): final LN1 (mean, rstd) per sample
-PBX_EXPORT int pbx_ln1_finalizex(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
-                                 const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, const float* gb,
-                                 const float* st1f, int B, int L, float eps, hipStream_t st) {
+PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
+                                const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
+                                float eps, hipStream_t st) {
   // at most 16 position tiles across x (a workgroup walks the rest), ~2 workgroups per CU overall
   const int tp = (L + PB - 1) / PB;
   const int gx = tp < 16 ? tp : 16;
@@ -1456,22 +1144,8 @@ PBX_EXPORT int pbx_ln1_finalizex(const void* dh1, const void* s1, const float* s
   if (lds > 163840) return (int)hipErrorInvalidValue;
   set_ln_attrs();
   hipLaunchKernelGGL(ln1_finalize_kernel, grid, dim3(512), lds, st, (const bf16_t*)dh1, (const bf16_t*)s1, st1, T1,
-                     BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, gb, st1f, B, L, eps);
+                     BM1, sums1, TS1, g1, (bf16_t*)ds1, dgb, B, L, eps);
   return pbx_launch_status();
-}
-
-// consts: [B][4] fp32 (mean1, rstd1, m1, m2) for pbx_conv_dgrad3_ln; st1f nullable (late gb)
-PBX_EXPORT int pbx_ln1_consts(const float* st1, int T1, int BM1, const float* sums1, int TS1, const float* st1f,
-                              float* consts, int B, int L, float eps, hipStream_t st) {
-  hipLaunchKernelGGL(ln1_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st1, T1, BM1, sums1, TS1, st1f, consts, B,
-                     L, eps);
-  return pbx_launch_status();
-}
-
-PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
-                                const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
-                                float eps, hipStream_t st) {
-  return pbx_ln1_finalizex(dh1, s1, st1, T1, BM1, sums1, TS1, g1, ds1, dgb, nullptr, nullptr, B, L, eps, st);
 }
 
 PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long rows, hipStream_t st) {

@@ -195,47 +195,6 @@ __device__ __forceinline__ void wave_ln_stats(const float* __restrict__ part, in
   rstd = rsqrtf(M2 / n + eps);
 }
 
-// LayerNorm(L, C = 128) statistics of s1 = s1' + gb (gb[c] broadcast over the positions) from the
-// tile partials (mean, M2) of s1', its per-tile channel sums cs[T][128] and gb, in centered form:
-//   mean = m' + gbar
-//   var  = M2'/n + (1/C) sum_c (gb_c - gbar)^2 + (2/C) sum_c (gb_c - gbar) (colmean'_c - m')
-// (the producer of s1' runs before gb exists; see conv_fwd3 / ln_linear_fwd "late gb").
-__device__ __forceinline__ void wave_ln_stats_gb(const float* __restrict__ part, int T, int BM, int L,
-                                                 const float* __restrict__ cs, const float* __restrict__ gbr,
-                                                 float eps, float& mean, float& rstd) {
-  const int lane = threadIdx.x & 63;
-  float n = 0.f, m = 0.f, M2 = 0.f;
-  for (int t = lane; t < T; t += 64) {
-    const float2 pm = *reinterpret_cast<const float2*>(part + 2 * t);
-    chan_merge(n, m, M2, (float)(min(BM, L - t * BM) * 128), pm.x, pm.y);
-  }
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    const float nb = __shfl_xor(n, o, 64), mb = __shfl_xor(m, o, 64), M2b = __shfl_xor(M2, o, 64);
-    chan_merge(n, m, M2, nb, mb, M2b);
-  }
-  const float g0 = gbr[lane], g1 = gbr[lane + 64];
-  float c0 = 0.f, c1 = 0.f;
-  for (int t = 0; t < T; ++t) {
-    c0 += cs[t * 128 + lane];
-    c1 += cs[t * 128 + lane + 64];
-  }
-  float a = g0 + g1;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) a += __shfl_xor(a, o, 64);
-  const float gbar = a * (1.0f / 128.0f);
-  const float d0 = g0 - gbar, d1 = g1 - gbar, invL = 1.0f / (float)L;
-  float vg = d0 * d0 + d1 * d1;
-  float cv = d0 * fmaf(c0, invL, -m) + d1 * fmaf(c1, invL, -m);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    vg += __shfl_xor(vg, o, 64);
-    cv += __shfl_xor(cv, o, 64);
-  }
-  mean = m + gbar;
-  rstd = rsqrtf(fmaxf(M2 / n + (vg + 2.0f * cv) * (1.0f / 128.0f), 0.f) + eps);
-}
-
 // ln_bwd_consts computed by a whole wave (parallel loads + butterfly sums)
 __device__ __forceinline__ void wave_bwd_consts(const float* __restrict__ part, int T, float inv_n, float& m1,
                                                 float& m2) {

@@ -13,7 +13,6 @@ import torch
 import torch.nn.functional as F
 
 from .global_track import FusedGlobalBlockFn, GlobalBlockFn, HeadsLossFn, InputLayerFn, glob_fused_ok, pack_batch
-from . import local_track, streams
 from .local_track import CH, EmbedFn, conv_images, local_block
 from .paper_track import PaperHeadsLossFn, paper_block, unit_attention_weight
 
@@ -76,9 +75,6 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         else:
             glob_imgs.append(None)
     pack_batch(items)
-    # late gb (reference semantics): each global block runs on an aux stream beside the next block's
-    # convolution, whose output leaves the broadcast global->local vector to its consumers
-    aux_glob = (not paper) and local_track.late_gb_enabled() and streams.ENABLED and h.is_cuda
     for i, blk in enumerate(blocks):
         att = blk.global_attention_layer
         if paper:
@@ -96,14 +92,11 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         args = (g, g_bf, vpart, l1.weight, l1.bias, n1.weight, n1.bias, l2.weight, l2.bias, n2.weight, n2.bias,
                 wp, None if nxt is None else nxt.weight, None if nxt is None else nxt.bias)
         if glob_imgs[i] is not None:
-            g, g_bf, gb = FusedGlobalBlockFn.apply(*args, glob_imgs[i], aux_glob)
+            g, g_bf, gb = FusedGlobalBlockFn.apply(*args, glob_imgs[i])
         else:
             g, g_bf, gb = GlobalBlockFn.apply(*args)
-    if aux_glob and not torch.is_grad_enabled():
-        streams.join()             # no backward will release the aux-stream inputs
     if return_bf16:
-        return h, g, g_bf          # consumers (HeadsLossFn) wait for the aux stream themselves
-    streams.wait_ready(g, g_bf)
+        return h, g, g_bf
     return h, g
 
 

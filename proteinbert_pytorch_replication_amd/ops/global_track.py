@@ -1,14 +1,15 @@
-"""Global track, input layer and pretraining heads on MI355X (``csrc/glob.hip`` + hipBLASLt).
+"""Global track, input layer and pretraining heads on MI355X (``csrc/glob2.hip``, ``csrc/glob.hip``,
+``csrc/gemm.hip``).
 
 Reference: ``ProteinBERT/modules.py:175-199,221-229`` (global MLP + LayerNorm(G)),
 ``:255-262`` (GO input layer), ``:277-293`` (heads) and ``ProteinBERT/utils.py:293-294`` (loss).
 
-The ``[B, G]``/``[B, A]`` GEMMs are plain library GEMMs (bf16 operands, fp32 output through
-``torch.mm(..., out_dtype=float32)`` -> hipBLASLt); bias, GELU, residual, LayerNorm, the attention
-scale ``sum(W)/K``, the loss and every elementwise backward step are fused HIP kernels.  Backward
-passes are written by hand: each autograd node is 2-6 launches instead of ~30 eager ops, and
-parameter gradients accumulate straight into the flat-arena ``.grad`` views (weight gradients via
-``addmm(out=grad)``, bias/affine gradients via in-kernel atomics).
+The ``[B, G]`` / ``[B, A]`` products run on the in-tree MFMA GEMM (:mod:`.gemm`: bf16 operands, fp32
+accumulation, deterministic split-K); the GO head's GEMM carries the sigmoid / BCE / dlogits epilogue.
+Bias, GELU, residual, LayerNorm, the attention scale ``sum(W)/K``, the loss and every elementwise
+backward step are fused HIP kernels.  Backward passes are written by hand: each autograd node is a
+few launches instead of ~30 eager ops, and parameter gradients accumulate straight into the
+flat-arena ``.grad`` views.
 """
 from __future__ import annotations
 
@@ -19,6 +20,8 @@ from typing import List, Optional, Tuple
 import torch
 
 from . import _lib, streams
+from .gemm import gemm as _gemm
+from .gemm import go_head_parts
 from ..train.arena import notify_grads_ready
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -38,7 +41,6 @@ def local_head_parts(B: int, L: int, dev) -> int:
     if 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (16 * 32 + 96) * 4 > 163840:
         return L
     return min(L, 2 * torch.cuda.get_device_properties(dev).multi_processor_count)
-_lib.register("pbx_go_head", [_P, _P, _P, _P, ctypes.c_long, ctypes.c_long, _P, _P, _P, _I, _I, _P])
 
 _lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P])
@@ -72,14 +74,60 @@ def bf16_of(p: torch.Tensor) -> torch.Tensor:
     return p.detach().to(BF16)
 
 
+def _operand(t: torch.Tensor, inner_axis: int):
+    """(base tensor with unit inner stride, transposed?) for a 2-D GEMM operand view: ``t`` itself
+    when its last axis is contiguous, else ``t.T`` (a transposed view of a row-major tensor)."""
+    if t.stride(1) == 1:
+        return t, False
+    if t.stride(0) == 1:
+        return t.t(), True
+    return t.contiguous(), False
+
+
 def mm32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bf16 x bf16 -> fp32 (hipBLASLt)."""
-    return torch.mm(a, b, out_dtype=F32)
+    """bf16 ``a [M, K]`` x bf16 ``b [K, N]`` -> new fp32 [M, N] (in-tree MFMA GEMM; either operand may
+    be a transposed view)."""
+    out = torch.empty((a.shape[0], b.shape[1]), dtype=F32, device=a.device)
+    (a0, ta), (b0, tb) = _operand(a, 1), _operand(b, 1)
+    return _gemm(a0, b0, out, ta, tb)
 
 
 def addmm_into(dst: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> None:
     """dst += a @ b with bf16 operands and fp32 accumulation/output, in place."""
-    torch.addmm(dst, a, b, out_dtype=F32, out=dst)
+    (a0, ta), (b0, tb) = _operand(a, 1), _operand(b, 1)
+    _gemm(a0, b0, dst, ta, tb, accumulate=True)
+
+
+def addmm_new(c: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """New fp32 ``c + a @ b`` (the incoming ``c`` is left untouched)."""
+    out = c.float().clone()
+    addmm_into(out, a, b)
+    return out
+
+
+A_ALIGN = 8
+
+
+def padded_cols(n: int) -> int:
+    return (n + A_ALIGN - 1) // A_ALIGN * A_ALIGN
+
+
+_PAD_CACHE = {}
+
+
+def bf16_padded(p: torch.Tensor) -> torch.Tensor:
+    """bf16 copy of a 2-D parameter ``[R, C]`` with its columns zero-padded to a multiple of 8
+    (16-B loads in the MFMA GEMM for odd C such as the 8943 GO annotations); the buffer is cached per
+    parameter and refreshed from the bf16 mirror each call.  Returns the ``[R, C]`` view."""
+    R, Cc = p.shape
+    key = (id(p), p.device)
+    buf = _PAD_CACHE.get(key)
+    if buf is None or buf.shape != (R, padded_cols(Cc)):
+        buf = torch.zeros((R, padded_cols(Cc)), dtype=BF16, device=p.device)
+        _PAD_CACHE[key] = buf
+    view = buf[:, :Cc]
+    view.copy_(bf16_of(p))
+    return view
 
 
 class _Grads:
@@ -113,8 +161,15 @@ class InputLayerFn(torch.autograd.Function):
     def forward(ctx, ann, w, b, wgl, bgl):
         dev = ann.device
         st = _s(dev)
-        ann_bf = ann.to(BF16)
-        u = mm32(ann_bf, bf16_of(w).t())
+        B, A = ann.shape
+        # the multi-hot annotations as bf16 ({0, 1, 2} exact) with the columns padded to 8 (16-B loads)
+        ann_pad = torch.empty((B, padded_cols(A)), dtype=BF16, device=dev)
+        ann_pad[:, A:].zero_()
+        ann_bf = ann_pad[:, :A]
+        ann_bf.copy_(ann)
+        wp = bf16_padded(w)                                                    # [G, A] bf16, padded
+        u = torch.empty((B, w.shape[0]), dtype=F32, device=dev)
+        _gemm(ann_bf, wp, u, ta=False, tb=True, pad_a=True, pad_b=True)
         B, G = u.shape
         g = torch.empty_like(u)
         g_bf = torch.empty((B, G), dtype=BF16, device=dev)
@@ -157,11 +212,11 @@ class InputLayerFn(torch.autograd.Function):
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
                       dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
             addmm_into(dwgl, dugl.t(), g_bf)
-            dg = torch.addmm(dg, dugl, bf16_of(wgl), out_dtype=F32)      # new buffer: no clone + add
+            dg = addmm_new(dg, dugl, bf16_of(wgl))
         du = torch.empty((B, G), dtype=BF16, device=dev)
         _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
                   st)
-        addmm_into(dw, du.t(), ann_bf)
+        _gemm(du, ann_bf, dw, ta=True, tb=False, accumulate=True, pad_b=True)      # dW_in += du^T ann
         return (None, *gr.finish())
 
 
@@ -215,14 +270,9 @@ class FusedGlobalBlockFn(torch.autograd.Function):
     :class:`GlobalBlockFn`."""
 
     @staticmethod
-    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl, packed=None, aux=False):
+    def forward(ctx, g, g_bf, vpart, w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl, packed=None):
         """``packed``: the six fragment images (f1, f1T, f2, f2T, fgl, fglT) already built by
-        :func:`pack_batch` for this step, else they are built here.
-
-        ``aux``: run the kernel on the ``gfwd`` aux stream and mark the outputs ready there; every
-        main-stream consumer must call :func:`.streams.wait_ready` on them first (the late-gb local
-        block does so after launching its convolution, so that kernel overlaps this one: the global
-        track occupies 32 workgroups for ~35 us per block)."""
+        :func:`pack_batch` for this step, else they are built here."""
         dev = g.device
         B, G = g.shape
         TV = vpart.shape[1]
@@ -246,20 +296,10 @@ class FusedGlobalBlockFn(torch.autograd.Function):
             vp, TVk = vp.sum(dim=1, keepdim=True), 1
         gc, gbc = g.contiguous(), g_bf.contiguous()
 
-        def launch():
-            _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
-                                            fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
-                                            gb if NGL else None),
-                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
-
-        if aux and dev.type == "cuda":
-            # outputs were allocated on the main stream above; the aux stream starts after the main
-            # stream's work so far, and the inputs stay referenced until the end-of-step join
-            with streams.on_aux(dev, "gfwd", keep=[gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b, fgl, bgl]):
-                launch()
-            streams.mark_ready(dev, "gfwd", [g2, g2_bf, gb])
-        else:
-            launch()
+        _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                        fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                        gb if NGL else None),
+                  B, G, NGL, TVk, K, LN_EPS, _s(dev))
         ctx.save_for_backward(g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT)
         ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
         ctx.meta = (TV, NGL)
@@ -384,7 +424,7 @@ class GlobalBlockFn(torch.autograd.Function):
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
                       dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
             addmm_into(dwgl, dugl.t(), g2_bf)
-            dg2 = torch.addmm(dg2, dugl, bf16_of(wgl), out_dtype=F32)   # new buffer (incoming grad untouched)
+            dg2 = addmm_new(dg2, dugl, bf16_of(wgl))                   # new buffer (incoming grad untouched)
         # LN2 + MLP2
         du2 = torch.empty((B, G), dtype=BF16, device=dev)
         dg1 = torch.empty((B, G), dtype=F32, device=dev)
@@ -409,8 +449,10 @@ class GlobalBlockFn(torch.autograd.Function):
 class HeadsLossFn(torch.autograd.Function):
     """Both pretraining heads + the reference loss (``utils.py:293-294``), reference semantics.
 
-    The loss is terminal, so the local-head kernel computes the input gradient in the forward pass;
-    the GO head runs its GEMM, then one fused sigmoid/BCE/dlogits pass.
+    The loss is terminal, so both heads compute their input gradients in the forward pass: the
+    local-head kernel writes dh, and the GO head is ONE MFMA GEMM launch whose epilogue evaluates
+    sigmoid / BCE / dlogits and the bias-gradient partials (``csrc/gemm.hip`` EPI_GO: the [B, 8943]
+    logits never reach memory).  The backward is two in-tree GEMMs (dg2 = dz Wa, dWa += dz^T g2).
     """
 
     @staticmethod
@@ -428,20 +470,8 @@ class HeadsLossFn(torch.autograd.Function):
         _lib.call("pbx_local_head2", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
                   y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(),
                   dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, P, st)
-        # the last global block may still run on its aux stream: the local head above overlapped it
-        streams.wait_ready(g2, g2_bf)
-        z = mm32(g2_bf, bf16_of(wa).t())
-        dz = torch.empty((B, A), dtype=BF16, device=dev)
-        dba = torch.zeros(A, dtype=F32, device=dev)
-        # per-row weights (the reference's any(annotation) broadcast) are read without expanding them
-        if w_g.dim() == 2 and w_g.stride(1) == 0:
-            wg, wsr, wsc = w_g[:, 0].float().contiguous(), 1, 0
-        else:
-            wg = w_g.float().expand(B, A).contiguous()
-            wsr, wsc = A, 1
-        _lib.call("pbx_go_head", z.data_ptr(), ba.data_ptr(), y_g.float().contiguous().data_ptr(), wg.data_ptr(),
-                  wsr, wsc, dz.data_ptr(), dba.data_ptr(), loss[1:].data_ptr(), B, A, st)
-        ctx.save_for_backward(dh, dwo_part, dbo_part, dz, dba, g2_bf)
+        dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
+        ctx.save_for_backward(dh, dwo_part, dbo_part, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)
         ctx.V = V
         total = loss.sum()
@@ -460,20 +490,62 @@ class HeadsLossFn(torch.autograd.Function):
             return (None,) * 11
         if _UNIT_LOSS_GRAD[0]:
             # loss.backward() from the training step: d(loss) == 1 exactly, skip the rescale passes
-            dz_s, dh_s = dz, dh
-            scale = None
+            dh_s, scale = dh, None
         else:
             scale = dtotal.reshape(1).to(F32).contiguous()
-            s0 = scale.reshape(())
-            dz_s, dh_s = (dz.float() * s0).to(dz.dtype), (dh.float() * s0).to(dh.dtype)
+            dh_s = (dh.float() * scale.reshape(())).to(dh.dtype)
         # per-position partials of the local head -> its weight / bias gradients (one pass each)
         L_, V_ = dbo_part.shape
         _lib.call("pbx_colsum_add", dwo_part.data_ptr(), L_, dwo_part[0].numel(), dwo.data_ptr(), _lib.ptr(scale), st)
         _lib.call("pbx_colsum_add", dbo_part.data_ptr(), L_, V_, dbo_dst.data_ptr(), _lib.ptr(scale), st)
-        _lib.call("pbx_colsum_add", dba.data_ptr(), 1, dba.numel(), dba_dst.data_ptr(), _lib.ptr(scale), st)
-        dg2 = mm32(dz_s, bf16_of(wa))
-        addmm_into(dwa, dz_s.t(), g2_bf)
+        dg2 = go_head_backward(dz, dba, g2_bf, wa, dwa, dba_dst, scale)
+
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)
+
+
+def go_head_forward(g2_bf: torch.Tensor, wa: torch.Tensor, ba: torch.Tensor, y_g: torch.Tensor,
+                    w_g: torch.Tensor, loss_slot: torch.Tensor):
+    """GO head + its BCE term (reference ``modules.py:286-293``, ``utils.py:294``) as ONE launch:
+    z = g2 Wa^T + ba, sigmoid, BCE with the log clamp, weight, dz = dL/dz (bf16) and the bias-gradient
+    partials (``pbx_go_head_fused``); the mean loss is added into ``loss_slot`` (device scalar).
+    Returns (dz [B, A] view of a column-padded buffer, bias-gradient partials [ceil(B/128), A], g2)."""
+    dev = g2_bf.device
+    st = _s(dev)
+    B, A = g2_bf.shape[0], wa.shape[0]
+    dz_pad = torch.empty((B, padded_cols(A)), dtype=BF16, device=dev)     # pad columns zeroed by the kernel
+    dz = dz_pad[:, :A]
+    dba = torch.empty(((B + 127) // 128, A), dtype=F32, device=dev)
+    lparts = torch.empty(go_head_parts(B, A), dtype=F32, device=dev)
+    y = y_g.float().contiguous()
+    # per-row weights (the reference's any(annotation) broadcast) are read without expanding them
+    if w_g.dim() == 2 and w_g.stride(1) == 0:
+        wrow, wfull = w_g[:, 0].float().contiguous(), None
+    else:
+        wrow, wfull = None, w_g.float().expand(B, A).contiguous()
+    gx = g2_bf.contiguous()
+    wab = bf16_of(wa)
+    _lib.call("pbx_go_head_fused", gx.data_ptr(), gx.stride(0), wab.data_ptr(), wab.stride(0), ba.data_ptr(),
+              y.data_ptr(), A, _lib.ptr(wrow), _lib.ptr(wfull), dz.data_ptr(), dz_pad.stride(0), dba.data_ptr(),
+              lparts.data_ptr(), B, A, gx.shape[1], st)
+    _lib.call("pbx_colsum_add", lparts.data_ptr(), lparts.numel(), 1, loss_slot.data_ptr(), None, st)
+    return dz, dba, gx
+
+
+def go_head_backward(dz, dba, g2_bf, wa, dwa_dst, dba_dst, scale=None) -> torch.Tensor:
+    """dg2 = s dz Wa (K = A: split-K), dWa += s dz^T g2, dba += s sum_rows(dz); ``scale`` (device
+    [1] or None) = the incoming gradient of the loss."""
+    B, A = dz.shape
+    st = _s(dz.device)
+    if scale is not None:
+        dz_s = torch.zeros((B, padded_cols(A)), dtype=BF16, device=dz.device)[:, :A]
+        dz_s.copy_(dz.float() * scale.reshape(()))
+    else:
+        dz_s = dz
+    _lib.call("pbx_colsum_add", dba.data_ptr(), dba.shape[0], A, dba_dst.data_ptr(), _lib.ptr(scale), st)
+    dg2 = torch.empty((B, g2_bf.shape[1]), dtype=F32, device=dz.device)
+    _gemm(dz_s, bf16_of(wa), dg2, ta=False, tb=False, pad_a=True)                   # dg2 = dz Wa
+    _gemm(dz_s, g2_bf, dwa_dst, ta=True, tb=False, accumulate=True, pad_a=True)      # dWa += dz^T g2
+    return dg2
 
 
 _UNIT_LOSS_GRAD = [False]

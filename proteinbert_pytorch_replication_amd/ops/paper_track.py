@@ -25,7 +25,8 @@ import torch
 
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
-from .global_track import BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, mm32, addmm_into
+from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
+                           addmm_into)
 from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
@@ -91,7 +92,7 @@ class PaperBlockFn(torch.autograd.Function):
         gb = gb.detach().float().contiguous()
         pre_n, pre_w, s1 = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=F32, device=dev)       # whole-sequence partials (unused here)
-        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, BM1, stream)
+        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream)
         h2 = torch.empty_like(x)
         stats = torch.empty((B * L, 4), dtype=F32, device=dev)
         _lib.call("pbx_pc_ln_linear_fwd", s1.data_ptr(), g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(),
@@ -184,7 +185,7 @@ class PaperBlockFn(torch.autograd.Function):
         if streams.GLOBAL_ENABLED:
             streams.fork(dev, "global")
         dx, dpn, dpw = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
-        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, BM1, stream)
+        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
                            keep=[dpn, dpw, x], name="wgrad")
@@ -256,21 +257,13 @@ class PaperHeadsLossFn(torch.autograd.Function):
         dlog.scatter_add_(1, y.unsqueeze(1), torch.full_like(wl, -1.0).unsqueeze(1))
         dlog.mul_((wl * inv).unsqueeze(1))
         dlog_bf = dlog.to(BF16)
+        # (the [B*L, 26] local-head products stay on the library GEMM: V = 26 is not an MFMA-tile shape)
         dh = torch.mm(dlog_bf, bf16_of(wo)).view(B, L, C)                             # bf16
         nc = _split_k_chunks(B * L)                                                    # K = B*L: split-K
         dwo = torch.bmm(dlog_bf.view(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C), out_dtype=F32).sum(dim=0)
         dbo = dlog.sum(dim=0)
-        z = mm32(g2_bf, bf16_of(wa).t())
-        dz = torch.empty((B, A), dtype=BF16, device=dev)
-        dba = torch.zeros(A, dtype=F32, device=dev)
-        if w_g.dim() == 2 and w_g.stride(1) == 0:
-            wg, wsr, wsc = w_g[:, 0].float().contiguous(), 1, 0
-        else:
-            wg = w_g.float().expand(B, A).contiguous()
-            wsr, wsc = A, 1
-        _lib.call("pbx_go_head", z.data_ptr(), ba.data_ptr(), y_g.float().contiguous().data_ptr(), wg.data_ptr(),
-                  wsr, wsc, dz.data_ptr(), dba.data_ptr(), loss[1:].data_ptr(), B, A, st)
-        ctx.save_for_backward(dh, dwo, dbo, dz, dba, g2_bf)
+        dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
+        ctx.save_for_backward(dh, dwo, dbo, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)
         ctx.mark_non_differentiable(loss)
         ctx.set_materialize_grads(False)
@@ -286,13 +279,11 @@ class PaperHeadsLossFn(torch.autograd.Function):
         dwo_d, dbo_d, dwa_d, dba_d = gr.dst
         if _UNIT_LOSS_GRAD[0]:
             s = None
-            dz_s, dh_s = dz, dh
+            dh_s = dh
         else:
-            s = dtotal.reshape(()).to(F32)
-            dz_s, dh_s = (dz.float() * s).to(dz.dtype), (dh.float() * s).to(dh.dtype)
+            s = dtotal.reshape(1).to(F32).contiguous()
+            dh_s = (dh.float() * s.reshape(())).to(dh.dtype)
         dwo_d.add_(dwo if s is None else dwo * s)
         dbo_d.add_(dbo if s is None else dbo * s)
-        dba_d.add_(dba if s is None else dba * s)
-        dg2 = mm32(dz_s, bf16_of(wa))
-        addmm_into(dwa_d, dz_s.t(), g2_bf)
+        dg2 = go_head_backward(dz, dba, g2_bf, wa, dwa_d, dba_d, s)
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)

@@ -50,19 +50,11 @@ def _idx(device: torch.device) -> int:
     return device.index if device.index is not None else torch.cuda.current_device()
 
 
-# aux streams whose work sits on the critical path and must be dispatched ahead of the main-stream
-# kernel launched beside it (the forward global track beside the next block's convolution)
-_HIGH_PRIORITY = {"gfwd"} if os.environ.get("PBX_GFWD_PRIO", "1") == "1" else set()
-
-
 def _aux(device: torch.device, name: str = "wgrad") -> torch.cuda.Stream:
     key = (_idx(device), name)
     s = _streams.get(key)
     if s is None:
-        if name in _HIGH_PRIORITY:
-            s = torch.cuda.Stream(device=key[0], priority=torch.cuda.Stream.priority_range()[1])
-        else:
-            s = torch.cuda.Stream(device=key[0])
+        s = torch.cuda.Stream(device=key[0])
         _streams[key] = s
     return s
 

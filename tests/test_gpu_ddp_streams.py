@@ -48,14 +48,12 @@ def _run(with_ddp: bool, steps: int = 3):
     return losses, opt.arena.data.clone(), g_first
 
 
-@pytest.mark.parametrize("global_stream,late", [(False, False), (True, False), (False, True)])
-def test_rccl_buckets_behind_aux_stream(global_stream, late, monkeypatch):
-    """late: late-gb local blocks, the forward global track on its high-priority aux stream."""
-    from proteinbert_pytorch_replication_amd.ops import local_track, streams
+@pytest.mark.parametrize("global_stream", [False, True])
+def test_rccl_buckets_behind_aux_stream(global_stream):
+    from proteinbert_pytorch_replication_amd.ops import streams
     from proteinbert_pytorch_replication_amd.parallel.dist import nccl_pg_options
     saved = streams.GLOBAL_ENABLED
     streams.GLOBAL_ENABLED = global_stream
-    monkeypatch.setattr(local_track, "LATE_GB", late)
     # the process-group options bench.py / pretrain use (high-priority RCCL streams)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{_port()}", rank=0, world_size=1,
                             timeout=datetime.timedelta(seconds=60), device_id=torch.device("cuda", 0),

@@ -1,0 +1,101 @@
+"""GPU numerics: the in-tree MFMA GEMM (csrc/gemm.hip) and the fused GO head vs plain PyTorch fp32.
+
+Shapes are the step's own (B x 8943 x 512 products, K = B weight gradients) plus odd extents that
+exercise partial tiles, the unaligned-load path and split-K."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _op(t, trans):
+    return t.float().t() if trans else t.float()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 512, 8943), (8943, 512, 512), (512, 8943, 512), (512, 512, 512),
+                                   (77, 130, 300), (128, 128, 128), (513, 255, 129)])
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm_layouts_vs_fp32(M, N, K, ta, tb):
+    from proteinbert_pytorch_replication_amd.ops.gemm import gemm
+    torch.manual_seed(M + N + K)
+    a = torch.randn((K, M) if ta else (M, K), device="cuda").to(torch.bfloat16)
+    b = torch.randn((N, K) if tb else (K, N), device="cuda").to(torch.bfloat16)
+    ref = _op(a, ta) @ _op(b, tb)
+    out = torch.full((M, N), float("nan"), device="cuda")
+    gemm(a, b, out, ta, tb)
+    torch.cuda.synchronize()
+    e = rel(out, ref)
+    assert e < 1e-5, e           # bf16 products are exact in fp32; only the summation order differs
+    acc = torch.randn(M, N, device="cuda")
+    acc0 = acc.clone()
+    gemm(a, b, acc, ta, tb, accumulate=True, splitk=3)
+    torch.cuda.synchronize()
+    assert rel(acc, acc0 + ref) < 1e-5
+
+
+def test_gemm_padded_operands_and_strided_output():
+    """A [B, 8943] operand stored with an 8960 stride (zero pad) takes the 16-B path; the output is a
+    strided view (columns 0..N of a wider buffer)."""
+    from proteinbert_pytorch_replication_amd.ops.gemm import gemm
+    torch.manual_seed(0)
+    B, A, G = 256, 8943, 512
+    buf = torch.zeros(B, 8960, device="cuda", dtype=torch.bfloat16)
+    buf[:, :A] = torch.randn(B, A, device="cuda").to(torch.bfloat16)
+    x = buf[:, :A]
+    du = torch.randn(B, G, device="cuda").to(torch.bfloat16)
+    out = torch.zeros(G, A + 5, device="cuda")[:, :A]
+    gemm(du, x, out, ta=True, tb=False, pad_b=True)          # dW_in = du^T ann
+    ref = du.float().t() @ x.float()
+    torch.cuda.synchronize()
+    assert rel(out, ref) < 1e-5
+
+
+def test_gemm_deterministic():
+    from proteinbert_pytorch_replication_amd.ops.gemm import gemm
+    torch.manual_seed(1)
+    a = torch.randn(512, 8943, device="cuda").to(torch.bfloat16)
+    b = torch.randn(8943, 512, device="cuda").to(torch.bfloat16)
+    o1 = torch.empty(512, 512, device="cuda")
+    o2 = torch.empty(512, 512, device="cuda")
+    gemm(a, b, o1)
+    gemm(a, b, o2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("B,A,per_row", [(512, 8943, True), (300, 8943, False), (64, 96, True)])
+def test_go_head_fused_vs_fp32(B, A, per_row):
+    """z = x Wa^T + ba, BCE(sigmoid(z), y) x w (reference modules.py:286-293, utils.py:294): loss, dz,
+    the bias-gradient partials."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
+    from proteinbert_pytorch_replication_amd.ops.gemm import go_head_parts
+    torch.manual_seed(B + A)
+    G = 512
+    x = (torch.randn(B, G, device="cuda") * 0.5).to(torch.bfloat16)
+    wa = (torch.randn(A, G, device="cuda") * 0.05).to(torch.bfloat16)
+    ba = torch.randn(A, device="cuda") * 0.1
+    y = (torch.rand(B, A, device="cuda") < 0.01).float()
+    wrow = (torch.rand(B, device="cuda") < 0.5).float()
+    wfull = wrow[:, None].expand(B, A).contiguous()
+    dz = torch.empty(B, A, device="cuda", dtype=torch.bfloat16)
+    nrt = (B + 127) // 128
+    dbp = torch.empty(nrt, A, device="cuda")
+    lp = torch.empty(go_head_parts(B, A), device="cuda")
+    st = _lib.stream_ptr(x.device)
+    _lib.call("pbx_go_head_fused", x.data_ptr(), G, wa.data_ptr(), G, ba.data_ptr(), y.data_ptr(), A,
+              wrow.data_ptr() if per_row else None, None if per_row else wfull.data_ptr(), dz.data_ptr(), A,
+              dbp.data_ptr(), lp.data_ptr(), B, A, G, st)
+    z = (x.float() @ wa.float().t() + ba).requires_grad_(True)
+    p = torch.sigmoid(z)
+    loss = (torch.nn.functional.binary_cross_entropy(p, y, reduction="none") * wfull).mean()
+    loss.backward()
+    torch.cuda.synchronize()
+    got_loss = lp.sum().item()
+    assert abs(got_loss - loss.item()) < 1e-4 * abs(loss.item()) + 1e-9
+    assert rel(dz, z.grad) < 5e-3                      # bf16 rounding of dz
+    assert rel(dbp.sum(0), z.grad.sum(0)) < 5e-3

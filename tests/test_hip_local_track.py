@@ -46,36 +46,31 @@ def torch_local(x, gb, blk):
     return h2, vsum
 
 
-@pytest.mark.parametrize("L,B,late", [(512, 3, False), (200, 2, False), (300, 2, False), (64, 4, False),
-                                      (1024, 2, False), (4096, 1, False), (512, 3, True), (300, 2, True),
-                                      (4096, 1, True)])
-def test_local_block_forward(L, B, late, monkeypatch):
-    from proteinbert_pytorch_replication_amd.ops import local_track as lt
+@pytest.mark.parametrize("L,B,frozen", [(512, 3, False), (200, 2, False), (300, 2, False), (64, 4, False),
+                                        (1024, 2, False), (4096, 1, False), (512, 3, True), (300, 2, True),
+                                        (4096, 1, True)])
+def test_local_block_forward(L, B, frozen):
+    """frozen: no input needs a gradient (frozen-encoder / inference forward): the forward-only pool
+    kernel (pbx_ln_attn_fwd) runs and no backward state is written."""
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
-    monkeypatch.setattr(lt, "LATE_GB", late)     # conv stores s1 without gb; LN1 consumers add it
     m, blk = make_block(L)
+    if frozen:
+        blk.requires_grad_(False)
     x = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb = torch.randn(B, 128, device="cuda") * 0.5
     with torch.no_grad():
         h2, vpart = local_block(x, gb, blk)
         rh2, rv = torch_local(x.float(), gb, blk)
     torch.cuda.synchronize()
-    assert rel(h2, rh2) < 1.5e-2
-    assert rel(vpart.sum(1), rv) < 1.5e-2
+    e_h, e_v = rel(h2, rh2), rel(vpart.sum(1), rv)
+    print(f"L={L} B={B} frozen={frozen}: rel h2 {e_h:.2e} vsum {e_v:.2e}")
+    assert e_h < 1.5e-2
+    assert e_v < 1.5e-2
 
 
-@pytest.mark.parametrize("L,B,pre_l,wgcu,late", [(512, 2, "store", 0, False), (200, 3, "store", 0, False),
-                                                 (4096, 1, "store", 0, False), (512, 2, "recompute", 0, False),
-                                                 (200, 3, "recompute", 2, False), (4096, 1, "recompute", 0, False),
-                                                 (300, 40, "recompute", 2, False), (512, 2, "store", 0, True),
-                                                 (300, 5, "recompute", 0, True), (4096, 1, "store", 0, True)])
-def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch, fuse=False):
-    from proteinbert_pytorch_replication_amd.ops import local_track as lt
+@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
+def test_local_block_backward(L, B):
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
-    monkeypatch.setattr(lt, "LN1_FUSE", fuse)          # LN1 backward inside the conv data gradient
-    monkeypatch.setattr(lt, "PRE_L", pre_l)            # MLP pre-activation stored, or recomputed in backward
-    monkeypatch.setattr(lt, "LN2_WG_PER_CU", wgcu)
-    monkeypatch.setattr(lt, "LATE_GB", late)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
@@ -99,24 +94,10 @@ def test_local_block_backward(L, B, pre_l, wgcu, late, monkeypatch, fuse=False):
     ref = torch.autograd.grad(lr, [xr, gbr] + params)
     torch.cuda.synchronize()
     names = ["x", "gb", "wn", "bn", "ww", "bw", "g1", "be1", "wl", "bl", "g2", "be2"]
-    for n, a, b in zip(names, got, ref):
-        e = rel(a, b)
+    errs = {n: rel(a, b) for n, a, b in zip(names, got, ref)}
+    print(f"L={L} B={B}: " + " ".join(f"{n}={e:.2e}" for n, e in errs.items()))
+    for n, e in errs.items():
         assert e < 3e-2, f"{n}: rel err {e:.3e}"
-
-
-@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1)])
-def test_local_block_backward_fused_ln1(L, B, monkeypatch):
-    """LN1 backward inside the conv data gradient (opt-in PBX_LN1_FUSE=1)."""
-    test_local_block_backward(L, B, "store", 0, False, monkeypatch, fuse=True)
-
-
-@pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (300, 5), (64, 4), (4096, 1)])
-def test_local_block_backward_pool_32pos_items(L, B, monkeypatch):
-    """Pool forward with 32-position work items at three waves per SIMD (PBX_ATTN_FWD2=12): one vpart
-    row per 32 positions, GELU' fragments in the same layout as the 64-position form."""
-    from proteinbert_pytorch_replication_amd.ops import local_track as lt
-    monkeypatch.setattr(lt, "ATTN_FWD2_CFG", 12)
-    test_local_block_backward(L, B, "store", 0, False, monkeypatch)
 
 
 def test_embedding_kernels():
@@ -133,19 +114,15 @@ def test_embedding_kernels():
     assert rel(E.grad, dref) < 1e-5
 
 
-@pytest.mark.parametrize("late", [False, True])
-def test_full_model_loss_and_grads_vs_torch(late, monkeypatch):
-    """late: the late-gb local blocks with every global block on its aux stream (overlapping the next
-    block's convolution and, for the last block, the local head)."""
+@pytest.mark.parametrize("nblocks", [2, 3])
+def test_full_model_loss_and_grads_vs_torch(nblocks):
     from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
-    from proteinbert_pytorch_replication_amd.ops import local_track as lt
-    monkeypatch.setattr(lt, "LATE_GB", late)
     from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss
     from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
     torch.manual_seed(0)
     L, A = 256, 8943
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
-                    num_blocks=3 if late else 2, device="cuda", backend="hip")
+                    num_blocks=nblocks, device="cuda", backend="hip")
     X, Y, W = SyntheticUniRefGO(L, A, 6, "cuda", seed=3).next_batch()
     loss = fused_pretrain_loss(m, X, Y, W)
     loss.backward()
