@@ -24,7 +24,8 @@ the HDF5 file format (spec version 3.0) that such files use, directly on ``mmap`
 Compatibility with files written by the real HDF5 library is by construction from the format
 specification; no HDF5 library exists in this image to cross-check against, so that parity is
 unpinned (``tests/test_hdf5.py`` round-trips our own files and checks the encoded structures
-byte by byte against the specification's field layouts).
+byte by byte against the specification's field layouts).  Files with a user block (superblock at
+512 or later, base address != 0) are refused rather than read at shifted offsets.
 """
 from __future__ import annotations
 
@@ -231,7 +232,9 @@ class H5Dataset:
             out = np.empty(len(lens), dtype=object)
             string = self.type.vtype == 1
             for i in range(len(lens)):
-                v = self.file.heap_object(int(addrs[i]), int(idx[i]))[:int(lens[i]) * self.type.base.size]
+                # a zero-length value may carry a null heap ID (libhdf5 writes address 0): no heap read
+                v = b"" if int(lens[i]) == 0 else \
+                    self.file.heap_object(int(addrs[i]), int(idx[i]))[:int(lens[i]) * self.type.base.size]
                 out[i] = v if string else np.frombuffer(v, self.type.base.numpy_dtype())
             return out.reshape((stop - start,) + tuple(self.shape[1:]))
         arr = raw.reshape(-1).view(self.type.numpy_dtype())
@@ -279,6 +282,11 @@ class H5File:
             self.base_addr, _, _, self.root = struct.unpack_from("<QQQQ", self.mm, base + 12)
         else:
             raise NotImplementedError(f"superblock version {ver}")
+        if self.base_addr != 0 or base != 0:
+            # a user block shifts every file address by the base address; this reader resolves
+            # addresses as absolute file offsets, so such files are refused instead of misread
+            raise NotImplementedError(f"{path}: HDF5 user block / non-zero base address ({self.base_addr}, "
+                                      f"superblock at {base}) is not supported")
         self._links = self._group_links(self.root)
 
     def _find_superblock(self) -> int:

@@ -84,7 +84,8 @@ class ProteinBERTForTokenClassification(_FinetuneBase):
         h, g = self._encode(x)
         from ..ops import finetune_head
         if finetune_head.supported(h, self.n_classes) and isinstance(self.dropout, nn.Identity):
-            # bf16 GEMM on the encoder output + streaming weight-gradient kernel (ops/finetune_head.py)
+            # fp32-accurate split-weight bf16 GEMMs on the encoder output + streaming weight-gradient
+            # kernel (ops/finetune_head.py)
             logits = finetune_head.TokenHeadFn.apply(h, self.head.weight, self.head.bias)
         else:
             logits = F.linear(self.dropout(h.float()), self.head.weight, self.head.bias)    # [B, L, K]

@@ -1,9 +1,13 @@
 """Per-residue fine-tuning head on MI355X (BASELINE cfg 5).
 
-``logits = h Wᵀ + b`` over ``[B*L, 128]`` bf16 encoder rows and K <= 16 classes: the forward is one
-bf16 hipBLASLt GEMM (22 us at B*L = 262,144 vs 75 us for the fp32 ``F.linear`` on an upcast copy);
-the weight gradient, a 262,144-long reduction that hipBLASLt ran at 230-410 us, is the streaming
-kernel in ``csrc/finetune.hip`` (fp32 accumulation, deterministic slab reduction).
+``logits = h Wᵀ + b`` over ``[B*L, 128]`` bf16 encoder rows and K <= 16 classes.  The head weight
+stays an fp32 parameter and the logits keep fp32 accuracy: W is split into two bf16 terms
+``W = W_hi + W_lo`` (``W_lo = bf16(W - W_hi)``, together exact to ~2^-17 relative) and the bf16
+encoder output (exact in fp32) meets both in two bf16 GEMMs accumulating in fp32 -- the same
+result as the fp32 ``F.linear`` on an upcast copy to ~1e-6 relative, at 2 x 22 us instead of 75 us
+at B*L = 262,144.  The weight gradient, a 262,144-long reduction that hipBLASLt ran at 230-410 us,
+is the streaming kernel in ``csrc/finetune.hip`` (fp32 accumulation, deterministic slab reduction);
+the input gradient (unfrozen encoders only) is fp32.
 """
 from __future__ import annotations
 
@@ -27,7 +31,10 @@ class TokenHeadFn(torch.autograd.Function):
     def forward(ctx, h, weight, bias):
         B, L, C = h.shape
         h2 = h.contiguous().view(B * L, C)
-        logits = torch.addmm(bias.float(), h2, weight.to(torch.bfloat16).t(), out_dtype=torch.float32)
+        w_hi = weight.detach().to(torch.bfloat16)
+        w_lo = (weight.detach() - w_hi.float()).to(torch.bfloat16)
+        logits = torch.addmm(bias.float(), h2, w_hi.t(), out_dtype=torch.float32)
+        torch.addmm(logits, h2, w_lo.t(), out_dtype=torch.float32, out=logits)
         ctx.save_for_backward(h2, weight)
         ctx.shape = (B, L)
         return logits.view(B, L, -1)
@@ -40,7 +47,7 @@ class TokenHeadFn(torch.autograd.Function):
         g = dlogits.reshape(B * L, K).float().contiguous()
         dh = dw = db = None
         if ctx.needs_input_grad[0]:
-            dh = torch.mm(g.to(torch.bfloat16), weight.to(torch.bfloat16)).view(B, L, -1)
+            dh = torch.mm(g, weight.float()).view(B, L, -1).to(h2.dtype)
         if ctx.needs_input_grad[1]:
             M = B * L
             P = max(1, min(2 * torch.cuda.get_device_properties(h2.device).multi_processor_count, (M + 15) // 16))

@@ -30,17 +30,34 @@ _lib.register("pbx_row_ln_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
 _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
-_lib.register("pbx_local_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
-_lib.register("pbx_local_head2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 
 
-def local_head_parts(B: int, L: int, dev) -> int:
-    """Partial-gradient rows of the local-head kernel (``csrc/glob.hip`` pbx_local_head2): one per
-    workgroup of the MFMA form (2 workgroups per CU walk the positions), else one per position."""
-    Bp = (B + 31) // 32 * 32
-    if 128 * 256 + 32 * 256 + Bp * 64 + Bp * 128 + (16 * 32 + 96) * 4 > 163840:
-        return L
-    return min(L, 2 * torch.cuda.get_device_properties(dev).multi_processor_count)
+def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l: torch.Tensor, w_l: torch.Tensor,
+                       loss_slot: torch.Tensor):
+    """Local head + its CE term, reference semantics (softmax over the batch axis; ``csrc/lhead.hip``):
+    five coalesced passes over 16-sample x 32-position row tiles.  Adds the mean loss into ``loss_slot``
+    and returns (dh [B, L, 128] bf16, dz [B*L, 32] bf16 -- dL/dlogits for the dWo GEMM -- and the
+    per-tile bias-gradient partials [tiles, V])."""
+    dev = h.device
+    st = _s(dev)
+    B, L, C = h.shape
+    V = wo.shape[0]
+    nt = ((B + 15) // 16) * ((L + 31) // 32)
+    nch = (B + 15) // 16
+    dh = torch.empty_like(h)
+    dz = torch.empty((B * L, 32), dtype=BF16, device=dev)
+    dbo_part = torch.empty((nt, V), dtype=F32, device=dev)
+    lparts = torch.empty(nt, dtype=F32, device=dev)
+    Z = torch.empty((B * L, 32), dtype=F32, device=dev)
+    part = torch.empty((2, nch, L, 32, 2), dtype=F32, device=dev)
+    ms_t = torch.empty((2, L, 32, 2), dtype=F32, device=dev)
+    _lib.call("pbx_local_head3", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
+              y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dz.data_ptr(),
+              dbo_part.data_ptr(), lparts.data_ptr(), Z.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
+              ms_t[0].data_ptr(), ms_t[1].data_ptr(), B, L, V, st)
+    _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+    return dh, dz, dbo_part
 
 _lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P])
@@ -463,15 +480,9 @@ class HeadsLossFn(torch.autograd.Function):
         V = wo.shape[0]
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
-        dh = torch.empty_like(h)
-        P = local_head_parts(B, L, dev)
-        dwo_part = torch.empty((P, V, C), dtype=F32, device=dev)
-        dbo_part = torch.empty((P, V), dtype=F32, device=dev)
-        _lib.call("pbx_local_head2", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
-                  y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(),
-                  dwo_part.data_ptr(), dbo_part.data_ptr(), loss.data_ptr(), B, L, V, P, st)
+        dh, dzl, dbo_part = local_head_forward(h, wo, bo, y_l, w_l, loss[0:1])
         dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
-        ctx.save_for_backward(dh, dwo_part, dbo_part, dz, dba, gx)
+        ctx.save_for_backward(dh, dzl, dbo_part, h, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)
         ctx.V = V
         total = loss.sum()
@@ -481,7 +492,7 @@ class HeadsLossFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dtotal, _dparts):
-        dh, dwo_part, dbo_part, dz, dba, g2_bf = ctx.saved_tensors
+        dh, dzl, dbo_part, h, dz, dba, g2_bf = ctx.saved_tensors
         wo, bo, wa, ba = ctx.params
         gr = _Grads([wo, bo, wa, ba])
         dwo, dbo_dst, dwa, dba_dst = gr.dst
@@ -494,10 +505,14 @@ class HeadsLossFn(torch.autograd.Function):
         else:
             scale = dtotal.reshape(1).to(F32).contiguous()
             dh_s = (dh.float() * scale.reshape(())).to(dh.dtype)
-        # per-position partials of the local head -> its weight / bias gradients (one pass each)
-        L_, V_ = dbo_part.shape
-        _lib.call("pbx_colsum_add", dwo_part.data_ptr(), L_, dwo_part[0].numel(), dwo.data_ptr(), _lib.ptr(scale), st)
-        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), L_, V_, dbo_dst.data_ptr(), _lib.ptr(scale), st)
+        # local head: dWo = dz^T h (K = B*L, deterministic split-K), dbo from the per-tile partials
+        V = wo.shape[0]
+        hr = h.reshape(-1, h.shape[-1])
+        if scale is None:
+            _gemm(dzl[:, :V], hr, dwo, ta=True, tb=False, accumulate=True, pad_a=True)
+        else:
+            dwo.add_(_gemm(dzl[:, :V], hr, torch.empty_like(dwo), ta=True, tb=False, pad_a=True) * scale)
+        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), dbo_part.shape[0], V, dbo_dst.data_ptr(), _lib.ptr(scale), st)
         dg2 = go_head_backward(dz, dba, g2_bf, wa, dwa, dba_dst, scale)
 
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)

@@ -18,8 +18,10 @@ collectives per step.
   backward on RCCL's own stream.
 * ``SUM`` reduction; the 1/world factor is folded into the fused Adam
   (``FusedAdam.grad_scale``) instead of an extra pass.
-* The last bucket (global input layer, ~18 MB, ready last and therefore
-  exposed) can be reduced in bf16 (``tail_bf16=True``).
+* ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
+  bf16-rounded gradient sums); the default is fp32.  (A bf16 reduction of only the last, exposed
+  bucket -- the 18 MB global input layer -- was an unmeasured option and has been removed: no
+  multi-rank run on this pool could show whether its saving beats the two conversion passes.)
 """
 from __future__ import annotations
 
@@ -35,14 +37,13 @@ from ..train.arena import FlatArena, add_grad_ready_listener, remove_grad_ready_
 
 class BucketedAllReduce:
     def __init__(self, arena: FlatArena, bucket_mb: float = 8.0, process_group=None,
-                 comm_dtype: torch.dtype = torch.float32, tail_bf16: bool = False, force: bool = False):
+                 comm_dtype: torch.dtype = torch.float32, force: bool = False):
         """``force`` runs the hooks and collectives even on a 1-rank group (tests of the stream
         ordering on a single GPU)."""
         self.arena = arena
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.comm_dtype = comm_dtype
-        self.tail_bf16 = tail_bf16
         limit = int(bucket_mb * 1024 * 1024 / 4)
         # bucket = [start, end) in arena elements, built on parameter boundaries
         self.buckets: List[List[int]] = []
@@ -100,15 +101,10 @@ class BucketedAllReduce:
                 self._mark(i)
         self._launch_ready()
 
-    def _dtype_for(self, b: int) -> torch.dtype:
-        if self.tail_bf16 and b == len(self.buckets) - 1:
-            return torch.bfloat16
-        return self.comm_dtype
-
     def _launch(self, b: int) -> None:
         s, e = self.buckets[b]
         view = self.arena.grad[s:e]
-        dt = self._dtype_for(b)
+        dt = self.comm_dtype
         # a bucket may hold conv weight gradients still being produced on the aux stream
         # (ops/streams.py): enqueue the collective behind both streams without stalling this one
         ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()

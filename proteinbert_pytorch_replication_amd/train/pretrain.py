@@ -70,7 +70,8 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
              log_every: int = 1, bucket_mb: float = 8.0, compute_dtype="auto", grad_clip: Optional[float] = None,
              async_checkpoint: bool = False, metrics_path: Optional[str] = None, resume: str = "none",
              fuse_optimizer: bool = True, final_save: bool = True, profile_steps: Optional[str] = None,
-             profile_dir: Optional[str] = None, zero_optimizer: bool = False) -> Dict[str, Any]:
+             profile_dir: Optional[str] = None, zero_optimizer: bool = False,
+             comm_dtype="fp32") -> Dict[str, Any]:
     info = pdist.init_distributed()
     if device is None:
         device = info.device
@@ -97,7 +98,9 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
         if isinstance(optimizer, ZeroFusedAdam):
             pdist.broadcast_module(model)
         else:
-            ddp = BucketedAllReduce(optimizer.arena, bucket_mb=bucket_mb)
+            cdt = comm_dtype if isinstance(comm_dtype, torch.dtype) else \
+                {"fp32": torch.float32, "bf16": torch.bfloat16}[comm_dtype]
+            ddp = BucketedAllReduce(optimizer.arena, bucket_mb=bucket_mb, comm_dtype=cdt)
             ddp.broadcast_parameters(model)
 
     scheduler = WarmupThenPlateau(optimizer, warmup_duration=warmup_duration, patience=optim_scheduler_patience)

@@ -243,3 +243,14 @@ def test_reference_dataset_class_reads_h5(tmp_path):
     X, Y, W = ds[0]
     assert X["local"].shape == (64,) and Y["global"].shape == (30,)
     np.testing.assert_array_equal(Y["global"].numpy() > 0, recs[1][2])
+
+
+def test_user_block_files_are_refused_not_misread(h5file, tmp_path):
+    """A file whose superblock sits behind a 512-byte user block resolves every address relative to
+    the base address; the reader refuses it explicitly instead of reading wrong offsets."""
+    p, _, _ = h5file
+    q = str(tmp_path / "ub.h5")
+    with open(p, "rb") as f, open(q, "wb") as g:
+        g.write(b"\0" * 512 + f.read())
+    with pytest.raises(NotImplementedError, match="user block"):
+        h5.H5File(q)
