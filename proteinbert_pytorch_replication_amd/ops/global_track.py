@@ -326,7 +326,22 @@ class FusedGlobalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dg2, _dg2bf, dgb):
-        g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        dev = saved[1].device
+        if streams.GLOBAL_ENABLED and dev.type == "cuda":
+            # on the global-track aux stream: it starts once the next block's LN1 finalize has
+            # produced dgb (streams.fork in LocalBlockFn.backward) and overlaps that block's conv data
+            # gradient; the local-block backward of this block waits for dvpart (streams.wait_ready)
+            with streams.on_aux(dev, "global", keep=[*saved, dg2, dgb]) as scope:
+                out = FusedGlobalBlockFn._backward(ctx, saved, dg2, dgb, on_aux=True)
+                scope.keep(*[t for t in out if isinstance(t, torch.Tensor)])
+            streams.mark_ready(dev, "global", [out[0], out[2]])
+            return out
+        return FusedGlobalBlockFn._backward(ctx, saved, dg2, dgb)
+
+    @staticmethod
+    def _backward(ctx, saved, dg2, dgb, on_aux=False):
+        g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT = saved
         w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl = ctx.params
         TV, NGL = ctx.meta
         dev = pre1.device
@@ -355,7 +370,7 @@ class FusedGlobalBlockFn(torch.autograd.Function):
                 addmm_into(dwgl, dugl.t(), g2_bf)
 
         direct = all(gr.direct[i] for i in (0, 4)) and (not NGL or gr.direct[9])
-        if direct and streams.ENABLED and dev.type == "cuda":
+        if direct and streams.ENABLED and dev.type == "cuda" and not on_aux:
             # dW = dU^T X (K = B rows) is off the critical path: the aux (weight-gradient) stream
             streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf], name="wgrad")
         else:
