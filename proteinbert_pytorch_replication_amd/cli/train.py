@@ -75,11 +75,21 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     if cfg.kernel.deterministic:
         determinism.enable()
     torch.manual_seed(cfg.train.seed)
+    if cfg.data.lengths:
+        # multi-length schedule: the LayerNorm affine is stored at the longest L and sliced per batch
+        import dataclasses
+        cfg.model = dataclasses.replace(cfg.model, sequences_length=max(int(x) for x in cfg.data.lengths),
+                                        variable_length=True)
     model = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
     B, L = cfg.train.batch_size, cfg.model.sequences_length
     corr = CorruptionParams(cfg.data.token_corruption_p, cfg.data.annotation_positive_p,
                             cfg.data.annotation_negative_p, cfg.data.blank_annotation_p)
-    if cfg.data.source == "synthetic":
+    if cfg.data.source == "synthetic" and cfg.data.lengths:
+        from ..data.synthetic import MultiLengthSynthetic
+        loader = MultiLengthSynthetic(cfg.data.lengths, cfg.model.num_annotations, B, dev,
+                                      seed=cfg.data.seed + 1000 * info.rank, min_length=cfg.data.min_length,
+                                      density=cfg.data.annotation_density, corruption=corr)
+    elif cfg.data.source == "synthetic":
         loader = SyntheticUniRefGO(L, cfg.model.num_annotations, B, dev, min_length=cfg.data.min_length,
                                    max_length=cfg.data.max_length, density=cfg.data.annotation_density,
                                    seed=cfg.data.seed + 1000 * info.rank, corruption=corr)

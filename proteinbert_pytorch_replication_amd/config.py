@@ -33,6 +33,9 @@ class ModelConfig:
     # "paper": the published ProteinBERT intent (softmax over L in attention,
     # softmax over the vocabulary, CE on logits, per-position LN over C).
     semantics: str = "reference"
+    # store the LayerNorm((L, C)) affine at L_max = sequences_length and slice it to each batch's L
+    # (multi-length training; the reference fixes one L per model)
+    variable_length: bool = False
 
     def kwargs(self) -> Dict[str, Any]:
         d = asdict(self)
@@ -50,6 +53,7 @@ class DataConfig:
     min_length: int = 0                 # dummy_tests.py:27 lengths U[0, 250]
     max_length: Optional[int] = None    # None -> sequences_length + 64 (forces crops)
     annotation_density: float = 0.005   # dummy_tests.py:34
+    lengths: tuple = ()                 # synthetic multi-length schedule, e.g. (128,512,1024)
     num_workers: int = 0
     seed: int = 0
 

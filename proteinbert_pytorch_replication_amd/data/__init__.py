@@ -6,6 +6,7 @@ from .transforms import (SimpleCharacterTokenizer, SentenceRandomCrop, SimpleTok
 from .datasets import (UniRefGO_PretrainingDataset, UniRefGO_StorePretrainingDataset,
                        UniRefGO_HDF5PretrainingDataset, collate_triples)
 from .store import ProteinStore, ProteinStoreWriter, has_h5py
-from .synthetic import SyntheticUniRefGO, CorruptionParams, corrupt_batch_torch, create_random_samples
+from .synthetic import (SyntheticUniRefGO, MultiLengthSynthetic, CorruptionParams, corrupt_batch_torch,
+                        create_random_samples)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -136,6 +136,30 @@ class SyntheticUniRefGO:
         return self.corrupt(tok, ann)
 
 
+class MultiLengthSynthetic:
+    """Batches whose sequence length cycles through ``lengths`` (the paper trained on a mix of
+    L = 128 / 512 / 1024; reference ``modules.py:148-151`` would need one model per L).  Pair with
+    ``ProteinBERT(..., sequences_length=max(lengths), variable_length=True)``.  ``batch_sizes``: one
+    per length (e.g. constant tokens per batch), default ``batch_size`` for all."""
+
+    def __init__(self, lengths, num_annotations: int = 8943, batch_size: int = 32, device="cpu",
+                 batch_sizes=None, seed: int = 0, **kw):
+        self.lengths = [int(x) for x in lengths]
+        bs = [int(b) for b in batch_sizes] if batch_sizes else [batch_size] * len(self.lengths)
+        self.gens = [SyntheticUniRefGO(L, num_annotations, b, device, seed=seed + 7919 * i, **kw)
+                     for i, (L, b) in enumerate(zip(self.lengths, bs))]
+        self.i = 0
+
+    def __iter__(self):
+        while True:
+            yield self.next_batch()
+
+    def next_batch(self) -> Batch:
+        g = self.gens[self.i % len(self.gens)]
+        self.i += 1
+        return g.next_batch()
+
+
 class SyntheticSecondaryStructure(torch.utils.data.Dataset):
     """Per-residue labelled synthetic proteins for the fine-tuning path (BASELINE cfg 5).
 

@@ -243,6 +243,12 @@ class ProteinBERTBlock(nn.Module):
                               dilation=conv.dilation).transpose(1, 2))
 
     def _local_norm(self, ln: nn.LayerNorm, x: torch.Tensor) -> torch.Tensor:
+        if self.semantics == "reference" and x.shape[1] != ln.normalized_shape[0]:
+            # variable-length model (ProteinBERT(variable_length=True)): the [L_max, C] affine is sliced
+            # to the batch's L; the statistics span the batch's L x C elements
+            L = x.shape[1]
+            return F.layer_norm(x.float(), (L, ln.normalized_shape[1]), ln.weight[:L], ln.bias[:L],
+                                ln.eps).to(x.dtype)
         return F.layer_norm(x.float(), ln.normalized_shape, ln.weight, ln.bias, ln.eps).to(x.dtype)
 
     def forward_torch(self, h: torch.Tensor, g: torch.Tensor, mask: Optional[torch.Tensor] = None,
@@ -280,12 +286,19 @@ class ProteinBERT(nn.Module):
     ``backend``: ``"auto"`` (HIP kernels when on a GPU, else torch), ``"hip"``
     or ``"torch"``.  ``compute_dtype``: dtype of activations on the fast path
     (bf16 by default on GPU; parameters stay fp32 masters).
+
+    ``variable_length``: the reference ties its ``LayerNorm((L, C))`` affine to one length
+    (``modules.py:148-151,161-164``; any other L raises).  With ``variable_length=True`` the affine is
+    stored at ``L_max = sequences_length`` and a batch of length ``L <= L_max`` uses rows ``[:L]``
+    (statistics over its own L x C elements), so one model trains on the paper's mixed lengths
+    (128 / 512 / 1024).  The state dict keeps the reference key set with ``[L_max, C]`` shapes; a
+    reference model loads it only at ``sequences_length == L_max``.
     """
 
     def __init__(self, sequences_length: int, num_annotations: int, local_dim: int, global_dim: int,
                  key_dim: int, num_heads: int, num_blocks: int, conv_kernel_size: int = 9,
                  wide_conv_dilation: int = 5, vocab_size: int = 26, device=None,
-                 semantics: str = "reference", backend: str = "auto"):
+                 semantics: str = "reference", backend: str = "auto", variable_length: bool = False):
         super().__init__()
         if semantics not in ("reference", "paper"):
             raise ValueError(f"semantics must be 'reference' or 'paper', got {semantics!r}")
@@ -295,6 +308,7 @@ class ProteinBERT(nn.Module):
                            num_blocks=num_blocks, conv_kernel_size=conv_kernel_size,
                            wide_conv_dilation=wide_conv_dilation, vocab_size=vocab_size, semantics=semantics)
         self.semantics = semantics
+        self.variable_length = variable_length
         self.sequences_length = sequences_length
         self.backend = backend
         self.local_embedding = nn.Embedding(vocab_size, local_dim, device=device)
@@ -325,9 +339,20 @@ class ProteinBERT(nn.Module):
             b.global_attention_layer.load_heads_state(state[str(i)])
 
     # ------------------------------------------------------------------------
+    def check_length(self, L: int) -> None:
+        """Reference semantics: the LayerNorm affine fixes L (exactly ``sequences_length``, or at most
+        it for a ``variable_length`` model); paper semantics (per-position LN) takes any L."""
+        if self.semantics != "reference":
+            return
+        if L > self.sequences_length or (L != self.sequences_length and not self.variable_length):
+            raise RuntimeError(f"input length {L} does not match the model's LayerNorm((L, C)) length "
+                               f"{self.sequences_length}" + ("" if self.variable_length else
+                                                             " (build with variable_length=True for L < L_max)"))
+
     def encode_torch(self, tokens: torch.Tensor, annotations: torch.Tensor,
                      compute_dtype: Optional[torch.dtype] = None,
                      faithful_attention: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        self.check_length(tokens.shape[1])
         dt = compute_dtype or torch.float32
         h = self.local_embedding.weight.to(dt)[tokens]                       # [B,L,C]
         lin = self.global_linear_layer[0]

@@ -45,6 +45,7 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
                  return_bf16: bool = False):
     """Encoder on the HIP path: returns ``h [B, L, 128]`` (bf16) and ``g [B, G]`` (fp32)."""
     _check(model)
+    model.check_length(tokens.shape[1])   # the kernels index the [L, C] LayerNorm affine by position
     blocks = list(model.proteinBERT_blocks)
     lin = model.global_linear_layer[0]
     gl0 = blocks[0].global_to_local_linear_layer[0]
