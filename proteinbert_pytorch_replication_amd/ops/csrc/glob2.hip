@@ -99,10 +99,11 @@ __device__ __forceinline__ void row_sums(const float (*v)[4], float* red, float*
   }
 }
 
-// column sums over the workgroup's valid rows of v[t][i] -> one atomic per column
+// column sums over the workgroup's valid rows of v[t][i] -> one atomic per column, or (sl != nullptr,
+// deterministic mode) one store into this workgroup's slab row, folded in a fixed order by the caller
 template <int NT>
 __device__ __forceinline__ void col_atomic(const float (*v)[4], const bool* rok, float* __restrict__ dst, int col0,
-                                           int lane) {
+                                           int lane, float* __restrict__ sl) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     float a = 0.f;
@@ -110,7 +111,10 @@ __device__ __forceinline__ void col_atomic(const float (*v)[4], const bool* rok,
     for (int i = 0; i < 4; ++i) a += rok[i] ? v[t][i] : 0.f;
     a += __shfl_xor(a, 16, 64);
     a += __shfl_xor(a, 32, 64);
-    if (lane < 16) atomicAdd(dst + col0 + t * 16 + lane, a);
+    if (lane < 16) {
+      if (sl != nullptr) sl[col0 + t * 16 + lane] = a;
+      else atomicAdd(dst + col0 + t * 16 + lane, a);
+    }
   }
 }
 
@@ -313,8 +317,12 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
     const bf16x8* __restrict__ f1T, float* __restrict__ dg, float* __restrict__ dvs, bf16_t* __restrict__ du1,
     bf16_t* __restrict__ du2, bf16_t* __restrict__ dugl, float* __restrict__ db1, float* __restrict__ dn1w,
     float* __restrict__ dn1b, float* __restrict__ db2, float* __restrict__ dn2w, float* __restrict__ dn2b,
-    float* __restrict__ dbgl, float* __restrict__ dwp, int B) {
+    float* __restrict__ dbgl, float* __restrict__ dwp, int B, float* __restrict__ slab, int K_) {
   constexpr int G = NT * 16 * NW, NT3 = NGL > 0 ? 1 : 0;
+  // deterministic mode: this workgroup's column sums go to slab row blockIdx.x:
+  //   [db1 | dn1w | dn1b | db2 | dn2w | dn2b] (G each) | dbgl (NGL) | dwp (K)
+  float* srow = slab != nullptr ? slab + (size_t)blockIdx.x * (6 * G + NGL + K_) : nullptr;
+  auto sub = [&](int k) { return srow != nullptr ? srow + k * G : nullptr; };
   __shared__ __attribute__((aligned(16))) unsigned char at[RB * G * 2];
   __shared__ float red[NW * RB];
   __shared__ float dsum[NT3 > 0 ? RB * NGL : 1];   // fp32 dugl for the bias-gradient column sums
@@ -351,7 +359,8 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
     for (int c = tid; c < NGL; c += NW * 64) {    // dbgl: column sums over the rows
       float a = 0.f;
       for (int row = 0; row < RB; ++row) a += dsum[row * NGL + c];
-      atomicAdd(dbgl + c, a);
+      if (srow != nullptr) srow[6 * G + c] = a;
+      else atomicAdd(dbgl + c, a);
     }
     gemm_rows<NT>(acc, at, NGL, fglT, w * NT, lane);
     __syncthreads();                              // A tile is rewritten below
@@ -364,7 +373,7 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
   auto ln_bwd = [&](const f4_t* dyv, const float* __restrict__ xh_in, const float* __restrict__ r_in,
                     const float* __restrict__ gam, const float* __restrict__ pre, bf16_t* __restrict__ du_o,
                     float* __restrict__ dbias, float* __restrict__ dgam, float* __restrict__ dbet,
-                    float (*ds)[4]) {
+                    float (*ds)[4], int sbase) {
     float xh[NT][4], dxh[NT][4], dxx[NT][4], tmp[NT][4];
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -378,12 +387,12 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
         tmp[t][i] = dyv[t][i] * xh[t][i];
       }
     }
-    col_atomic<NT>(tmp, rok, dgam, col0, lane);
+    col_atomic<NT>(tmp, rok, dgam, col0, lane, sub(sbase + 1));
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i) tmp[t][i] = dyv[t][i];
-    col_atomic<NT>(tmp, rok, dbet, col0, lane);
+    col_atomic<NT>(tmp, rok, dbet, col0, lane, sub(sbase + 2));
     float m1[4], m2[4], rs[4];
     row_sums<NT, NW>(dxh, red, m1, lane, w);
     row_sums<NT, NW>(dxx, red, m2, lane, w);
@@ -406,14 +415,14 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
         if (rok[i]) du_o[(size_t)grow[i] * G + c] = db;
       }
     }
-    col_atomic<NT>(tmp, rok, dbias, col0, lane);
+    col_atomic<NT>(tmp, rok, dbias, col0, lane, sub(sbase));
     __syncthreads();                              // du tile complete
   };
 
   // ---- LN2 / MLP2: dg1 = ds2 + du2 W2 ----
   {
     float ds[NT][4];
-    ln_bwd(acc, xh2, r2, n2w, pre2, du2, db2, dn2w, dn2b, ds);
+    ln_bwd(acc, xh2, r2, n2w, pre2, du2, db2, dn2w, dn2b, ds, 3);
 #pragma unroll
     for (int t = 0; t < NT; ++t)
 #pragma unroll
@@ -424,7 +433,7 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
   // ---- LN1 / MLP1 / attention: dg = ds1 + du1 W1 ; dvs = scale ds1 ; dwp += sum(ds1 vsum) / K ----
   {
     float ds[NT][4];
-    ln_bwd(acc, xh1, r1, n1w, pre1, du1, db1, dn1w, dn1b, ds);
+    ln_bwd(acc, xh1, r1, n1w, pre1, du1, db1, dn1w, dn1b, ds, 0);
     float sv = 0.f;
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
@@ -446,7 +455,8 @@ __global__ void __launch_bounds__(NW * 64) glob_bwd_kernel(
       float a = 0.f;
 #pragma unroll
       for (int ww = 0; ww < NW; ++ww) a += red[ww];
-      atomicAdd(dwp + tid, a / (float)K);
+      if (srow != nullptr) srow[6 * G + NGL + tid] = a / (float)K;
+      else atomicAdd(dwp + tid, a / (float)K);
     }
     gemm_rows<NT>(acc, at, G, f1T, w * NT, lane);
 #pragma unroll
@@ -487,14 +497,15 @@ void launch_fwd(int B, const void* const* p, const int* iv, float eps, hipStream
 }
 
 template <int NT, int NW, int NGL>
-void launch_bwd(int B, const void* const* p, int K, hipStream_t st) {
+void launch_bwd(int B, const void* const* p, int K, float* slab, hipStream_t st) {
   hipLaunchKernelGGL((glob_bwd_kernel<NT, NW, NGL>), dim3((B + RB - 1) / RB), dim3(NW * 64), 0, st, (const float*)p[0],
                      (const float*)p[1], (const float*)p[2], (const bf16x8*)p[3], (const float*)p[4],
                      (const float*)p[5], (const float*)p[6], (const float*)p[7], (const bf16x8*)p[8],
                      (const float*)p[9], (const float*)p[10], (const float*)p[11], (const float*)p[12],
                      (const float*)p[13], (const float*)p[14], K, (const bf16x8*)p[15], (float*)p[16],
                      (float*)p[17], (bf16_t*)p[18], (bf16_t*)p[19], (bf16_t*)p[20], (float*)p[21], (float*)p[22],
-                     (float*)p[23], (float*)p[24], (float*)p[25], (float*)p[26], (float*)p[27], (float*)p[28], B);
+                     (float*)p[23], (float*)p[24], (float*)p[25], (float*)p[26], (float*)p[27], (float*)p[28], B,
+                     slab, K);
 }
 // forward waves per workgroup: 16 (half the column tiles per wave: shorter dependent chains per
 // row block) or 8; PBX_GLOB_WAVES overrides
@@ -524,14 +535,28 @@ PBX_EXPORT int pbx_glob_fwd(const void* const* p, int B, int G, int NGL, int TV,
   return pbx_launch_status();
 }
 
+extern "C" int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, float* dst, const float* scale,
+                                 hipStream_t st);
+
 // p: dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum, wp, f1T, dg, dvs, du1, du2, dugl,
 //    db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl, dwp   (29 pointers)
-PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, hipStream_t st) {
+// slab (nullable, deterministic mode): [ceil(B / 16)][6 G + NGL + K] fp32 column-sum partials, folded into
+// the eight gradient destinations in a fixed order
+PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, float* slab, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1 || K > 512) return (int)hipErrorInvalidValue;
   // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves)
-  if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, st);
-  else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, st);
-  return pbx_launch_status();
+  if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, slab, st);
+  else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, slab, st);
+  int rc = pbx_launch_status();
+  if (rc != 0 || slab == nullptr) return rc;
+  const int rows = (B + RB - 1) / RB, ld = 6 * G + NGL + K;
+  float* dst[8] = {(float*)p[21], (float*)p[22], (float*)p[23], (float*)p[24], (float*)p[25], (float*)p[26],
+                   (float*)p[27], (float*)p[28]};
+  const int off[8] = {0, G, 2 * G, 3 * G, 4 * G, 5 * G, 6 * G, 6 * G + NGL};
+  const int len[8] = {G, G, G, G, G, G, NGL, K};
+  for (int i = 0; i < 8 && rc == 0; ++i)
+    if (len[i] > 0 && dst[i] != nullptr) rc = pbx_colsum_add_ld(slab + off[i], rows, len[i], ld, dst[i], nullptr, st);
+  return rc;
 }
 
 // fragment images of W [N][Kd] (N, Kd multiples of 32; N*Kd bf16 each)

@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     const float* __restrict__ consts,
     bf16_t* __restrict__ dh1, float* __restrict__ sums1, float* __restrict__ dg2, float* __restrict__ db2,
     float* __restrict__ dg1, float* __restrict__ db1, float* __restrict__ dwl, float* __restrict__ dbl,
-    float* __restrict__ dwl_slab, int B, int L) {
+    float* __restrict__ dwl_slab, float* __restrict__ dbl_slab, int B, int L) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;                                          // Wl, 32 KB
   unsigned char* dt = smem + 32768;                                  // dpre tile bf16 [32][128]
@@ -832,7 +832,9 @@ __global__ void __launch_bounds__(512) ln2_linear_bwd_kernel(
     float a = 0.f;
 #pragma unroll 8
     for (int k = 0; k < 32; ++k) a += yt[k * CH + tid];
-    atomicAdd(dbl + tid, a);
+    // one slab row per workgroup (folded in a fixed order with dWl's slab) or one atomic
+    if (dbl_slab != nullptr) dbl_slab[(size_t)(blockIdx.y * gridDim.x + blockIdx.x) * CH + tid] = a;
+    else atomicAdd(dbl + tid, a);
   }
   // local-MLP weight: D[co][ci], lane -> ci (128 contiguous bytes per half-wave).  dwl_slab: this
   // workgroup's partial goes to its own slab row (folded by one column-sum pass) instead of 16 K float
@@ -946,9 +948,12 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restr
 // in LDS (swz256) and read transposed as the B operand, the one-hot A operand is built in registers
 // from the staged tokens, wave w owns channels 32w..32w+31; one atomic flush of [V][128] per
 // workgroup.  (The previous LDS-atomic scatter serialised on the 26 hot token rows.)
+// dE: accumulated with one atomic per (token, channel) and workgroup, or (slab != nullptr, the
+// deterministic mode) this workgroup's [V][128] partial goes to slab row blockIdx.x (folded in a fixed
+// order by the caller)
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restrict__ tok,
                                                         const bf16_t* __restrict__ dout, float* __restrict__ dE,
-                                                        long rows, int V) {
+                                                        long rows, int V, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) unsigned char ds[256 * 256];
   __shared__ int ts[256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -986,7 +991,11 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restr
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int v = (i & 3) + 8 * (i >> 2) + 4 * h;
-    if (v < V && acc[i] != 0.f) atomicAdd(dE + v * CH + w * 32 + r, acc[i]);
+    if (slab != nullptr) {
+      if (v < V) slab[((size_t)blockIdx.x * V + v) * CH + w * 32 + r] = acc[i];
+    } else if (v < V && acc[i] != 0.f) {
+      atomicAdd(dE + v * CH + w * 32 + r, acc[i]);
+    }
   }
 }
 
@@ -1093,15 +1102,17 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
   return pbx_launch_status();
 }
 
-// dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into (atomics).
+// dg2/db2/dg1/db1 ([L, C]), dwl ([128, 128]) and dbl ([128]) fp32 are accumulated into.
 // consts: [B][8] fp32 workspace; sums1: [B][ceil(L/2)][2] LN1 partials (TS1 = ceil(L/2)).
-// dwl_slab (nullable): [slab_rows][128][128] scratch for per-workgroup dWl partials (else atomics).
+// dwl_slab (nullable): [slab_rows][128 * 128 + 128] scratch for per-workgroup dWl / dbl partials (else
+// atomics).  det: one workgroup per position pair for every sample (the [L, C] affine gradients then
+// have a single writer each) -- with the slab the whole kernel is run-to-run deterministic.
 PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
                                   int BM1, const float* g1, const float* be1, const void* wl, float* consts,
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, float* dgb_zero, int B, int L, float eps, float* dwl_slab, int slab_rows,
-                                  hipStream_t st) {
+                                  int det, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
@@ -1110,7 +1121,7 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
   const int target = num_cus();
   int nsplit = (target + pairs - 1) / pairs;        // at least one workgroup per CU
   if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
-  if (nsplit < 1) nsplit = 1;
+  if (nsplit < 1 || det) nsplit = 1;
   // long sequences: one workgroup walks several position pairs (its dWl partial is flushed once; at
   // L = 4096 one workgroup per pair made 33 M float atomics on the 16 K dWl elements)
   const int gx = pairs < target ? pairs : target;
@@ -1118,24 +1129,29 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
   // dWl partials: one slab row per workgroup when the caller's slab is large enough, else atomics
   const int nwg = gx * nsplit;
   float* slab = dwl_slab != nullptr && nwg <= slab_rows ? dwl_slab : nullptr;
+  float* bslab = slab != nullptr ? slab + (size_t)slab_rows * CH * CH : nullptr;    // [slab_rows][128] after dWl's
+  if (det && slab == nullptr) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
                      (const bf16_t*)s2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
-                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, slab, B, L);
+                     consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, slab, bslab, B, L);
   if (slab != nullptr) {
-    const int rc = pbx_launch_status();
+    int rc = pbx_launch_status();
     if (rc != 0) return rc;
-    return pbx_colsum_add(slab, nwg, CH * CH, dwl, nullptr, st);
+    rc = pbx_colsum_add(slab, nwg, CH * CH, dwl, nullptr, st);
+    if (rc != 0) return rc;
+    return pbx_colsum_add(bslab, nwg, CH, dbl, nullptr, st);
   }
   return pbx_launch_status();
 }
 
 // dgb ([B, 128] fp32) is accumulated into
+// det: one workgroup walks every position tile of its samples (dgb then has a single writer per row)
 PBX_EXPORT int pbx_ln1_finalize(const void* dh1, const void* s1, const float* st1, int T1, int BM1,
                                 const float* sums1, int TS1, const float* g1, void* ds1, float* dgb, int B, int L,
-                                float eps, hipStream_t st) {
+                                float eps, int det, hipStream_t st) {
   // at most 16 position tiles across x (a workgroup walks the rest), ~2 workgroups per CU overall
   const int tp = (L + PB - 1) / PB;
-  const int gx = tp < 16 ? tp : 16;
+  const int gx = det ? 1 : (tp < 16 ? tp : 16);
   int gy = (2 * num_cus() + gx - 1) / gx;
   gy = gy < 1 ? 1 : (gy > B ? B : gy);
   dim3 grid(gx, gy);
@@ -1155,12 +1171,24 @@ PBX_EXPORT int pbx_embed_fwd(const void* tok, const float* E, void* out, long ro
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long rows, int V, hipStream_t st) {
-  if (V > 32) return (int)hipErrorInvalidValue;
+// number of workgroups (= slab rows of the deterministic form) pbx_embed_bwd uses
+PBX_EXPORT int pbx_embed_bwd_groups(long rows) {
   long g = (rows + 511) / 512;
   if (g > 2 * num_cus()) g = 2 * num_cus();
-  if (g < 1) g = 1;
+  return g < 1 ? 1 : (int)g;
+}
+
+// slab (nullable): [pbx_embed_bwd_groups(rows)][V][128] fp32 -> deterministic fixed-order fold into dE
+PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long rows, int V, float* slab,
+                             hipStream_t st) {
+  if (V > 32) return (int)hipErrorInvalidValue;
+  const int g = pbx_embed_bwd_groups(rows);
   hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
-                     (const bf16_t*)dout, dE, rows, V);
+                     (const bf16_t*)dout, dE, rows, V, slab);
+  if (slab != nullptr) {
+    const int rc = pbx_launch_status();
+    if (rc != 0) return rc;
+    return pbx_colsum_add(slab, g, V * CH, dE, nullptr, st);
+  }
   return pbx_launch_status();
 }

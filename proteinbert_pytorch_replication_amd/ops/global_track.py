@@ -23,12 +23,13 @@ from . import _lib, streams
 from .gemm import gemm as _gemm
 from .gemm import go_head_parts
 from ..train.arena import notify_grads_ready
+from ..utils.determinism import fused_deterministic
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("pbx_row_ln_fwd", [_P, _P, _P, _P, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_row_ln_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
-_lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P])
+_lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 
@@ -60,7 +61,7 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     return dh, dz, dbo_part
 
 _lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
-_lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P])
+_lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P, _P])
 _lib.register("pbx_pack_glob_frags", [_P, _P, _P, _I, _I, _P])
 
 LN_EPS = 1e-5
@@ -227,14 +228,19 @@ class InputLayerFn(torch.autograd.Function):
             N = ugl.shape[1]
             dugl = torch.empty((B, N), dtype=BF16, device=dev)
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
-                      dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, 32), N, dev)), st)
             addmm_into(dwgl, dugl.t(), g_bf)
             dg = addmm_new(dg, dugl, bf16_of(wgl))
         du = torch.empty((B, G), dtype=BF16, device=dev)
         _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
-                  st)
+                  _lib.ptr(_det_slab(min(B, 32), G, dev)), st)
         _gemm(du, ann_bf, dw, ta=True, tb=False, accumulate=True, pad_b=True)      # dW_in += du^T ann
         return (None, *gr.finish())
+
+
+def _det_slab(rows: int, cols: int, dev) -> Optional[torch.Tensor]:
+    """Fixed-order reduction scratch for the deterministic mode (None: in-kernel float atomics)."""
+    return torch.empty((rows, cols), dtype=F32, device=dev) if fused_deterministic() else None
 
 
 def _ptrs(*ts) -> ctypes.Array:
@@ -361,7 +367,7 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum, wp,
                                         f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
                                         dbgl if NGL else None, dwp),
-                  B, G, NGL, wp.numel(), _s(dev))
+                  B, G, NGL, wp.numel(), _lib.ptr(_det_slab((B + 15) // 16, 6 * G + NGL + wp.numel(), dev)), _s(dev))
 
         def weight_grads():
             addmm_into(dw1, du1.t(), g_bf)
@@ -454,7 +460,7 @@ class GlobalBlockFn(torch.autograd.Function):
             N = ugl.shape[1]
             dugl = torch.empty((B, N), dtype=BF16, device=dev)
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
-                      dugl.data_ptr(), dbgl.data_ptr(), B, N, st)
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, 32), N, dev)), st)
             addmm_into(dwgl, dugl.t(), g2_bf)
             dg2 = addmm_new(dg2, dugl, bf16_of(wgl))                   # new buffer (incoming grad untouched)
         # LN2 + MLP2

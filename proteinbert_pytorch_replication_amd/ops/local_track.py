@@ -24,6 +24,7 @@ import torch
 
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
+from ..utils.determinism import fused_deterministic
 from .global_track import bf16_of
 
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
@@ -37,10 +38,11 @@ _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _P])
-_lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _P])
+                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _P])
+_lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
-_lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P])
+_lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
+_lib.register("pbx_embed_bwd_groups", [_L])
 
 CH = 128          # kernels are specialised for local_dim = 128
 PB = 32           # positions per workgroup of the position-major LayerNorm kernels
@@ -78,16 +80,18 @@ _DWL_SLAB: Dict[int, torch.Tensor] = {}
 
 
 def dwl_slab(dev: torch.device) -> Tuple[Optional[int], int]:
-    """(pointer, rows) of a per-device [2 x CUs, 128, 128] fp32 scratch slab for the local-MLP weight
-    gradient partials of the LayerNorm/MLP backward kernels (one row per workgroup, folded by one
-    column-sum launch; the kernels fall back to float atomics when it is absent or too small).  The
-    kernels run on one stream in order, so one slab per device is reused by every block."""
+    """(pointer, rows) of a per-device [2 x CUs] x (128 x 128 + 128) fp32 scratch slab for the
+    local-MLP weight / bias gradient partials of the LayerNorm/MLP backward kernels (one row per
+    workgroup, folded by fixed-order column-sum launches; the kernels fall back to float atomics when
+    it is too small).  The kernels run on one stream in order, so one slab per device is reused by
+    every block."""
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     s = _DWL_SLAB.get(idx)
+    rows = 2 * _num_cus(dev)
     if s is None:
-        s = torch.empty((2 * _num_cus(dev), CH, CH), dtype=torch.float32, device=dev)
+        s = torch.empty(rows * (CH * CH + CH), dtype=torch.float32, device=dev)
         _DWL_SLAB[idx] = s
-    return s.data_ptr(), s.shape[0]
+    return s.data_ptr(), rows
 
 
 def _num_cus(dev: torch.device) -> int:
@@ -227,14 +231,15 @@ class LocalBlockFn(torch.autograd.Function):
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, *dwl_slab(dev), stream)
+                  dgb.data_ptr(), B, L, LN_EPS, *dwl_slab(dev), int(fused_deterministic()), stream)
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
         _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
-                  TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, stream)
+                  TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, int(fused_deterministic()),
+                  stream)
         if streams.GLOBAL_ENABLED:
             # the previous block's global-track backward (next autograd node, aux stream) needs only
             # dgb: let it start here, beside the conv data gradient below
@@ -276,7 +281,11 @@ class EmbedFn(torch.autograd.Function):
         (tok,) = ctx.saved_tensors
         dE = torch.zeros((ctx.V, CH), dtype=torch.float32, device=tok.device)
         d = dout.to(torch.bfloat16).contiguous()
-        _lib.call("pbx_embed_bwd", tok.data_ptr(), d.data_ptr(), dE.data_ptr(), tok.numel(), ctx.V,
+        slab = None
+        if fused_deterministic():
+            g = _lib.lib().pbx_embed_bwd_groups(tok.numel())
+            slab = torch.empty((g, ctx.V, CH), dtype=torch.float32, device=tok.device)
+        _lib.call("pbx_embed_bwd", tok.data_ptr(), d.data_ptr(), dE.data_ptr(), tok.numel(), ctx.V, _lib.ptr(slab),
                   _lib.stream_ptr(tok.device))
         return None, dE
 

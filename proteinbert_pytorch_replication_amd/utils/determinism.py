@@ -1,20 +1,24 @@
-"""Deterministic mode: bitwise run-to-run reproducible training.
+"""Deterministic mode: bitwise run-to-run reproducible training on the fused HIP path.
 
-The fused HIP path reduces several gradients with float atomics whose order depends on workgroup
-scheduling, so two runs agree only to rounding (bounded, tested in ``tests/test_determinism.py``):
+By default a few small gradient reductions of the fused path use float atomics whose order depends on
+workgroup scheduling, so two runs agree only to rounding:
 
-* ``csrc/ln.hip``   - local-MLP ``dWl``/``dbl`` (one flush per position-pair workgroup), the [L, C]
-  LayerNorm affine gradients when more than one workgroup shares a position pair (L < 2 x #CUs),
-  the broadcast-vector gradient ``dgb`` (one add per 32-position block), the embedding gradient;
-* ``csrc/glob.hip`` / ``csrc/glob2.hip`` - global-track LayerNorm / bias gradients (one add per
-  16-row block), the local-head column sum of G*P (LDS atomics across waves), the GO-head bias
-  gradient, the loss scalars;
-* library GEMMs that select split-K algorithms.
+* ``csrc/ln.hip``    - the [L, C] LayerNorm affine gradients when several workgroups share a position
+  pair (L < 2 x #CUs), the broadcast-vector gradient ``dgb`` (one add per 32-position block), the
+  embedding gradient;
+* ``csrc/glob2.hip`` / ``csrc/glob.hip`` - the global-track LayerNorm / bias / attention-scale column
+  sums (one add per 16-row block), the GO input-layer bias gradient.
 
-The conv weight gradients (the largest reduction, ``csrc/wgrad.hip``) use fixed-order slab
-reductions and are deterministic.  :func:`enable` switches a run to the PyTorch path with
-``torch.use_deterministic_algorithms`` (same model, same semantics, eager speed); the fused Adam,
-gradient clipping (two-phase sum of squares) and data generation kernels are deterministic.
+Everything else is deterministic by construction: the conv weight gradients (``csrc/wgrad.hip``), the
+local-MLP weight and bias gradients, the in-tree GEMMs (fixed-order split-K, ``csrc/gemm.hip``), the
+heads and their loss partials, the fused Adam and the gradient clipping.
+
+:func:`enable` (or ``PBX_DETERMINISTIC=1`` in the environment) switches those reductions to
+fixed-order forms on the same kernels: per-workgroup partial slabs folded by a column-sum launch, and
+a single writer per destination for the LayerNorm-affine / ``dgb`` gradients.  The cost is a few
+extra small launches per block (``profiles/`` records it).  It also sets
+``torch.use_deterministic_algorithms`` for the PyTorch ops around the kernels.  The paper-semantics
+kernels and the PyTorch-op fallback for unsupported shapes are not covered by the fixed-order forms.
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ import os
 
 import torch
 
-_STATE = {"on": False}
+_STATE = {"on": os.environ.get("PBX_DETERMINISTIC", "0") == "1"}
 
 
 def enable(seed: int = None) -> None:
@@ -36,10 +40,19 @@ def enable(seed: int = None) -> None:
     _STATE["on"] = True
 
 
+def disable() -> None:
+    _STATE["on"] = False
+
+
 def enabled() -> bool:
     return _STATE["on"]
 
 
+def fused_deterministic() -> bool:
+    """The fused HIP kernels use their fixed-order reduction forms."""
+    return _STATE["on"]
+
+
 def backend_for(requested: str) -> str:
-    """Kernel backend to use: the PyTorch path whenever deterministic mode is on."""
-    return "torch" if _STATE["on"] else requested
+    """Kernel backend to use (the fused HIP path has a deterministic form: the request stands)."""
+    return requested
