@@ -166,65 +166,131 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
         }
       }
   } else {
-    // GO head: one thread per (row, column); the column's bias gradient over this tile's 128 rows is
-    // summed through LDS (two wm halves), the loss over the whole tile
-    float* red = reinterpret_cast<float*>(smem);     // reuse the staging tiles: [2][128] dbias + 4
+    // GO head.  The 128 x 128 fp32 tile goes through LDS (row stride 132 floats) so the epilogue
+    // runs on row-contiguous 8-column chunks: 2 x 16-B loads of y, one 16-B dz store, per thread a fixed
+    // 8-column group (tid & 15) over 8 rows -> column sums in registers, folded over the 16 row groups
+    constexpr int TS = BT + 4;
+    float* ft = reinterpret_cast<float*>(smem);
+    __syncthreads();                                  // staging tiles no longer read
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          ft[(wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h) * TS + wn * 64 + j * 32 + r] = acc[i][j][e];
     __syncthreads();
+    const int c8 = tid & 15, rg = tid >> 4;           // columns n0 + 8 c8 .. +7, rows rg + 16 k
+    const int nb = n0 + 8 * c8;
+    float bc[8], dcol[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      bc[e] = nb + e < N ? go.bias[nb + e] : 0.f;
+      dcol[e] = 0.f;
+    }
+    const bool full = nb + 8 <= N && (go.ldy % 4) == 0 && ((uintptr_t)go.y & 15) == 0;
+    const bool dzv = (go.lddz % 8) == 0 && ((uintptr_t)go.dz & 15) == 0;
     float lsum = 0.f;
-    float dcol[2] = {0.f, 0.f};
+#pragma unroll 2
+    for (int k = 0; k < 8; ++k) {
+      const int rl = rg + 16 * k, m = m0 + rl;
+      if (m >= M) break;
+      const float4 z0 = *reinterpret_cast<const float4*>(ft + rl * TS + 8 * c8);
+      const float4 z1 = *reinterpret_cast<const float4*>(ft + rl * TS + 8 * c8 + 4);
+      const float zz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+      float yy[8], wv[8];
+      const float* yrow = go.y + (size_t)m * go.ldy + nb;
+      if (full) {
+        const float4 a = *reinterpret_cast<const float4*>(yrow), b = *reinterpret_cast<const float4*>(yrow + 4);
+        yy[0] = a.x; yy[1] = a.y; yy[2] = a.z; yy[3] = a.w; yy[4] = b.x; yy[5] = b.y; yy[6] = b.z; yy[7] = b.w;
+      } else {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + r;
-      const bool okn = n < N;
-      const float bc = okn ? go.bias[n] : 0.f;
+        for (int e = 0; e < 8; ++e) yy[e] = nb + e < N ? yrow[e] : 0.f;
+      }
+      if (go.wrow != nullptr) {
+        const float wr = go.wrow[m];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+        for (int e = 0; e < 8; ++e) wv[e] = wr;
+      } else {
+        const float* wr = go.wfull + (size_t)m * go.ldy + nb;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (m >= M) continue;
-          if (!okn) {                                // zero pad columns: dz feeds 16-B padded loads
-            if (n < go.lddz) go.dz[(size_t)m * go.lddz + n] = 0;
-            continue;
-          }
-          const float zz = acc[i][j][e] + bc;
-          const float p = 1.0f / (1.0f + __expf(-zz));
-          const float yy = go.y[(size_t)m * go.ldy + n];
-          const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.0f - p), -100.f);
-          const float wgt = go.wrow != nullptr ? go.wrow[m] : go.wfull[(size_t)m * go.ldy + n];
-          lsum += wgt * -(yy * lp + (1.0f - yy) * l1p) * go.inv_mn;
-          const float pq = p * (1.0f - p);
-          const float g = wgt * go.inv_mn * (p - yy) * pq / fmaxf(pq, 1e-12f);
-          const bf16_t gb = f2bf(g);
-          go.dz[(size_t)m * go.lddz + n] = gb;
-          dcol[j] += bf2f(gb);
-        }
+        for (int e = 0; e < 8; ++e) wv[e] = nb + e < N ? wr[e] : 0.f;
+      }
+      float g[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = 1.0f / (1.0f + __expf(-(zz[e] + bc[e])));
+        const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.0f - p), -100.f);
+        const bool ok = nb + e < N;
+        lsum += ok ? wv[e] * -(yy[e] * lp + (1.0f - yy[e]) * l1p) * go.inv_mn : 0.f;
+        const float pq = p * (1.0f - p);
+        g[e] = ok ? wv[e] * go.inv_mn * (p - yy[e]) * pq / fmaxf(pq, 1e-12f) : 0.f;
+      }
+      const uint4 q = packq8(g);
+      if (dzv && nb + 8 <= go.lddz) {                // pad columns [N, lddz) are written as zeros
+        *reinterpret_cast<uint4*>(go.dz + (size_t)m * go.lddz + nb) = q;
+      } else {
+        const unsigned short* qs = reinterpret_cast<const unsigned short*>(&q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (nb + e < go.lddz) go.dz[(size_t)m * go.lddz + nb + e] = qs[e];
+      }
+      float gr[8];
+      unpack8(q, gr);                                // the bias gradient sums the stored (bf16) dz
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dcol[e] += gr[e];
     }
-    // column sums: lanes r and r + 32 hold the same column (h halves), then the two wm halves
+    // column sums over the 16 row groups: through LDS (reuse the tile after a barrier)
+    __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dcol[j] += __shfl_xor(dcol[j], 32, 64);
-    if (h == 0) {
-      red[wm * 128 + wn * 64 + r] = dcol[0];
-      red[wm * 128 + wn * 64 + 32 + r] = dcol[1];
-    }
+    for (int e = 0; e < 8; ++e) ft[rg * TS + 8 * c8 + e] = dcol[e];
     __syncthreads();
     if (tid < BT) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) a += ft[k * TS + tid];
       const int n = n0 + tid;
-      if (n < N) go.dbias_part[(size_t)blockIdx.y * N + n] = red[tid] + red[128 + tid];
+      if (n < N) go.dbias_part[(size_t)blockIdx.y * N + n] = a;
     }
-    __syncthreads();
-    const float lt = block_sum256(lsum, red + 256);
+    float* red = ft + 16 * TS;
+    const float lt = block_sum256(lsum, red);
     if (tid == 0) go.loss_part[blockIdx.y * gridDim.x + blockIdx.x] = lt;
   }
 }
 
-// C[m][n] (+)= sum_z slab[z][m][n]  (fixed order)
+// C[m][n] (+)= sum_z slab[z][m][n]  (fixed order); VEC: N and ldc multiples of 4 (16-B accesses)
+template <bool VEC>
 __global__ void __launch_bounds__(256) gemm_reduce_kernel(const float* __restrict__ slab, int S, float* __restrict__ C,
                                                           long ldc, int M, int N, int accumulate) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
   const long n4 = (N + 3) / 4;
   if (idx >= (long)M * n4) return;
   const int m = (int)(idx / n4), n = (int)(idx - (idx / n4) * n4) * 4;
+  if (VEC) {
+    const size_t zs = (size_t)M * N;
+    const float4* p = reinterpret_cast<const float4*>(slab + (size_t)m * N + n);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 4 <= S; z += 4) {                 // four slabs in flight per step, summed in slab order
+      const float4 a = p[(z * zs) / 4], b = p[((z + 1) * zs) / 4], c = p[((z + 2) * zs) / 4],
+                   d = p[((z + 3) * zs) / 4];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+      s.x += c.x; s.y += c.y; s.z += c.z; s.w += c.w;
+      s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+    }
+    for (; z < S; ++z) {
+      const float4 a = p[(z * zs) / 4];
+      s.x += a.x; s.y += a.y; s.z += a.z; s.w += a.w;
+    }
+    float4* c = reinterpret_cast<float4*>(C + (size_t)m * ldc + n);
+    if (accumulate) {
+      const float4 o = *c;
+      s.x += o.x; s.y += o.y; s.z += o.z; s.w += o.w;
+    }
+    *c = s;
+    return;
+  }
   float s[4] = {0.f, 0.f, 0.f, 0.f};
   for (int z = 0; z < S; ++z) {
     const float* p = slab + ((size_t)z * M + m) * N + n;
@@ -240,17 +306,18 @@ __global__ void __launch_bounds__(256) gemm_reduce_kernel(const float* __restric
 template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
 int launch(const void* A, long lda, const void* B, long ldb, float* C, long ldc, int M, int N, int K, int splitk,
            int accumulate, const GoArgs& go, hipStream_t st) {
+  constexpr int lds = EPI == EPI_GO ? BT * (BT + 4) * 4 : 2 * TILE;     // GO: the fp32 tile for the epilogue
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm_kernel<TA, TB, AL_A, AL_B, EPI>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * TILE);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   const int nkc = (K + BK - 1) / BK;
   const int per = (nkc + splitk - 1) / splitk;
   const int sk = (nkc + per - 1) / per;   // no empty splits
   dim3 grid((N + BT - 1) / BT, (M + BT - 1) / BT, sk);
-  hipLaunchKernelGGL((gemm_kernel<TA, TB, AL_A, AL_B, EPI>), grid, dim3(256), 2 * TILE, st, (const bf16_t*)A, lda,
+  hipLaunchKernelGGL((gemm_kernel<TA, TB, AL_A, AL_B, EPI>), grid, dim3(256), lds, st, (const bf16_t*)A, lda,
                      (const bf16_t*)B, ldb, C, ldc, M, N, K, per, accumulate, go);
   return pbx_launch_status();
 }
@@ -289,8 +356,9 @@ PBX_EXPORT int pbx_gemm(const void* A, long lda, int ta, const void* B, long ldb
 PBX_EXPORT int pbx_gemm_reduce(const float* slab, int S, float* C, long ldc, int M, int N, int accumulate,
                                hipStream_t st) {
   const long n = (long)M * ((N + 3) / 4);
-  hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, slab, S, C, ldc, M, N,
-                     accumulate);
+  const bool vec = N % 4 == 0 && ldc % 4 == 0 && ((size_t)C & 15) == 0 && ((size_t)slab & 15) == 0;
+  hipLaunchKernelGGL(vec ? gemm_reduce_kernel<true> : gemm_reduce_kernel<false>, dim3((unsigned)((n + 255) / 256)),
+                     dim3(256), 0, st, slab, S, C, ldc, M, N, accumulate);
   return pbx_launch_status();
 }
 
