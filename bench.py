@@ -41,6 +41,7 @@ from proteinbert_pytorch_replication_amd.train.step import PretrainStep  # noqa:
 
 METRIC = "sequences/sec (whole node) ProteinBERT pretrain L=512 at 1/2/4/8 MI355X"
 PAPER_IMPLIED_SEQ_PER_S = 277.0  # 670M sequences / 28 days on one RTX 5000
+REFERENCE_CFG1_CPU_SEQ_PER_S = 179.5  # reference cfg 1 step, 8-core CPU, survey measurement
 
 
 def parse():
@@ -163,9 +164,19 @@ def main():
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
                           "impl": a.impl, "hip_graph": graphed},
                "world_size": n, "backend": info.backend if n > 1 else "single",
-               "final_loss": round(final_loss, 5)}
+               "device": _device_label(dev), "final_loss": round(final_loss, 5)}
+        if dev.type != "cuda" and a.preset == "cfg1_cpu_smoke":
+            # BASELINE cfg 1 is a CPU config: compare with the reference step measured on a CPU
+            out["vs_baseline"] = round(value / REFERENCE_CFG1_CPU_SEQ_PER_S, 2)
+            out["baseline"] = "reference modules.py cfg 1 step on an 8-core CPU (BASELINE.md)"
         print(json.dumps(out), flush=True)
     pdist.destroy()
+
+
+def _device_label(dev) -> str:
+    if dev.type != "cuda":
+        return f"cpu ({torch.get_num_threads()} threads)"
+    return torch.cuda.get_device_name(dev)
 
 
 def _data_label(dev) -> str:
