@@ -36,10 +36,8 @@ def split_count(M: int, N: int, K: int, dev, splitk: Optional[int] = None) -> in
     kernel drops empty splits the same way: per = ceil(chunks / s), s' = ceil(chunks / per))."""
     nkc = (K + BK - 1) // BK
     if splitk is None:
-        # split only long reductions: with <= 8 chunks of 128 the slab round trip and the fold launch
-        # cost more than the chunks a workgroup walks (the K = B = 512 weight gradients)
         tiles = ((M + BT - 1) // BT) * ((N + BT - 1) // BT)
-        splitk = 1 if nkc <= 8 else max(1, min(nkc // 4, _num_cus(dev) // max(1, tiles)))
+        splitk = max(1, min(nkc, _num_cus(dev) // max(1, tiles)))
     per = (nkc + splitk - 1) // splitk
     return (nkc + per - 1) // per
 
