@@ -83,34 +83,9 @@ __device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
 
 // Packed GELU / GELU' for VALU-bound epilogues (the attention pool: one GELU per element of a
 // [rows, 512] GEMM output, ~13 VALU + 2 transcendentals each, 3-4x the MFMA time of the GEMM).
-// Same A&S 7.1.26 erf, rearranged so every non-transcendental step is one v_pk_* instruction for
-// two values:  gelu(x) = 0.5 x + |x| * h,  h = 0.5 erf(|x|/sqrt2) = 0.5 - 0.5 t P(t) e  (the -0.5 is
+// A&S 7.1.26 erf, arranged so every non-transcendental step is one v_pk_* instruction for two
+// values:  gelu(x) = 0.5 x + |x| * h,  h = 0.5 erf(|x|/sqrt2) = 0.5 - 0.5 t P(t) e  (the -0.5 is
 // folded into the polynomial coefficients), e = exp(-x^2 / 2), t = 1 / (1 + p |x| / sqrt2).
-__device__ __forceinline__ void gelu_core2(f32x2 x, f32x2& ax, f32x2& h, f32x2& e) {
-  ax = __builtin_elementwise_abs(x);
-  const f32x2 den = __builtin_elementwise_fma(ax, (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
-  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-  const f32x2 q = (x * -0.72134752044448170f) * x;                  // -x^2/2 * log2(e)
-  e = (f32x2){__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  f32x2 pl = __builtin_elementwise_fma(t, (f32x2){-0.5307027145f, -0.5307027145f},
-                                       (f32x2){0.7265760135f, 0.7265760135f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.7107068705f, -0.7107068705f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){0.142248368f, 0.142248368f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.127414796f, -0.127414796f});
-  h = __builtin_elementwise_fma(pl * t, e, (f32x2){0.5f, 0.5f});
-}
-__device__ __forceinline__ f32x2 gelu2_fast(f32x2 x) {
-  f32x2 ax, h, e;
-  gelu_core2(x, ax, h, e);
-  return __builtin_elementwise_fma(ax, h, x * 0.5f);
-}
-// GELU'(x) = Phi(x) + x phi(x) = 0.5 + sign(x) h + x e / sqrt(2 pi)
-__device__ __forceinline__ f32x2 gelu_grad2_fast(f32x2 x) {
-  f32x2 ax, h, e;
-  gelu_core2(x, ax, h, e);
-  const f32x2 sh = {copysignf(h.x, x.x), copysignf(h.y, x.y)};
-  return __builtin_elementwise_fma(x * 0.3989422804014327f, e, sh + 0.5f);
-}
 
 // Scalar form of the interleaved cores below: the same A&S stages on 2N independent scalars, one
 // v_fma_f32 per value per stage.  Beside in-flight MFMAs a v_pk_*_f32 costs far more than its two
@@ -119,34 +94,46 @@ __device__ __forceinline__ f32x2 gelu_grad2_fast(f32x2 x) {
 template <int N, int MODE>   // MODE 0: GELU, 1: GELU', 2: both (g and gd)
 __device__ __forceinline__ void gelu_scalar_n(const f32x2* x, f32x2* g, f32x2* gd) {
   constexpr int M = 2 * N;
-  float xs[M], ax[M], t[M], e[M], pl[M];
+  float xs[M], t[M], e[M], pl[M];
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     xs[i] = (i & 1) ? x[i >> 1].y : x[i >> 1].x;
-    ax[i] = fabsf(xs[i]);
-    t[i] = fmaf(ax[i], 0.23164190f, 1.0f);
-    e[i] = (xs[i] * -0.72134752044448170f) * xs[i];
+    t[i] = fmaf(fabsf(xs[i]), 0.23164190f, 1.0f);
+    // MODE 0: e = exp(-x^2/2); MODE 1/2: e = phi(x) = exp(-x^2/2) / sqrt(2 pi) (Zelen-Severo form:
+    // Phi(|x|) = 1 - phi(x) t B(t), the same A&S 7.1.26 polynomial rescaled), so GELU' = Phi + x e is one fma
+    e[i] = MODE == 0 ? (xs[i] * -0.72134752044448170f) * xs[i]
+                     : fmaf(xs[i] * xs[i], -0.72134752044448170f, -1.3257480647361592f);
   }
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     t[i] = __builtin_amdgcn_rcpf(t[i]);
     e[i] = __builtin_amdgcn_exp2f(e[i]);
   }
+  constexpr float c5 = MODE == 0 ? -0.5307027145f : -1.3302744295891233f;
+  constexpr float c4 = MODE == 0 ? 0.7265760135f : 1.8212559791077754f;
+  constexpr float c3 = MODE == 0 ? -0.7107068705f : -1.7814779365698128f;
+  constexpr float c2 = MODE == 0 ? 0.142248368f : 0.3565637812489156f;
+  constexpr float c1 = MODE == 0 ? -0.127414796f : -0.31938153025994087f;
 #pragma unroll
-  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], -0.5307027145f, 0.7265760135f);
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], c5, c4);
 #pragma unroll
-  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], -0.7107068705f);
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], c3);
 #pragma unroll
-  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], 0.142248368f);
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], c2);
 #pragma unroll
-  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], -0.127414796f);
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(t[i], pl[i], c1);
 #pragma unroll
-  for (int i = 0; i < M; ++i) pl[i] = fmaf(pl[i] * t[i], e[i], 0.5f);   // h
+  for (int i = 0; i < M; ++i) pl[i] = fmaf(pl[i] * t[i], e[i], 0.5f);   // h = 0.5 erf(|x| / sqrt 2)
 #pragma unroll
   for (int i = 0; i < M; ++i) {
     float gv = 0.f, dv = 0.f;
-    if (MODE != 1) gv = fmaf(ax[i], pl[i], xs[i] * 0.5f);
-    if (MODE != 0) dv = fmaf(xs[i] * 0.3989422804014327f, e[i], copysignf(pl[i], xs[i]) + 0.5f);
+    if (MODE == 0) {
+      gv = fmaf(fabsf(xs[i]), pl[i], xs[i] * 0.5f);
+    } else {
+      const float Phi = copysignf(pl[i], xs[i]) + 0.5f;
+      if (MODE == 2) gv = xs[i] * Phi;
+      dv = fmaf(xs[i], e[i], Phi);
+    }
     if (i & 1) {
       if (MODE != 1) g[i >> 1].y = gv;
       if (MODE != 0) gd[i >> 1].y = dv;
@@ -172,12 +159,23 @@ __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
   else gelu_scalar_n<N, 0>(x, out, nullptr);
   return;
 #endif
+  // GRAD: e = phi(x) with the Zelen-Severo coefficients (see gelu2_both_n), GELU' = Phi + x e
+  constexpr float q1 = GRAD ? -1.3257480647361592f : 0.0f;
+  constexpr float c5 = GRAD ? -1.3302744295891233f : -0.5307027145f;
+  constexpr float c4 = GRAD ? 1.8212559791077754f : 0.7265760135f;
+  constexpr float c3 = GRAD ? -1.7814779365698128f : -0.7107068705f;
+  constexpr float c2 = GRAD ? 0.3565637812489156f : 0.142248368f;
+  constexpr float c1 = GRAD ? -0.31938153025994087f : -0.127414796f;
   f32x2 ax[N], t[N], e[N], pl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     ax[i] = __builtin_elementwise_abs(x[i]);
     t[i] = __builtin_elementwise_fma(ax[i], (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
-    e[i] = (x[i] * -0.72134752044448170f) * x[i];
+    if (GRAD)
+      e[i] = __builtin_elementwise_fma(x[i] * x[i], (f32x2){-0.72134752044448170f, -0.72134752044448170f},
+                                       (f32x2){q1, q1});
+    else
+      e[i] = (x[i] * -0.72134752044448170f) * x[i];
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -185,22 +183,20 @@ __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
     e[i] = (f32x2){__builtin_amdgcn_exp2f(e[i].x), __builtin_amdgcn_exp2f(e[i].y)};
   }
 #pragma unroll
-  for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], (f32x2){-0.5307027145f, -0.5307027145f},
-                                      (f32x2){0.7265760135f, 0.7265760135f});
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], (f32x2){c5, c5}, (f32x2){c4, c4});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.7107068705f, -0.7107068705f});
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c3, c3});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){0.142248368f, 0.142248368f});
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c2, c2});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.127414796f, -0.127414796f});
+  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c1, c1});
 #pragma unroll
   for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(pl[i] * t[i], e[i], (f32x2){0.5f, 0.5f});   // h
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     if (GRAD) {
-      const f32x2 sh = {copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)};
-      out[i] = __builtin_elementwise_fma(x[i] * 0.3989422804014327f, e[i], sh + 0.5f);
+      const f32x2 Phi = (f32x2){copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)} + 0.5f;
+      out[i] = __builtin_elementwise_fma(x[i], e[i], Phi);
     } else {
       out[i] = __builtin_elementwise_fma(ax[i], pl[i], x[i] * 0.5f);
     }
@@ -224,12 +220,15 @@ __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd
   gelu_scalar_n<N, 2>(x, g, gd);
   return;
 #endif
-  f32x2 ax[N], t[N], e[N], pl[N];
+  // e = phi(x) (the 1/sqrt(2 pi) folded into the exponent and the polynomial: Zelen-Severo form of
+  // the same A&S 7.1.26 erf), Phi = 0.5 + sign(x) h, GELU = x Phi, GELU' = Phi + x phi: 13 VALU + 2 T
+  f32x2 t[N], e[N], pl[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    ax[i] = __builtin_elementwise_abs(x[i]);
-    t[i] = __builtin_elementwise_fma(ax[i], (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
-    e[i] = (x[i] * -0.72134752044448170f) * x[i];
+    t[i] = __builtin_elementwise_fma(__builtin_elementwise_abs(x[i]), (f32x2){0.23164190f, 0.23164190f},
+                                     (f32x2){1.0f, 1.0f});
+    e[i] = __builtin_elementwise_fma(x[i] * x[i], (f32x2){-0.72134752044448170f, -0.72134752044448170f},
+                                     (f32x2){-1.3257480647361592f, -1.3257480647361592f});
   }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
@@ -238,21 +237,24 @@ __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd
   }
 #pragma unroll
   for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], (f32x2){-0.5307027145f, -0.5307027145f},
-                                      (f32x2){0.7265760135f, 0.7265760135f});
+    pl[i] = __builtin_elementwise_fma(t[i], (f32x2){-1.3302744295891233f, -1.3302744295891233f},
+                                      (f32x2){1.8212559791077754f, 1.8212559791077754f});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.7107068705f, -0.7107068705f});
+  for (int i = 0; i < N; ++i)
+    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-1.7814779365698128f, -1.7814779365698128f});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){0.142248368f, 0.142248368f});
+  for (int i = 0; i < N; ++i)
+    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){0.3565637812489156f, 0.3565637812489156f});
 #pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.127414796f, -0.127414796f});
+  for (int i = 0; i < N; ++i)
+    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.31938153025994087f, -0.31938153025994087f});
 #pragma unroll
   for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(pl[i] * t[i], e[i], (f32x2){0.5f, 0.5f});   // h
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    g[i] = __builtin_elementwise_fma(ax[i], pl[i], x[i] * 0.5f);
-    const f32x2 sh = {copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)};
-    gd[i] = __builtin_elementwise_fma(x[i] * 0.3989422804014327f, e[i], sh + 0.5f);
+    const f32x2 Phi = (f32x2){copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)} + 0.5f;
+    g[i] = x[i] * Phi;
+    gd[i] = __builtin_elementwise_fma(x[i], e[i], Phi);
   }
 }
 

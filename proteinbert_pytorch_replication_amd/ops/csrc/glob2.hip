@@ -516,7 +516,7 @@ int glob_waves() {
 }  // namespace
 
 // G in {256, 512}; NGL in {0, 128} (the local width C = 128 of the paper configuration).
-PBX_EXPORT int pbx_glob_supported(int G, int NGL) {
+static int pbx_glob_supported(int G, int NGL) {   // mirrored by global_track.glob_fused_ok
   return (G == 256 || G == 512) && (NGL == 0 || NGL == 128);
 }
 

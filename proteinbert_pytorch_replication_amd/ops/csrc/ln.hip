@@ -69,10 +69,14 @@ __device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict
   for (int k = 0; k < KB; ++k) {
     const int ci = (k0 + k) * 16 + 8 * h;
     sq[k] = *reinterpret_cast<const uint4*>(src + ci);
+#ifdef PBX_ABL_NOAFFINE   // ablation builds only: the cost of the [L, C] affine loads
+    ga[k][0] = ga[k][1] = ba[k][0] = ba[k][1] = make_float4(mean, rstd, mean, rstd);
+#else
     ga[k][0] = *reinterpret_cast<const float4*>(gam + ci);
     ga[k][1] = *reinterpret_cast<const float4*>(gam + ci + 4);
     ba[k][0] = *reinterpret_cast<const float4*>(bet + ci);
     ba[k][1] = *reinterpret_cast<const float4*>(bet + ci + 4);
+#endif
   }
 #pragma unroll
   for (int k = 0; k < KB; ++k) {
@@ -87,7 +91,11 @@ __device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ok ? (sv[e] - mean) * rstd * g[e] + be[e] : 0.f;
     const uint4 q = packq8(v);
+#ifdef PBX_ABL_NOH2   // ablation builds only: the cost of the h2 stores
+    if (ok && out != nullptr && mean > 1e30f) *reinterpret_cast<uint4*>(out + ci) = q;
+#else
     if (ok && out != nullptr) *reinterpret_cast<uint4*>(out + ci) = q;
+#endif
     f[kk] = __builtin_bit_cast(bf16x8, q);
   }
   }
@@ -309,6 +317,57 @@ __global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
 }
 
 // ------------------------------------------------------------------------------------------------
+// h2 = LN_(L,C)(s2) as a streaming position-major pass (the pattern of ln_linear_fwd): a workgroup
+// owns PB = 32 positions, keeps their fp32 affine in registers (thread: position j, 8 channels) and
+// walks its sample group with AP samples' rows in flight per thread.  The pool forward then reads the
+// normalised rows directly.
+constexpr int AP = 4;
+__global__ void __launch_bounds__(512) ln2_apply_kernel(const bf16_t* __restrict__ s2, const float* __restrict__ st2,
+                                                        const float* __restrict__ g2, const float* __restrict__ be2,
+                                                        bf16_t* __restrict__ h2, int B, int L, float eps) {
+  __shared__ float tab[2 * 256];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = tid >> 4, ch = tid & 15;
+  const int l = blockIdx.x * PB + j;
+  const bool okl = l < L;
+  const int T2 = (L + BML - 1) / BML;
+  const int nbg = gridDim.y;
+  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
+  const int nb = b1 - b0;                          // <= 256 (host: nbg >= ceil(B / 256))
+  for (int i = w; i < nb; i += 8) {
+    float mean, rstd;
+    wave_ln_stats(st2 + (size_t)(b0 + i) * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+    if (lane == 0) {
+      tab[2 * i] = mean;
+      tab[2 * i + 1] = rstd;
+    }
+  }
+  float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (okl) {
+    load_f8(g2 + (size_t)l * CH + ch * 8, gam);
+    load_f8(be2 + (size_t)l * CH + ch * 8, bet);
+  }
+  __syncthreads();
+  if (!okl) return;
+  const size_t col = (size_t)l * CH + ch * 8;
+  for (int bb = b0; bb < b1; bb += AP) {
+    uint4 q[AP];
+#pragma unroll
+    for (int k = 0; k < AP; ++k) q[k] = ldq(s2 + (size_t)min(bb + k, b1 - 1) * L * CH + col, true);
+#pragma unroll
+    for (int k = 0; k < AP; ++k) {
+      if (bb + k >= b1) break;
+      const float mean = tab[2 * (bb + k - b0)], rstd = tab[2 * (bb + k - b0) + 1];
+      float sv[8], o[8];
+      unpack8(q[k], sv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (sv[e] - mean) * rstd * gam[e] + bet[e];
+      *reinterpret_cast<uint4*>(h2 + (size_t)(bb + k) * L * CH + col) = packq8(o);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Attention pool with the GELU derivative stored by the forward (v2).
 //
 // The backward of the pool needs GELU'(h2 Wv) at every (position, value column): recomputing it costs
@@ -327,9 +386,22 @@ __global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
 constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
 constexpr int GT_BYTES = 32 * GT_STRIDE;
 
+#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/build_flags.sh st -DPBX_STAMPS): per-phase clocks
+__device__ long long* pbx_stamp_buf;
+#define PBX_STAMP(k)                                                                       \
+  do {                                                                                     \
+    if (blockIdx.x < 4 && lane == 0 && (k) < 64)                                           \
+      pbx_stamp_buf[(blockIdx.x * 8 + w) * 64 + (k)] = (long long)clock64();               \
+  } while (0)
+#else
+#define PBX_STAMP(k) do {} while (0)
+#endif
+
 // Work item: 64 positions (two 32-position MFMA tiles; each Wv fragment read from LDS feeds two MFMAs;
 // ~248 VGPRs, two waves per SIMD).  NI: GELU pairs interleaved per core call.
-template <int NWAVE, int NI>
+// PRENORM: s2 already holds the normalised rows (h2 from ln2_apply_kernel); no statistics, no affine
+// loads and no h2 stores (the [L, C] fp32 affine re-read per 64-position item cost ~35 us of ~175)
+template <int NWAVE, int NI, bool PRENORM>
 __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
@@ -347,27 +419,51 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
   constexpr int NP = 2;                             // 32-position MFMA tiles per work item
   const int NJT = NJ / 32;
   const long items = (long)B * TW;
+  PBX_STAMP(0);
   stage_weight(ws, wv, NJ);
   __syncthreads();
-  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW) {
+#ifdef PBX_DESYNC   // experiment builds: the second wave of each SIMD starts PBX_DESYNC x 8k cycles late
+  if (w >= 4)
+    for (int i = 0; i < PBX_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
+  PBX_STAMP(1);
+  int sb = 2;
+  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW, sb += 20) {
     const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
     const int pos0 = tw * 32 * NP;
-    float mean, rstd;
-    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+    PBX_STAMP(sb);
     bf16x8 hf0[8], hf1[8];
-    {
+    if constexpr (PRENORM) {
+      const int pa = pos0 + r, pb = pos0 + 32 + r;
+      const bf16_t* ra = s2 + ((size_t)b * L + min(pa, L - 1)) * CH + 8 * h;
+      const bf16_t* rb = s2 + ((size_t)b * L + min(pb, L - 1)) * CH + 8 * h;
+      uint4 qa[8], qb[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        qa[kk] = *reinterpret_cast<const uint4*>(ra + kk * 16);
+        qb[kk] = *reinterpret_cast<const uint4*>(rb + kk * 16);
+      }
+      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        hf0[kk] = __builtin_bit_cast(bf16x8, pa < L ? qa[kk] : z);
+        hf1[kk] = __builtin_bit_cast(bf16x8, pb < L ? qb[kk] : z);
+      }
+      PBX_STAMP(sb + 1);
+    } else {
+      float mean, rstd;
+      wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+      PBX_STAMP(sb + 1);
       const int pa = pos0 + r;
       const int ca = min(pa, L - 1);
       const size_t ra = ((size_t)b * L + ca) * CH;
-      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h,
-                                     h2 + ra);
-      {
-        const int pb = pos0 + 32 + r;
-        const int cb = min(pb, L - 1);
-        const size_t rb = ((size_t)b * L + cb) * CH;
-        ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
-      }
+      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
+      const int pb = pos0 + 32 + r;
+      const int cb = min(pb, L - 1);
+      const size_t rb = ((size_t)b * L + cb) * CH;
+      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
     }
+    PBX_STAMP(sb + 2);
     float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
     // fragment base of this item's 32-position tiles: [b][2 ceil(L/64)][jt][s][lane]
     bf16x8* gdst = gfrag + ((size_t)b * 2 * TW64 + NP * tw) * NJT * 2 * 64 + lane;
@@ -441,8 +537,10 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
       if (jt > 0) epi(p0, p1, jt - 1);
       p0 = c0;
       p1 = c1;
+      PBX_STAMP(sb + 3 + jt);
     }
     epi(p0, p1, NJT - 1);
+    PBX_STAMP(sb + 19);
   }
 }
 
@@ -1025,7 +1123,8 @@ static void set_ln_attrs() {
   if (ln_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -1070,8 +1169,14 @@ PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2
 // v2 pool: also writes gfrag (bf16 GELU' fragments, B * 2 ceil(L/64) * NJ * 32 elements).  8 waves per
 // workgroup (two per SIMD), 4 GELU pairs per interleaved core call; measured against 4 waves x 8 / 16
 // pairs and 12 waves of 32-position items (profiles/r2_v8_pool_32pos_ab.txt): equal or slower.
+#ifdef PBX_STAMPS
+PBX_EXPORT int pbx_set_stamps(long long* buf) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pbx_stamp_buf), &buf, sizeof(buf));
+}
+#endif
+
 PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
-                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, float eps,
+                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, float eps, int prenorm,
                                 hipStream_t st) {
   set_ln_attrs();
   constexpr int nw = 8;
@@ -1079,9 +1184,22 @@ PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g
   const long items2 = (long)B * ((L + 63) / 64);
   long wg2 = (items2 + nw - 1) / nw;
   if (wg2 > num_cus()) wg2 = num_cus();
-  hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES, st,
-                     (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag, B, L,
-                     NJ, eps);
+  if (prenorm) {
+    // h2 = LN(s2) first (streaming pass), then the pool on the normalised rows
+    const int tp = (L + PB - 1) / PB;
+    int nbg = (2 * num_cus() + tp - 1) / tp;
+    nbg = max(nbg, (B + 255) / 256);
+    nbg = min(nbg, B);
+    hipLaunchKernelGGL(ln2_apply_kernel, dim3(tp, nbg), dim3(512), 0, st, (const bf16_t*)s2, st2, g2, be2,
+                       (bf16_t*)h2, B, L, eps);
+    hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
+                       st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
+                       B, L, NJ, eps);
+  } else {
+    hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, false>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
+                       st, (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
+                       B, L, NJ, eps);
+  }
   return pbx_launch_status();
 }
 

@@ -32,6 +32,7 @@ _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_local_head3_tiles", [_I, _I])
 
 
 def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l: torch.Tensor, w_l: torch.Tensor,
@@ -44,7 +45,7 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     st = _s(dev)
     B, L, C = h.shape
     V = wo.shape[0]
-    nt = ((B + 15) // 16) * ((L + 31) // 32)
+    nt = _lib.lib().pbx_local_head3_tiles(B, L)          # the kernel's tile grid (16 samples x 32 positions)
     nch = (B + 15) // 16
     dh = torch.empty_like(h)
     dz = torch.empty((B * L, 32), dtype=BF16, device=dev)

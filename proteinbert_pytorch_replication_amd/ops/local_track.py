@@ -18,6 +18,7 @@ Every op raises if the HIP library is missing — there is no silent eager fallb
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Dict, Optional, Tuple
 
 import torch
@@ -35,7 +36,7 @@ _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
-_lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _P])
@@ -50,6 +51,8 @@ LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 
 
 BM1 = 128         # positions per conv-forward workgroup (= the tile of the LayerNorm-1 partials)
+# pool forward: 1 = LayerNorm-2 as its own streaming pass, the pool reads normalised rows (A/B knob)
+POOL_PRENORM = int(os.environ.get("PBX_POOL_PRENORM", "1"))
 
 
 def attn_pool_supported(NJ: int) -> bool:
@@ -182,7 +185,7 @@ class LocalBlockFn(torch.autograd.Function):
             gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
             _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), gfrag.data_ptr(), B, L, NJ, LN_EPS,
-                      stream)
+                      POOL_PRENORM, stream)
         else:
             # forward-only pool (GELU only, 8 independent waves per workgroup)
             gfrag = None
