@@ -116,23 +116,41 @@ __global__ void __launch_bounds__(512) lhead_logits_kernel(const bf16_t* __restr
 
 // ---- passes 2 / 4: fold the per-chunk partials of every (l, v)
 //  mode 0: (max, sum exp) -> (M, 1/S);  mode 1: sum G P -> T (stored in .x)
+// 64 (l, v) entries per workgroup, the chunks split over 4 thread groups (one pass with an online
+// max / rescaled-sum merge, 4x the loads in flight of a thread walking all chunks twice), the four
+// partials combined in a fixed order
 __global__ void __launch_bounds__(256) lhead_fold_kernel(const float2* __restrict__ part, int nchunks, int L,
                                                          float2* __restrict__ out, int mode) {
-  const int i = blockIdx.x * 256 + threadIdx.x;      // l * 32 + v
-  if (i >= L * VP) return;
-  if (mode == 0) {
-    float m = -3.0e38f;
-    for (int c = 0; c < nchunks; ++c) m = fmaxf(m, part[(size_t)c * L * VP + i].x);
-    float s = 0.f;
-    for (int c = 0; c < nchunks; ++c) {
+  __shared__ float2 red[4][64];
+  const int il = threadIdx.x & 63, cg = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + il;                 // l * 32 + v
+  const bool ok = i < L * VP;
+  float m = -3.0e38f, sum = 0.f;
+  if (ok) {
+    for (int c = cg; c < nchunks; c += 4) {
       const float2 p = part[(size_t)c * L * VP + i];
-      s += p.y * __expf(p.x - m);
+      if (mode == 0) {
+        const float mn = fmaxf(m, p.x);
+        sum = sum * __expf(m - mn) + p.y * __expf(p.x - mn);
+        m = mn;
+      } else {
+        sum += p.x;
+      }
     }
-    out[i] = make_float2(m, s > 0.f ? 1.0f / s : 0.f);
+  }
+  red[cg][il] = make_float2(m, sum);
+  __syncthreads();
+  if (cg != 0 || !ok) return;
+  if (mode == 0) {
+    float mm = red[0][il].x;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) mm = fmaxf(mm, red[k][il].x);
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ss += red[k][il].y * __expf(red[k][il].x - mm);
+    out[i] = make_float2(mm, ss > 0.f ? 1.0f / ss : 0.f);
   } else {
-    float t = 0.f;
-    for (int c = 0; c < nchunks; ++c) t += part[(size_t)c * L * VP + i].x;
-    out[i] = make_float2(t, 0.f);
+    out[i] = make_float2(red[0][il].y + red[1][il].y + red[2][il].y + red[3][il].y, 0.f);
   }
 }
 
@@ -366,7 +384,7 @@ PBX_EXPORT int pbx_local_head3(const void* h, const float* wo, const float* bo, 
   }
   hipLaunchKernelGGL(lhead_logits_kernel, dim3(nt), dim3(512), lds1, st, (const bf16_t*)h, wo, bo, Z, (float2*)part,
                      B, L, V);
-  const int nf = (L * VP + 255) / 256;
+  const int nf = (L * VP + 63) / 64;
   hipLaunchKernelGGL(lhead_fold_kernel, dim3(nf), dim3(256), 0, st, (const float2*)part, nch, L, (float2*)MS, 0);
   hipLaunchKernelGGL(lhead_ce_kernel, dim3(nt), dim3(512), 0, st, Z, (const float2*)MS, (const long long*)y, wl,
                      (float2*)tpart, loss_part, B, L, V, inv_bl);

@@ -63,6 +63,10 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
 
 _lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P, _P])
+_lib.register("pbx_glob3_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_glob3_bwd", [_P, _I, _I, _I, _I, _P, _P])
+_lib.register("pbx_glob3_fold", [_P, _I, _I, _I, _I, _P, _P])
+_lib.register("pbx_glob3_slab_cols", [_I, _I])
 _lib.register("pbx_pack_glob_frags", [_P, _P, _P, _I, _I, _P])
 
 LN_EPS = 1e-5
@@ -253,6 +257,12 @@ def _ptrs(*ts) -> ctypes.Array:
 
 # one-launch global-track kernels (csrc/glob2.hip); PBX_GLOBAL_FUSED=0 selects the library-GEMM path
 GLOBAL_FUSED = os.environ.get("PBX_GLOBAL_FUSED", "1") != "0"
+# column-split global track (csrc/glob3.hip: 3 launches per direction over ceil(B/16) x G/64 workgroups)
+# vs the one-launch form (csrc/glob2.hip, B/16 workgroups), per direction.  The backward runs beside the
+# conv weight gradient on the aux stream, where the three short launches queue behind its workgroups
+# (6 + 43 + 45 us vs 52 us for the one-launch form, profiles/r3h_critpath.txt): forward split, backward not.
+GLOB3 = os.environ.get("PBX_GLOB3", "1") != "0"              # forward
+GLOB3_BWD = os.environ.get("PBX_GLOB3_BWD", "0") != "0"      # backward
 
 
 def glob_fused_ok(G: int, NGL: int) -> bool:
@@ -320,10 +330,19 @@ class FusedGlobalBlockFn(torch.autograd.Function):
             vp, TVk = vp.sum(dim=1, keepdim=True), 1
         gc, gbc = g.contiguous(), g_bf.contiguous()
 
-        _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
-                                        fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
-                                        gb if NGL else None),
-                  B, G, NGL, TVk, K, LN_EPS, _s(dev))
+        if GLOB3:
+            NCT = G // 64
+            z1, z2 = e(B, G), e(B, G)
+            part1, part2 = e(B, NCT, 2), e(B, NCT, 2)
+            _lib.call("pbx_glob3_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                             fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                             gb if NGL else None, z1, z2, part1, part2),
+                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
+        else:
+            _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                            fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                            gb if NGL else None),
+                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
         ctx.save_for_backward(g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT)
         ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
         ctx.meta = (TV, NGL)
@@ -365,21 +384,39 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         du1 = torch.empty((B, G), dtype=BF16, device=dev)
         du2 = torch.empty((B, G), dtype=BF16, device=dev)
         dugl = torch.empty((B, NGL), dtype=BF16, device=dev) if NGL else None
-        _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum, wp,
-                                        f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
-                                        dbgl if NGL else None, dwp),
-                  B, G, NGL, wp.numel(), _lib.ptr(_det_slab((B + 15) // 16, 6 * G + NGL + wp.numel(), dev)), _s(dev))
+        slab = None
+        if GLOB3_BWD:
+            NCT = G // 64
+            e = lambda *shape: torch.empty(shape, dtype=F32, device=dev)  # noqa: E731
+            slab = e((B + 15) // 16, _lib.lib().pbx_glob3_slab_cols(G, NGL))
+            _lib.call("pbx_glob3_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum,
+                                             wp, f1T, dg, dvs, du1, du2, dugl, e(B, G), e(B, G), e(B, NCT, 2),
+                                             e(B, NCT, 2)),
+                      B, G, NGL, wp.numel(), slab.data_ptr(), _s(dev))
+        else:
+            _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum,
+                                            wp, f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
+                                            dbgl if NGL else None, dwp),
+                      B, G, NGL, wp.numel(), _lib.ptr(_det_slab((B + 15) // 16, 6 * G + NGL + wp.numel(), dev)),
+                      _s(dev))
 
         def weight_grads():
+            if slab is not None:
+                # the per-row-tile column sums (bias / LayerNorm affine / attention-weight gradients)
+                _lib.call("pbx_glob3_fold", slab.data_ptr(), B, G, NGL, wp.numel(),
+                          _ptrs(db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl if NGL else None, dwp), _s(dev))
             addmm_into(dw1, du1.t(), g_bf)
             addmm_into(dw2, du2.t(), g1_bf)
             if NGL:
                 addmm_into(dwgl, dugl.t(), g2_bf)
 
         direct = all(gr.direct[i] for i in (0, 4)) and (not NGL or gr.direct[9])
+        if slab is not None:
+            direct = direct and all(gr.direct[i] for i in (1, 2, 3, 5, 6, 7, 8)) and (not NGL or gr.direct[10])
         if direct and streams.ENABLED and dev.type == "cuda" and not on_aux:
-            # dW = dU^T X (K = B rows) is off the critical path: the aux (weight-gradient) stream
-            streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf], name="wgrad")
+            # dW = dU^T X (K = B rows) and the column-sum fold are off the critical path: the aux
+            # (weight-gradient) stream
+            streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf, slab], name="wgrad")
         else:
             weight_grads()
         dvpart = dvs.unsqueeze(1).expand(B, TV, G)
@@ -527,15 +564,27 @@ class HeadsLossFn(torch.autograd.Function):
         else:
             scale = dtotal.reshape(1).to(F32).contiguous()
             dh_s = (dh.float() * scale.reshape(())).to(dh.dtype)
-        # local head: dWo = dz^T h (K = B*L, deterministic split-K), dbo from the per-tile partials
+        # weight gradients (dWo = dzl^T h with K = B*L, dbo, dWa = dz^T g2, dba) feed only the optimizer
+        # and the DP all-reduce: on the aux weight-gradient stream, beside the critical-path dg2 GEMM and
+        # the last block's backward
         V = wo.shape[0]
         hr = h.reshape(-1, h.shape[-1])
-        if scale is None:
-            _gemm(dzl[:, :V], hr, dwo, ta=True, tb=False, accumulate=True, pad_a=True)
+
+        def weight_grads():
+            if scale is None:
+                _gemm(dzl[:, :V], hr, dwo, ta=True, tb=False, accumulate=True, pad_a=True)
+            else:
+                dwo.add_(_gemm(dzl[:, :V], hr, torch.empty_like(dwo), ta=True, tb=False, pad_a=True) * scale)
+            _lib.call("pbx_colsum_add", dbo_part.data_ptr(), dbo_part.shape[0], V, dbo_dst.data_ptr(),
+                      _lib.ptr(scale), _s(dh.device))
+            go_head_weight_grads(dz_s, dba, g2_bf, dwa, dba_dst, scale)
+
+        dz_s = go_head_scaled_dz(dz, scale)
+        if all(gr.direct) and streams.ENABLED and dh.device.type == "cuda":
+            streams.launch(dh.device, weight_grads, keep=[dzl, h, dbo_part, dz_s, dba, g2_bf], name="wgrad")
         else:
-            dwo.add_(_gemm(dzl[:, :V], hr, torch.empty_like(dwo), ta=True, tb=False, pad_a=True) * scale)
-        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), dbo_part.shape[0], V, dbo_dst.data_ptr(), _lib.ptr(scale), st)
-        dg2 = go_head_backward(dz, dba, g2_bf, wa, dwa, dba_dst, scale)
+            weight_grads()
+        dg2 = go_head_input_grad(dz_s, g2_bf, wa)
 
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)
 
@@ -568,21 +617,36 @@ def go_head_forward(g2_bf: torch.Tensor, wa: torch.Tensor, ba: torch.Tensor, y_g
     return dz, dba, gx
 
 
+def go_head_scaled_dz(dz, scale=None):
+    """dz times the incoming loss gradient (device [1]) when it is not exactly 1 (column-padded copy)."""
+    if scale is None:
+        return dz
+    B, A = dz.shape
+    dz_s = torch.zeros((B, padded_cols(A)), dtype=BF16, device=dz.device)[:, :A]
+    dz_s.copy_(dz.float() * scale.reshape(()))
+    return dz_s
+
+
+def go_head_input_grad(dz_s, g2_bf, wa) -> torch.Tensor:
+    """dg2 = dz Wa (K = A: split-K)."""
+    dg2 = torch.empty((dz_s.shape[0], g2_bf.shape[1]), dtype=F32, device=dz_s.device)
+    _gemm(dz_s, bf16_of(wa), dg2, ta=False, tb=False, pad_a=True)
+    return dg2
+
+
+def go_head_weight_grads(dz_s, dba, g2_bf, dwa_dst, dba_dst, scale=None) -> None:
+    """dWa += dz^T g2, dba += s sum_rows(dz) (from the per-row-tile partials)."""
+    A = dz_s.shape[1]
+    _lib.call("pbx_colsum_add", dba.data_ptr(), dba.shape[0], A, dba_dst.data_ptr(), _lib.ptr(scale), _s(dz_s.device))
+    _gemm(dz_s, g2_bf, dwa_dst, ta=True, tb=False, accumulate=True, pad_a=True)
+
+
 def go_head_backward(dz, dba, g2_bf, wa, dwa_dst, dba_dst, scale=None) -> torch.Tensor:
     """dg2 = s dz Wa (K = A: split-K), dWa += s dz^T g2, dba += s sum_rows(dz); ``scale`` (device
     [1] or None) = the incoming gradient of the loss."""
-    B, A = dz.shape
-    st = _s(dz.device)
-    if scale is not None:
-        dz_s = torch.zeros((B, padded_cols(A)), dtype=BF16, device=dz.device)[:, :A]
-        dz_s.copy_(dz.float() * scale.reshape(()))
-    else:
-        dz_s = dz
-    _lib.call("pbx_colsum_add", dba.data_ptr(), dba.shape[0], A, dba_dst.data_ptr(), _lib.ptr(scale), st)
-    dg2 = torch.empty((B, g2_bf.shape[1]), dtype=F32, device=dz.device)
-    _gemm(dz_s, bf16_of(wa), dg2, ta=False, tb=False, pad_a=True)                   # dg2 = dz Wa
-    _gemm(dz_s, g2_bf, dwa_dst, ta=True, tb=False, accumulate=True, pad_a=True)      # dWa += dz^T g2
-    return dg2
+    dz_s = go_head_scaled_dz(dz, scale)
+    go_head_weight_grads(dz_s, dba, g2_bf, dwa_dst, dba_dst, scale)
+    return go_head_input_grad(dz_s, g2_bf, wa)
 
 
 _UNIT_LOSS_GRAD = [False]
