@@ -359,6 +359,234 @@ __global__ void __launch_bounds__(512) lhead_grad_kernel(const float* __restrict
     dbo_part[(size_t)blockIdx.x * V + tid] = s;
   }
 }
+
+// ---- one-launch form (B <= 512): a workgroup owns PP = 2 positions and ALL samples, so both batch
+// reductions ((max, sum exp), then T = sum_b G P) are workgroup-local and the head is one pass over h:
+// (1) Z = h Wo^T + bo for the 2B rows (MFMA) into an fp32 LDS table, (2) column (max, sum exp) ->
+// (M, 1/S), (3) per row P, the CE term and G P (P kept in registers), (4) column sums -> T, (5) dZ =
+// P (G - T) into the table and the bf16 dz rows for the dWo GEMM, (6) dbo partial and dh = dZ Wo (MFMA,
+// staged through LDS for 256-B row stores).  h is read once (512-B runs per sample), Z never leaves
+// the CU.
+constexpr int PP = 2;
+constexpr int BMAXF = 512;
+constexpr int ZS = VP + 1;        // fp32 row stride of the table (column walks hit distinct banks)
+constexpr int FUSED_LDS = PP * BMAXF * ZS * 4 + VP * 256 + VP * 4 + 8 * 64 * 8 + 64 * 8 + 64 * 4 + 8 * 4;
+
+__global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restrict__ h, const float* __restrict__ wo,
+                                                          const float* __restrict__ bo,
+                                                          const long long* __restrict__ y,
+                                                          const float* __restrict__ wl, bf16_t* __restrict__ dh,
+                                                          bf16_t* __restrict__ dz, float* __restrict__ dbo_part,
+                                                          float* __restrict__ loss_part, int B, int L, int V,
+                                                          float inv_bl) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* zt = reinterpret_cast<float*>(smem);                              // [PP * B][ZS]
+  unsigned char* wos = smem + PP * BMAXF * ZS * 4;                         // [32][128] bf16
+  float* bo_s = reinterpret_cast<float*>(wos + VP * 256);                  // [32]
+  float2* red = reinterpret_cast<float2*>(bo_s + VP);                      // [8][64]
+  float2* ms = red + 8 * 64;                                               // [64] (M, 1/S) per (p, v)
+  float* tt = reinterpret_cast<float*>(ms + 64);                           // [64] T per (p, v)
+  float* lred = tt + 64;                                                   // [8]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hh = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int l0 = blockIdx.x * PP;
+  const int NR = PP * B, NT = (NR + 31) / 32;
+  stage_wo(wos, bo_s, wo, bo, V);
+  __syncthreads();
+  // (1) logits
+  {
+    bf16x8 wf[8];
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(wos, swz256(r, kk * 2 + hh));
+    const float bv = bo_s[r];
+#pragma unroll 2
+    for (int t = w; t < NT; t += 8) {
+      const int row = min(t * 32 + r, NR - 1);
+      const int p = row / B, s = row - (row / B) * B;
+      const bf16_t* src = h + ((size_t)s * L + min(l0 + p, L - 1)) * CH + 8 * hh;
+      bf16x8 hf[8];
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) hf[kk] = *reinterpret_cast<const bf16x8*>(src + kk * 16);
+      f32x16_t acc = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) acc = mfma32(hf[kk], wf[kk], acc);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int rr = t * 32 + (e & 3) + 8 * (e >> 2) + 4 * hh;
+        if (rr < NR) zt[rr * ZS + r] = acc[e] + bv;
+      }
+    }
+  }
+  __syncthreads();
+  const int pair = tid & 63, part = tid >> 6;       // column (p, v) and sample slice of the reductions
+  const int pp = pair >> 5, pv = pair & 31;
+  // (2) (max, sum exp) over the samples of every (p, v)
+  {
+    float m = -3.0e38f, se = 0.f;
+    for (int s = part; s < B; s += 8) {
+      const float z = zt[(pp * B + s) * ZS + pv];
+      const float mn = fmaxf(m, z);
+      se = se * __expf(m - mn) + __expf(z - mn);
+      m = mn;
+    }
+    red[part * 64 + pair] = make_float2(m, se);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float mm = red[tid].x;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) mm = fmaxf(mm, red[k * 64 + tid].x);
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ss += red[k * 64 + tid].y * __expf(red[k * 64 + tid].x - mm);
+    ms[tid] = make_float2(mm, ss > 0.f ? 1.0f / ss : 0.f);
+  }
+  __syncthreads();
+  // (3) per row: P (registers), CE term, G P into the table
+  constexpr int RPT = PP * BMAXF / 512;             // rows per thread
+  float P[RPT][VP], rse[RPT], coef[RPT];
+  int yv[RPT];
+  float lsum = 0.f;
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int row = tid + 512 * k;
+    const int p = row / B, s = row - (row / B) * B;
+    const bool ok = row < NR && l0 + p < L;
+    const size_t gi = (size_t)s * L + min(l0 + p, L - 1);
+    yv[k] = ok ? (int)y[gi] : -1;
+    const float wgt = ok ? wl[gi] : 0.f;
+    coef[k] = wgt * inv_bl;
+    float e[VP], se = 0.f, py = 0.f;
+#pragma unroll
+    for (int v = 0; v < VP; ++v) {
+      const float2 mv = ms[(p & 1) * 32 + v];
+      const float z = row < NR ? zt[row * ZS + v] : 0.f;
+      P[k][v] = ok && v < V ? __expf(z - mv.x) * mv.y : 0.f;
+      e[v] = ok && v < V ? __expf(P[k][v]) : 0.f;
+      se += e[v];
+      py += v == yv[k] ? P[k][v] : 0.f;
+    }
+    rse[k] = se > 0.f ? 1.0f / se : 0.f;
+    lsum += ok ? wgt * (__logf(se) - py) : 0.f;
+    if (row < NR) {
+#pragma unroll
+      for (int v = 0; v < VP; ++v) zt[row * ZS + v] = coef[k] * (e[v] * rse[k] - (v == yv[k] ? 1.f : 0.f)) * P[k][v];
+    }
+  }
+  __syncthreads();
+  // (4) T = sum_b G P for every (p, v)
+  {
+    float a = 0.f;
+    for (int s = part; s < B; s += 8) a += zt[(pp * B + s) * ZS + pv];
+    red[part * 64 + pair] = make_float2(a, 0.f);
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += red[k * 64 + tid].x;
+    tt[tid] = a;
+  }
+  __syncthreads();
+  // (5) dZ = P (G - T): fp32 into the table, bf16 rows for the dWo GEMM
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int row = tid + 512 * k;
+    if (row >= NR) continue;
+    const int p = row / B, s = row - (row / B) * B;
+    const bool ok = l0 + p < L;
+    float d[VP];
+#pragma unroll
+    for (int v = 0; v < VP; ++v) {
+      const float G = coef[k] * (__expf(P[k][v]) * rse[k] - (v == yv[k] ? 1.f : 0.f));
+      d[v] = ok && v < V ? P[k][v] * (G - tt[(p & 1) * 32 + v]) : 0.f;
+      zt[row * ZS + v] = d[v];
+    }
+    if (ok) {
+      uint4* dst = reinterpret_cast<uint4*>(dz + ((size_t)s * L + l0 + p) * VP);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[c] = packq8(d + 8 * c);
+    }
+  }
+  lsum = wave_reduce_sum(lsum);
+  if (lane == 0) lred[w] = lsum;
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a += lred[k];
+    loss_part[blockIdx.x] = a * inv_bl;
+  }
+  // (6a) dbo partial: column sums of dZ (16 row slices of the 32 columns)
+  {
+    const int v = tid & 31, sl = tid >> 5;
+    float a = 0.f;
+    for (int row = sl; row < NR; row += 16) a += zt[row * ZS + v];
+    reinterpret_cast<float*>(red)[sl * 32 + v] = a;
+  }
+  // (6b) dh = dZ Wo: A fragments (bf16 of the fp32 table) of this wave's row tiles first
+  constexpr int TPW = PP * BMAXF / 32 / 8;          // row tiles per wave
+  bf16x8 fa[TPW][2];
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int row = (w + 8 * i) * 32 + r;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      float a8[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a8[j] = row < NR ? zt[row * ZS + kk * 16 + 8 * hh + j] : 0.f;
+      fa[i][kk] = pack8(a8);
+    }
+  }
+  __syncthreads();                                   // table and dbo slices read
+  if (tid < V) {
+    float a = 0.f;
+#pragma unroll
+    for (int sl = 0; sl < 16; ++sl) a += reinterpret_cast<float*>(red)[sl * 32 + tid];
+    dbo_part[(size_t)blockIdx.x * V + tid] = a;
+  }
+  unsigned char* myot = smem + w * PT * 256;        // per-wave [32][128] bf16 staging over the table
+#pragma unroll
+  for (int i = 0; i < TPW; ++i) {
+    const int t = w + 8 * i;
+    if (t >= NT) break;
+    f32x16_t acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = zero16();
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int rlo = kk * 16 + 8 * hh + q;
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        const int col = ct * 32 + tc;
+        const bf16x8 fb = cat_tr(lds_tr(wos, swz256e(rlo, col)), lds_tr(wos, swz256e(rlo + 4, col)));
+        acc[ct] = mfma32(fa[i][kk], fb, acc[ct]);
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        *reinterpret_cast<bf16_t*>(myot + swz256e((e & 3) + 8 * (e >> 2) + 4 * hh, ct * 32 + r)) = f2bf(acc[ct][e]);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int idx = lane + 64 * k;                 // 512 16-B chunks = 32 rows x 16
+      const int rr = idx >> 4, c8 = idx & 15;
+      const int row = t * 32 + rr;
+      const int p = row / B, s = row - (row / B) * B;
+      if (row < NR && l0 + p < L)
+        *reinterpret_cast<uint4*>(dh + ((size_t)s * L + l0 + p) * CH + c8 * 8) =
+            *reinterpret_cast<const uint4*>(myot + swz256(rr, c8));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+}
 }  // namespace
 
 // Workspace sizes (floats) for pbx_local_head3: Z [B*L*32], part/tpart [ceil(B/16) * L * 32 * 2] each,
@@ -391,5 +619,21 @@ PBX_EXPORT int pbx_local_head3(const void* h, const float* wo, const float* bo, 
   hipLaunchKernelGGL(lhead_fold_kernel, dim3(nf), dim3(256), 0, st, (const float2*)tpart, nch, L, (float2*)T, 1);
   hipLaunchKernelGGL(lhead_grad_kernel, dim3(nt), dim3(512), lds5, st, Z, (const float2*)MS, (const float2*)T,
                      (const long long*)y, wl, wo, bo, (bf16_t*)dh, (bf16_t*)dz, dbo_part, B, L, V, inv_bl);
+  return pbx_launch_status();
+}
+
+// One-launch head (B <= 512): dbo_part [ceil(L / 2)][V], loss_part [ceil(L / 2)] (each already / (B L))
+PBX_EXPORT int pbx_local_head_fused(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
+                                    void* dh, void* dz, float* dbo_part, float* loss_part, int B, int L, int V,
+                                    hipStream_t st) {
+  if (V > VP || V < 1 || B < 1 || B > BMAXF || L < 1) return (int)hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lhead_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FUSED_LDS);
+    attr = true;
+  }
+  const float inv_bl = 1.0f / ((float)B * (float)L);
+  hipLaunchKernelGGL(lhead_fused_kernel, dim3((L + PP - 1) / PP), dim3(512), FUSED_LDS, st, (const bf16_t*)h, wo, bo,
+                     (const long long*)y, wl, (bf16_t*)dh, (bf16_t*)dz, dbo_part, loss_part, B, L, V, inv_bl);
   return pbx_launch_status();
 }

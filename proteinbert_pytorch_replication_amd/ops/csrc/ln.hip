@@ -551,7 +551,10 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
 // the dv row, all 2 NJT GELU' fragments of the tile (one coalesced 1-KiB load each, ~32 KiB in
 // flight per wave), then the epilogue operands; no load is outstanding across the item loop's back
 // edge, so the compiler's waits stay exact.
-template <int NJT>
+// FIXTW: the grid stride is a multiple of the tiles per sample, so every item of a wave has the same
+// 32 positions and their [L, C] affine gamma is loaded once per wave, not per item (~16 of ~72 KB per
+// item; the compiler's vmcnt tracking wants the item loads branch-free, hence a template flag)
+template <int NJT, bool FIXTW>
 __global__ void __launch_bounds__(256) attn_bwd2_kernel(
     const bf16x8* __restrict__ gfrag, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
@@ -586,6 +589,14 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
     return dvpart + ((size_t)b * TV + (tw * 32) / BMV) * NJ;
   };
   long item = (long)blockIdx.x * NW + w;
+  float4 gq4[4][4];
+  if constexpr (FIXTW) {
+    const int pc = min((int)(item % TW) * 32 + r, L - 1);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ct * 32 + 8 * i + 4 * h);
+  }
   if (item < items) {
     const float* dvg = dv_src(item);
 #pragma unroll
@@ -617,7 +628,6 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
     const float dmask = dh2_in != nullptr ? 1.f : 0.f;
     const float* stb = st2 + (size_t)b * T2 * 2;
     uint2 dq[4][4], sq[4][4];
-    float4 gq4[4][4];
     float2 pm0, pm1;
     // the epilogue operands are issued EPI steps before the end of the tile: vmcnt counts at most 63
     // outstanding operations per wave (2 + 2 NJT ring + 50 would overflow it if issued up front)
@@ -633,7 +643,7 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
           const int ci0 = ct * 32 + 8 * i + 4 * h;
           dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
           sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
-          gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+          if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
         }
       pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
       pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
@@ -1125,8 +1135,10 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
@@ -1214,7 +1226,10 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
   long wgl = (items + nw - 1) / nw;
   if (wgl > num_cus()) wgl = num_cus();
   const int lds = NJ * 256 + nw * 2 * NJ * 4;
-  hipLaunchKernelGGL(NJ == 512 ? attn_bwd2_kernel<16> : attn_bwd2_kernel<8>, dim3((int)wgl), dim3(64 * nw), lds, st,
+  const bool fix = ((wgl * nw) % ((L + 31) / 32)) == 0;
+  const auto kern = NJ == 512 ? (fix ? attn_bwd2_kernel<16, true> : attn_bwd2_kernel<16, false>)
+                              : (fix ? attn_bwd2_kernel<8, true> : attn_bwd2_kernel<8, false>);
+  hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st,
                      (const bf16x8*)gfrag, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
                      (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
   return pbx_launch_status();

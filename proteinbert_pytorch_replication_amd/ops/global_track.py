@@ -33,6 +33,10 @@ _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_local_head3_tiles", [_I, _I])
+_lib.register("pbx_local_head_fused", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+# local head: one launch for B <= 512 (pbx_local_head_fused: 61 vs 108 us for the five-pass form at
+# B = L = 512, profiles/r3k_*); larger per-GPU batches take the five-pass form
+LHEAD_FUSED = True
 
 
 def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l: torch.Tensor, w_l: torch.Tensor,
@@ -45,6 +49,18 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     st = _s(dev)
     B, L, C = h.shape
     V = wo.shape[0]
+    if LHEAD_FUSED and B <= 512:
+        # one launch: a workgroup per 2 positions x all samples (the batch reductions stay on chip)
+        nt = (L + 1) // 2
+        dh = torch.empty_like(h)
+        dz = torch.empty((B * L, 32), dtype=BF16, device=dev)
+        dbo_part = torch.empty((nt, V), dtype=F32, device=dev)
+        lparts = torch.empty(nt, dtype=F32, device=dev)
+        _lib.call("pbx_local_head_fused", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
+                  y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dz.data_ptr(),
+                  dbo_part.data_ptr(), lparts.data_ptr(), B, L, V, st)
+        _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+        return dh, dz, dbo_part
     nt = _lib.lib().pbx_local_head3_tiles(B, L)          # the kernel's tile grid (16 samples x 32 positions)
     nch = (B + 15) // 16
     dh = torch.empty_like(h)

@@ -1,4 +1,5 @@
-"""GPU: the fused pretraining heads + loss (HeadsLossFn: the multi-pass local head of csrc/lhead.hip,
+"""GPU: the fused pretraining heads + loss (HeadsLossFn: the one-launch local head of csrc/lhead.hip
+for B <= 512 and its five-pass form,
 the GO head fused into the MFMA GEMM of csrc/gemm.hip) match the PyTorch fp32 reference
 (models/proteinbert.py heads_torch + train/losses.py) -- loss, dh, dg and every head parameter
 gradient (Wo, bo, Wa, ba), at the real 8943-wide GO head and at batch / length extents that leave
@@ -14,8 +15,11 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("B,L,A", [(6, 24, 96), (100, 24, 96), (512, 24, 96), (640, 24, 96), (6, 1100, 96),
                                    (40, 2000, 96), (512, 64, 8943), (300, 37, 8943), (17, 512, 8943)])
-def test_heads_loss_matches_torch(B, L, A):
+@pytest.mark.parametrize("lhead_fused", [True, False])
+def test_heads_loss_matches_torch(B, L, A, lhead_fused, monkeypatch):
+    from proteinbert_pytorch_replication_amd.ops import global_track
     from proteinbert_pytorch_replication_amd.ops.global_track import HeadsLossFn
+    monkeypatch.setattr(global_track, "LHEAD_FUSED", lhead_fused)
     torch.manual_seed(B + L)
     G = 256
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=G, key_dim=64, num_heads=4,
