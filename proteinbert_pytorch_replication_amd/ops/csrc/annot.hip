@@ -1,0 +1,365 @@
+// Sparse GO-annotation input layer: g0 = GELU(X W^T + b) and its weight / bias gradients,
+// where X [B, A] is the corrupted multi-hot annotation matrix (reference modules.py:255-262,301;
+// the input of global_linear_layer).  X is ~0.5 % dense (8943 GO terms, ~45 set per annotated
+// sequence) and half of the rows are blanked by the corruption (data_processing.py annotation noise),
+// so the dense [B, 8943] x [8943, G] GEMMs of the forward and of dW = dU^T X move ~18 MB of zeros
+// through the MFMA pipe for ~9 k useful rows.  Here:
+//
+//   ann_csr    one workgroup per row: ordered compaction of the non-zeros (ballot + popcount over
+//              register-held values in chunk-major order: the list is sorted by column, so the
+//              forward sum has a fixed order)
+//   ann_wt     fp32 W [G, A] -> bf16 W^T [A, G] through a padded LDS tile (one image per step)
+//   ann_fwd    one wave per row: acc[n] = sum_k v_k W^T[a_k, n] over the row's list (coalesced
+//              1-KB rows of W^T, 8 in flight), bias + exact-erf GELU epilogue -> pre (saved), g, g_bf
+//   ann_csc    64 columns per workgroup: per-column lists of (row, value) sorted by row
+//   ann_du     dU^T = (dG * GELU'(pre))^T through an LDS tile (rows of dU^T are what ann_wgrad reads)
+//   ann_wgrad  two W rows x 1/8 of the columns per workgroup: the two dU^T rows staged in LDS, the bias
+//              gradient as a fixed-order block sum, then dW[n, a] += sum over column a's list of
+//              v * dU[b, n] with consecutive threads on consecutive a (coalesced read-modify-write)
+//
+// Every sum runs in a fixed order (no float atomics): the layer is deterministic by construction.
+// Values are taken as stored (any float, not only {0, 1}); a NaN in X is a non-zero and propagates.
+#include "common.h"
+
+namespace {
+typedef unsigned short bf16_t;
+constexpr int CSR_NCH = 40;        // ann_csr: row values held in registers, A <= 256 * 40 = 10240
+constexpr int CSC_WAVES = 16;      // ann_csc: 1024 threads, rows split into 16 ranges ...
+constexpr int CSC_R = 32;          // ... of <= 32 rows held in registers per pass (512 rows per pass)
+constexpr int WG_SPLIT = 8;        // ann_wgrad: the A columns of a W row pair split over 8 workgroups
+constexpr int WG_COLS = 8;         // ann_wgrad: columns per thread per pass (loads issued together)
+
+// grid (B), block 256: every value of the row is loaded once, up front (one memory latency), then
+// counted and scattered from registers
+__global__ void __launch_bounds__(256) ann_csr_kernel(const float* __restrict__ ann, int A, int* __restrict__ cnt,
+                                                      int2* __restrict__ ent) {
+  __shared__ int wc[CSR_NCH * 4];
+  const int b = blockIdx.x;
+  const float* __restrict__ row = ann + (size_t)b * A;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nch = (A + 255) >> 8;
+  float v[CSR_NCH];
+#pragma unroll
+  for (int j = 0; j < CSR_NCH; ++j) {
+    const int a = (j << 8) + threadIdx.x;
+    v[j] = (j < nch && a < A) ? row[a] : 0.0f;
+  }
+  unsigned long long m[CSR_NCH];
+#pragma unroll
+  for (int j = 0; j < CSR_NCH; ++j) {
+    m[j] = __ballot(v[j] != 0.0f);
+    if (lane == 0 && j < nch) wc[j * 4 + w] = __popcll(m[j]);
+  }
+  __syncthreads();
+  if (w == 0) {
+    // exclusive scan of the nch * 4 (chunk, wave) counts in chunk-major order: lane i owns entries
+    // 4i .. 4i+3 (chunk i), a wave-wide scan of the per-chunk sums places them
+    int c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    if (lane < nch) {
+      c0 = wc[4 * lane];
+      c1 = wc[4 * lane + 1];
+      c2 = wc[4 * lane + 2];
+      c3 = wc[4 * lane + 3];
+    }
+    const int tot = c0 + c1 + c2 + c3;
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    if (lane < nch) {
+      const int ex = incl - tot;
+      wc[4 * lane] = ex;
+      wc[4 * lane + 1] = ex + c0;
+      wc[4 * lane + 2] = ex + c0 + c1;
+      wc[4 * lane + 3] = ex + c0 + c1 + c2;
+    }
+    if (lane == 63) cnt[b] = incl;
+  }
+  __syncthreads();
+  // scatter (column, value) in chunk-major / wave / lane order = ascending column
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  int2* __restrict__ out = ent + (size_t)b * A;
+#pragma unroll
+  for (int j = 0; j < CSR_NCH; ++j) {
+    if (j < nch && v[j] != 0.0f)
+      out[wc[j * 4 + w] + __popcll(m[j] & lt)] = make_int2((j << 8) + threadIdx.x, __float_as_int(v[j]));
+  }
+}
+
+// W [G, A] fp32 -> Wt [A, G] bf16.  grid (ceil(A / 64), G / 64), block 256
+__global__ void __launch_bounds__(256) ann_wt_kernel(const float* __restrict__ w, bf16_t* __restrict__ wt, int G,
+                                                     int A) {
+  __shared__ float tile[64][65];
+  const int a0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int n = n0 + r + 4 * i, a = a0 + c;
+    tile[r + 4 * i][c] = a < A ? w[(size_t)n * A + a] : 0.0f;
+  }
+  __syncthreads();
+  // 32 threads per output row (2 bf16 each), 8 rows per pass
+  const int cp = threadIdx.x & 31, rr = threadIdx.x >> 5;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int al = rr + 8 * i, a = a0 + al;
+    if (a < A) {
+      const unsigned int lo = f2bf(tile[2 * cp][al]), hi = f2bf(tile[2 * cp + 1][al]);
+      *reinterpret_cast<unsigned int*>(wt + (size_t)a * G + n0 + 2 * cp) = lo | (hi << 16);
+    }
+  }
+}
+
+// grid (ceil(B / 4)), block 256: one wave per row, lane l owns columns 8 l .. 8 l + 7 of every
+// 512-column slab (one 16-byte W^T load per entry per lane); the row list is walked 8 entries at a
+// time with all 8 loads in flight
+__global__ void __launch_bounds__(256) ann_fwd_kernel(const int* __restrict__ cnt, const int2* __restrict__ ent,
+                                                      const bf16_t* __restrict__ wt, const float* __restrict__ bias,
+                                                      float* __restrict__ pre, float* __restrict__ g,
+                                                      bf16_t* __restrict__ g_bf, int B, int A, int G) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const int c = cnt[b];
+  const int2* __restrict__ rent = ent + (size_t)b * A;
+  for (int s0 = 0; s0 < G; s0 += 512) {
+    const int col = s0 + 8 * lane;
+    const bool act = col < G;
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+    for (int k0 = 0; k0 < c; k0 += 64) {
+      // 64 entries of the list: one coalesced load, then broadcast by shuffles
+      const int2 mine = k0 + lane < c ? rent[k0 + lane] : make_int2(0, 0);
+      const int m = min(64, c - k0);
+      for (int j0 = 0; j0 < m; j0 += 8) {
+        bf16x8_t wv[8];
+        float vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u;
+          const int aj = __shfl(mine.x, j & 63, 64);
+          vv[u] = j < m ? __int_as_float(__shfl(mine.y, j & 63, 64)) : 0.0f;
+          wv[u] = (j < m && act) ? *reinterpret_cast<const bf16x8_t*>(wt + (size_t)aj * G + col) : (bf16x8_t){};
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+#pragma unroll
+          for (int i = 0; i < 8; ++i) acc[i] = fmaf(vv[u], bf2f((unsigned short)wv[u][i]), acc[i]);
+      }
+    }
+    if (act) {
+      const size_t o = (size_t)b * G + col;
+      float u8[8], g8[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        u8[i] = acc[i] + bias[col + i];
+        g8[i] = gelu_f(u8[i]);
+      }
+      *reinterpret_cast<f32x4_t*>(pre + o) = (f32x4_t){u8[0], u8[1], u8[2], u8[3]};
+      *reinterpret_cast<f32x4_t*>(pre + o + 4) = (f32x4_t){u8[4], u8[5], u8[6], u8[7]};
+      *reinterpret_cast<f32x4_t*>(g + o) = (f32x4_t){g8[0], g8[1], g8[2], g8[3]};
+      *reinterpret_cast<f32x4_t*>(g + o + 4) = (f32x4_t){g8[4], g8[5], g8[6], g8[7]};
+      bf16x8_t ob;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) ob[i] = (short)f2bf(g8[i]);
+      *reinterpret_cast<bf16x8_t*>(g_bf + o) = ob;
+    }
+  }
+}
+
+// grid (ceil(A / 64)), block 1024: lane = column, wave = row range; rows in passes of 512 with the
+// values of a pass held in registers (one memory latency per pass)
+__global__ void __launch_bounds__(1024) ann_csc_kernel(const float* __restrict__ ann, int B, int A,
+                                                       int* __restrict__ ccnt, int* __restrict__ cptr,
+                                                       int2* __restrict__ ent) {
+  __shared__ int wc[CSC_WAVES][64];
+  __shared__ int carry[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int a = blockIdx.x * 64 + lane;
+  const bool col_ok = a < A;
+  // column totals first (pass 1 over all rows), so the block's columns can be laid out contiguously
+  int n = 0;
+  for (int p0 = 0; p0 < B; p0 += CSC_WAVES * CSC_R) {
+    const int r0 = p0 + w * CSC_R;
+    float v[CSC_R];
+#pragma unroll
+    for (int i = 0; i < CSC_R; ++i) v[i] = (col_ok && r0 + i < B) ? ann[(size_t)(r0 + i) * A + a] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < CSC_R; ++i) n += v[i] != 0.0f;
+  }
+  wc[w][lane] = n;
+  __syncthreads();
+  if (w == 0) {
+    int tot = 0;
+#pragma unroll
+    for (int i = 0; i < CSC_WAVES; ++i) tot += wc[i][lane];
+    int incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += y;
+    }
+    const int base = blockIdx.x * 64 * B + (incl - tot);
+    if (col_ok) {
+      ccnt[a] = tot;
+      cptr[a] = base;
+    }
+    carry[lane] = base;
+  }
+  __syncthreads();
+  // pass 2: per 512-row pass, the per-wave counts of the pass give each wave's write offset
+  for (int p0 = 0; p0 < B; p0 += CSC_WAVES * CSC_R) {
+    const int r0 = p0 + w * CSC_R;
+    float v[CSC_R];
+#pragma unroll
+    for (int i = 0; i < CSC_R; ++i) v[i] = (col_ok && r0 + i < B) ? ann[(size_t)(r0 + i) * A + a] : 0.0f;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < CSC_R; ++i) k += v[i] != 0.0f;
+    wc[w][lane] = k;
+    __syncthreads();
+    int off = carry[lane];
+    for (int i = 0; i < w; ++i) off += wc[i][lane];
+    if (col_ok) {
+#pragma unroll
+      for (int i = 0; i < CSC_R; ++i)
+        if (v[i] != 0.0f) ent[off++] = make_int2(r0 + i, __float_as_int(v[i]));
+    }
+    __syncthreads();
+    if (w == CSC_WAVES - 1) carry[lane] = off;
+    __syncthreads();
+  }
+}
+
+// dU^T [G, B] = (dG * GELU'(pre))^T through a padded LDS tile.  grid (ceil(B / 64), G / 64), block 256
+__global__ void __launch_bounds__(256) ann_du_kernel(const float* __restrict__ dg, const float* __restrict__ pre,
+                                                     float* __restrict__ dut, int B, int G) {
+  __shared__ float tile[64][65];
+  const int b0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int b = b0 + r + 4 * i;
+    const size_t o = (size_t)b * G + n0 + c;
+    tile[r + 4 * i][c] = b < B ? dg[o] * gelu_grad_f(pre[o]) : 0.0f;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int nl = r + 4 * i, b = b0 + c;
+    if (b < B) dut[(size_t)(n0 + nl) * B + b] = tile[c][nl];
+  }
+}
+
+// grid (G / 2, WG_SPLIT), block 256, dynamic LDS 2 * B floats.  Workgroup (x, y) owns W rows 2x, 2x+1
+// and the y-th slice of the A columns; it stages the two dU^T rows (coalesced), the y = 0 slice also
+// writes the two bias gradients (fixed-order block sums).
+__global__ void __launch_bounds__(256) ann_wgrad_kernel(const float* __restrict__ dut, const int* __restrict__ ccnt,
+                                                        const int* __restrict__ cptr, const int2* __restrict__ ent,
+                                                        float* __restrict__ dw, float* __restrict__ db, int B, int A) {
+  extern __shared__ float du_s[];     // [2][B]
+  __shared__ float red[2][4];
+  const int n0 = blockIdx.x * 2;
+  float s0 = 0.0f, s1 = 0.0f;
+  for (int b = threadIdx.x; b < B; b += 256) {
+    const float d0 = dut[(size_t)n0 * B + b], d1 = dut[(size_t)(n0 + 1) * B + b];
+    du_s[b] = d0;
+    du_s[B + b] = d1;
+    s0 += d0;
+    s1 += d1;
+  }
+  if (blockIdx.y == 0) {
+    s0 = wave_reduce_sum(s0);
+    s1 = wave_reduce_sum(s1);
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = s0;
+      red[1][threadIdx.x >> 6] = s1;
+    }
+  }
+  __syncthreads();
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    db[n0] += (red[0][0] + red[0][1]) + (red[0][2] + red[0][3]);
+    db[n0 + 1] += (red[1][0] + red[1][1]) + (red[1][2] + red[1][3]);
+  }
+  const int per = (A + WG_SPLIT - 1) / WG_SPLIT;
+  const int a_lo = blockIdx.y * per, a_hi = min(A, a_lo + per);
+  float* __restrict__ dw0 = dw + (size_t)n0 * A;
+  float* __restrict__ dw1 = dw0 + A;
+  for (int a0 = a_lo + threadIdx.x; a0 < a_hi; a0 += 256 * WG_COLS) {
+    int c[WG_COLS], p[WG_COLS];
+    float w0[WG_COLS], w1[WG_COLS];
+#pragma unroll
+    for (int i = 0; i < WG_COLS; ++i) {     // metadata and the two dW values: all loads in flight
+      const int a = a0 + 256 * i;
+      const bool ok = a < a_hi;
+      c[i] = ok ? ccnt[a] : 0;
+      p[i] = ok ? cptr[a] : 0;
+      w0[i] = ok ? dw0[a] : 0.0f;
+      w1[i] = ok ? dw1[a] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < WG_COLS; ++i) {
+      float t0 = 0.0f, t1 = 0.0f;
+      for (int k = 0; k < c[i]; ++k) {
+        const int2 e = ent[p[i] + k];
+        const float v = __int_as_float(e.y);
+        t0 = fmaf(v, du_s[e.x], t0);
+        t1 = fmaf(v, du_s[B + e.x], t1);
+      }
+      const int a = a0 + 256 * i;
+      if (a < a_hi) {
+        dw0[a] = w0[i] + t0;
+        dw1[a] = w1[i] + t1;
+      }
+    }
+  }
+}
+}  // namespace
+
+PBX_EXPORT int pbx_ann_supported(int B, int A, int G) {
+  return B >= 1 && B <= 8192 && A >= 1 && A <= 256 * CSR_NCH && G >= 64 && G % 64 == 0 && G <= 4096;
+}
+
+// ann fp32 [B, A]; cnt int [B]; ent int2 [B * A]
+PBX_EXPORT int pbx_ann_csr(const float* ann, int B, int A, int* cnt, void* ent, hipStream_t st) {
+  if (!pbx_ann_supported(B, A, 64)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ann_csr_kernel, dim3(B), dim3(256), 0, st, ann, A, cnt, (int2*)ent);
+  return pbx_launch_status();
+}
+
+// w fp32 [G, A] -> wt bf16 [A, G]
+PBX_EXPORT int pbx_ann_wt(const float* w, void* wt, int G, int A, hipStream_t st) {
+  if (G % 64 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ann_wt_kernel, dim3((A + 63) / 64, G / 64), dim3(256), 0, st, w, (bf16_t*)wt, G, A);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_ann_fwd(const int* cnt, const void* ent, const void* wt, const float* bias, float* pre, float* g,
+                           void* g_bf, int B, int A, int G, hipStream_t st) {
+  if (!pbx_ann_supported(B, A, G)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ann_fwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, cnt, (const int2*)ent, (const bf16_t*)wt,
+                     bias, pre, g, (bf16_t*)g_bf, B, A, G);
+  return pbx_launch_status();
+}
+
+// ccnt, cptr int [A]; ent int2 [ceil(A / 64) * 64 * B]
+PBX_EXPORT int pbx_ann_csc(const float* ann, int B, int A, int* ccnt, int* cptr, void* ent, hipStream_t st) {
+  if (!pbx_ann_supported(B, A, 64)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ann_csc_kernel, dim3((A + 63) / 64), dim3(1024), 0, st, ann, B, A, ccnt, cptr, (int2*)ent);
+  return pbx_launch_status();
+}
+
+// dut scratch fp32 [G, B]; dw [G, A] += dU^T X, db [G] += colsum(dU), dU = dg * GELU'(pre)  (dg, pre fp32 [B, G])
+PBX_EXPORT int pbx_ann_wgrad(const float* dg, const float* pre, const int* ccnt, const int* cptr, const void* ent,
+                             float* dut, float* dw, float* db, int B, int A, int G, hipStream_t st) {
+  if (!pbx_ann_supported(B, A, G)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(ann_du_kernel, dim3((B + 63) / 64, G / 64), dim3(256), 0, st, dg, pre, dut, B, G);
+  const int rc = pbx_launch_status();
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(ann_wgrad_kernel, dim3(G / 2, WG_SPLIT), dim3(256), (size_t)2 * B * sizeof(float), st, dut, ccnt,
+                     cptr, (const int2*)ent, dw, db, B, A);
+  return pbx_launch_status();
+}

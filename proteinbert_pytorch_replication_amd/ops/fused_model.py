@@ -85,7 +85,7 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:
-            h, vpart = local_block(h, gb, blk, conv_imgs[i])
+            h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0))
             wp = att.W_parameter
         nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
         l1, l2 = blk.global_linear_layer_1[0], blk.global_linear_layer_2[0]

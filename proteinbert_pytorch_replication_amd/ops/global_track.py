@@ -192,33 +192,93 @@ class _Grads:
         return [None if (d or p is None) else g for p, g, d in zip(self.params, self.dst, self.direct)]
 
 
+_lib.register("pbx_ann_supported", [_I, _I, _I])
+_lib.register("pbx_ann_csr", [_P, _I, _I, _P, _P, _P])
+_lib.register("pbx_ann_wt", [_P, _P, _I, _I, _P])
+_lib.register("pbx_ann_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_ann_csc", [_P, _I, _I, _P, _P, _P, _P])
+_lib.register("pbx_ann_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+# sparse GO input layer (csrc/annot.hip); PBX_ANN_SPARSE=0 selects the dense MFMA-GEMM form
+ANN_SPARSE = os.environ.get("PBX_ANN_SPARSE", "1") != "0"
+
+
+def ann_sparse_ok(B: int, A: int, G: int) -> bool:
+    return ANN_SPARSE and bool(_lib.lib().pbx_ann_supported(B, A, G))
+
+
 class InputLayerFn(torch.autograd.Function):
     """g0 = GELU(ann W_in^T + b_in) (reference modules.py:255-262,301); ann is the corrupted GO
-    multi-hot (values {0, 1, 2}, exact in bf16)."""
+    multi-hot (values {0, 1, 2} from the corruption, any float accepted).
+
+    Sparse form (default, ``csrc/annot.hip``): the ~0.5 %-dense annotation rows are compacted to
+    ordered (column, value) lists and the layer gathers rows of a bf16 ``W^T`` image; the weight
+    gradient walks per-column (row, value) lists with ``dU = dG * GELU'(pre)`` kept on chip.  Dense
+    form: the in-tree MFMA GEMM on the padded bf16 annotations."""
 
     @staticmethod
     def forward(ctx, ann, w, b, wgl, bgl):
         dev = ann.device
         st = _s(dev)
         B, A = ann.shape
-        # the multi-hot annotations as bf16 ({0, 1, 2} exact) with the columns padded to 8 (16-B loads)
-        ann_pad = torch.empty((B, padded_cols(A)), dtype=BF16, device=dev)
-        ann_pad[:, A:].zero_()
-        ann_bf = ann_pad[:, :A]
-        ann_bf.copy_(ann)
-        wp = bf16_padded(w)                                                    # [G, A] bf16, padded
-        u = torch.empty((B, w.shape[0]), dtype=F32, device=dev)
-        _gemm(ann_bf, wp, u, ta=False, tb=True, pad_a=True, pad_b=True)
-        B, G = u.shape
-        g = torch.empty_like(u)
-        g_bf = torch.empty((B, G), dtype=BF16, device=dev)
-        _lib.call("pbx_bias_gelu", u.data_ptr(), b.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, G, st)
+        G = w.shape[0]
+        sparse = ann_sparse_ok(B, A, G)
+        if sparse:
+            annc = ann.float().contiguous()
+            train = any(ctx.needs_input_grad)
+            # training: the W^T image and the per-column lists (needed only by the backward) are built on
+            # the "ann" aux stream beside the row compaction / the rest of the forward
+            aux = train and streams.ENABLED and dev.type == "cuda"
+            wt = torch.empty((A, G), dtype=BF16, device=dev)
+            wd = w.detach().contiguous()
+            if aux:
+                with streams.on_aux(dev, "ann", keep=[annc, wd, wt]):
+                    _lib.call("pbx_ann_wt", wd.data_ptr(), wt.data_ptr(), G, A, _s(dev))
+            else:
+                _lib.call("pbx_ann_wt", wd.data_ptr(), wt.data_ptr(), G, A, st)
+            cnt = torch.empty(B, dtype=torch.int32, device=dev)
+            ent = torch.empty((B * A, 2), dtype=torch.int32, device=dev)
+            _lib.call("pbx_ann_csr", annc.data_ptr(), B, A, cnt.data_ptr(), ent.data_ptr(), st)
+            if aux:
+                streams.wait_for(dev, "ann")
+            u = torch.empty((B, G), dtype=F32, device=dev)             # pre-activation, bias included
+            g = torch.empty_like(u)
+            g_bf = torch.empty((B, G), dtype=BF16, device=dev)
+            _lib.call("pbx_ann_fwd", cnt.data_ptr(), ent.data_ptr(), wt.data_ptr(), b.detach().contiguous().data_ptr(),
+                      u.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, A, G, st)
+            saved_x = None
+            if train:
+                ccnt = torch.empty(A, dtype=torch.int32, device=dev)
+                cptr = torch.empty(A, dtype=torch.int32, device=dev)
+                cent = torch.empty(((A + 63) // 64 * 64 * B, 2), dtype=torch.int32, device=dev)
+                if aux:
+                    with streams.on_aux(dev, "ann", keep=[annc, ccnt, cptr, cent]):
+                        _lib.call("pbx_ann_csc", annc.data_ptr(), B, A, ccnt.data_ptr(), cptr.data_ptr(),
+                                  cent.data_ptr(), _s(dev))
+                    streams.mark_ready(dev, "ann", [ccnt])
+                else:
+                    _lib.call("pbx_ann_csc", annc.data_ptr(), B, A, ccnt.data_ptr(), cptr.data_ptr(), cent.data_ptr(),
+                              st)
+                ctx.csc = (ccnt, cptr, cent, A)
+        else:
+            # the multi-hot annotations as bf16 ({0, 1, 2} exact) with the columns padded to 8 (16-B loads)
+            ann_pad = torch.empty((B, padded_cols(A)), dtype=BF16, device=dev)
+            ann_pad[:, A:].zero_()
+            ann_bf = ann_pad[:, :A]
+            ann_bf.copy_(ann)
+            wp = bf16_padded(w)                                                    # [G, A] bf16, padded
+            u = torch.empty((B, G), dtype=F32, device=dev)
+            _gemm(ann_bf, wp, u, ta=False, tb=True, pad_a=True, pad_b=True)
+            g = torch.empty_like(u)
+            g_bf = torch.empty((B, G), dtype=BF16, device=dev)
+            _lib.call("pbx_bias_gelu", u.data_ptr(), b.data_ptr(), g.data_ptr(), g_bf.data_ptr(), B, G, st)
+            saved_x = ann_bf
         # block 0's global->local vector gb = GELU(g Wgl^T + bgl)
         ugl = mm32(g_bf, bf16_of(wgl).t())
         gb = torch.empty_like(ugl)
         _lib.call("pbx_bias_gelu", ugl.data_ptr(), bgl.data_ptr(), gb.data_ptr(), None, B, ugl.shape[1], st)
-        ctx.save_for_backward(ann_bf, u, g_bf, ugl)
+        ctx.save_for_backward(saved_x, u, g_bf, ugl)
         ctx.params = (w, b, wgl, bgl)
+        ctx.sparse = sparse
         ctx.mark_non_differentiable(g_bf)
         ctx.set_materialize_grads(False)     # no zero-filled gradients for unused outputs
         return g, g_bf, gb
@@ -229,7 +289,8 @@ class InputLayerFn(torch.autograd.Function):
         dev = saved[1].device
         if streams.GLOBAL_ENABLED and dev.type == "cuda":
             # weight gradients only: run on the global-track aux stream (ops/streams.py)
-            with streams.on_aux(dev, "global", keep=[*saved, dg, dgb]) as scope:
+            extra = list(ctx.csc[:3]) if getattr(ctx, "csc", None) is not None else []
+            with streams.on_aux(dev, "global", keep=[*saved, dg, dgb, *extra]) as scope:
                 out = InputLayerFn._backward(ctx, saved, dg, dgb)
                 scope.keep(*out)
             return out
@@ -237,7 +298,7 @@ class InputLayerFn(torch.autograd.Function):
 
     @staticmethod
     def _backward(ctx, saved, dg, dgb):
-        ann_bf, u, g_bf, ugl = saved
+        x, u, g_bf, ugl = saved
         w, b, wgl, bgl = ctx.params
         dev = u.device
         st = _s(dev)
@@ -252,10 +313,19 @@ class InputLayerFn(torch.autograd.Function):
                       dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, 32), N, dev)), st)
             addmm_into(dwgl, dugl.t(), g_bf)
             dg = addmm_new(dg, dugl, bf16_of(wgl))
+        if ctx.sparse:
+            ccnt, cptr, cent, A = ctx.csc
+            streams.wait_ready(ccnt)                # built on the "ann" aux stream in the forward
+            streams.queue_join()                    # release the forward's aux-stream keep list
+            dut = torch.empty((G, B), dtype=F32, device=dev)
+            _lib.call("pbx_ann_wgrad", dg.data_ptr(), u.data_ptr(), ccnt.data_ptr(), cptr.data_ptr(), cent.data_ptr(),
+                      dut.data_ptr(), dw.data_ptr(), db.data_ptr(), B, A, G, st)
+            del ctx.csc
+            return (None, *gr.finish())
         du = torch.empty((B, G), dtype=BF16, device=dev)
         _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
                   _lib.ptr(_det_slab(min(B, 32), G, dev)), st)
-        _gemm(du, ann_bf, dw, ta=True, tb=False, accumulate=True, pad_b=True)      # dW_in += du^T ann
+        _gemm(du, x, dw, ta=True, tb=False, accumulate=True, pad_b=True)      # dW_in += du^T ann
         return (None, *gr.finish())
 
 

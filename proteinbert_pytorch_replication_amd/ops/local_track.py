@@ -120,8 +120,13 @@ def _grad_dst(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
     return torch.zeros(shape, dtype=torch.float32, device=p.device), False
 
 
+# the first block's weight gradient is the last kernel of the backward (the main stream only has the
+# embedding / input-layer tail left beside it): it takes every CU (PBX_WGRAD_TAIL_FULL=0: 7/8 as the rest)
+WGRAD_TAIL_FULL = os.environ.get("PBX_WGRAD_TAIL_FULL", "1") != "0"
+
+
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
-           B: int, L: int, outs):
+           B: int, L: int, outs, full_chip: bool = False):
     """outs: [(dw, db)] destinations (accumulated into).  Returns the scratch tensors (the caller keeps
     them alive while the launch may still be running on another stream)."""
     dev = x.device
@@ -130,6 +135,8 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     # (R = 56 on 256 CUs): the aux-stream weight gradient runs beside the main-stream backward, and
     # leaving it a few CUs measured +2.4 % on the step over R = 64 (R = 48: +1.3 %, 32: -0.4 %)
     R = max(8, (7 * _num_cus(dev) // (16 * nconv)) // 8 * 8)
+    if full_chip:
+        R = max(8, (_num_cus(dev) // (2 * nconv)) // 8 * 8)
     R = min(R, ntiles)
     slab = torch.empty((R, nconv, KS, CH, CH), dtype=torch.float32, device=dev)
     bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
@@ -144,8 +151,10 @@ class LocalBlockFn(torch.autograd.Function):
     """Fused local track of one block (reference semantics)."""
 
     @staticmethod
-    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None):
-        """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch)."""
+    def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None,
+                tail: bool = False):
+        """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch);
+        ``tail``: the first block (its backward ends the step: the conv weight gradient gets every CU)."""
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
         B, L, C = x.shape
         assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
@@ -193,6 +202,7 @@ class LocalBlockFn(torch.autograd.Function):
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
         ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
+        ctx.tail = bool(tail) and WGRAD_TAIL_FULL
         ctx.set_materialize_grads(False)
         ctx.params = params
         return h2, vpart
@@ -251,7 +261,7 @@ class LocalBlockFn(torch.autograd.Function):
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
-            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
+            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], ctx.tail),
                            keep=[dpn, dpw, x], name="wgrad")
         else:
             _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
@@ -259,7 +269,7 @@ class LocalBlockFn(torch.autograd.Function):
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None, None)
+        return (dx, dgb, *pgrads, None, None, None, None)
 
 
 class EmbedFn(torch.autograd.Function):
@@ -314,12 +324,13 @@ def conv_images(wn: torch.Tensor, ww: torch.Tensor):
     return imgs, [(0, wn.detach(), imgs[0], imgs[1], KS, 0), (0, ww.detach(), imgs[2], imgs[3], KS, 0)]
 
 
-def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``)."""
+def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``); ``tail``: it is the first block."""
     att = blk.global_attention_layer
     wv = _wv_bf16(att)                                                       # [H*vd, C]
     nc = blk.local_narrow_conv_layer[0]
     wc = blk.local_wide_conv_layer[0]
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
-                              blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed)
+                              blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed,
+                              tail)

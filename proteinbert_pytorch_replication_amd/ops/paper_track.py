@@ -25,6 +25,7 @@ import torch
 
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
+from .gemm import gemm as _gemm
 from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
                            addmm_into)
 from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad
@@ -42,6 +43,10 @@ _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _
 PAPER_ATTN = os.environ.get("PBX_PAPER_ATTN", "fused")
 FUSED_CHUNK_F = 256                         # positions per forward work item
 FUSED_BWD_WAVES = int(os.environ.get("PBX_PF_BWD_WAVES", "8"))   # backward: 32 positions per wave
+
+# weight gradients of the K/V projections and of the local head (K = B*L reductions): the in-tree
+# split-K MFMA GEMM (default) or chunked library bmm (PBX_PAPER_WGRAD=bmm, A/B)
+PAPER_WGRAD_GEMM = os.environ.get("PBX_PAPER_WGRAD", "gemm") != "bmm"
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
@@ -165,9 +170,14 @@ class PaperBlockFn(torch.autograd.Function):
                           stream)
                 dh2_att = [torch.mm(dpre, wsave.t()), None]                               # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
-            nc = _split_k_chunks(R)
-            dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
-                              out_dtype=F32).sum(dim=0)                                   # [C, N] fp32
+            if PAPER_WGRAD_GEMM:
+                # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
+                dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
+                _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)                   # [C, N] fp32
+            else:
+                nc = _split_k_chunks(R)
+                dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
+                                  out_dtype=F32).sum(dim=0)                               # [C, N] fp32
             dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
             dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
             dqpre = dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)                              # [B, H, K]
@@ -259,8 +269,12 @@ class PaperHeadsLossFn(torch.autograd.Function):
         dlog_bf = dlog.to(BF16)
         # (the [B*L, 26] local-head products stay on the library GEMM: V = 26 is not an MFMA-tile shape)
         dh = torch.mm(dlog_bf, bf16_of(wo)).view(B, L, C)                             # bf16
-        nc = _split_k_chunks(B * L)                                                    # K = B*L: split-K
-        dwo = torch.bmm(dlog_bf.view(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C), out_dtype=F32).sum(dim=0)
+        if PAPER_WGRAD_GEMM:
+            dwo = torch.empty((V, C), dtype=F32, device=dev)
+            _gemm(dlog_bf, hb.reshape(B * L, C), dwo, ta=True, tb=False)                 # K = B*L: split-K
+        else:
+            nc = _split_k_chunks(B * L)
+            dwo = torch.bmm(dlog_bf.view(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C), out_dtype=F32).sum(dim=0)
         dbo = dlog.sum(dim=0)
         dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
         ctx.save_for_backward(dh, dwo, dbo, dz, dba, gx)

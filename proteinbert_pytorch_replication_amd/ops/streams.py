@@ -35,7 +35,9 @@ import torch
 ENABLED = os.environ.get("PBX_AUX_STREAM", "1") != "0"            # conv weight gradient
 # The global-track backward on its own stream measured SLOWER on MI355X (5.2 -> 5.4-5.8 ms/step,
 # paper config): its small hipBLASLt GEMMs take CUs from the critical-path conv data gradient beside
-# the weight-gradient stream; a high-priority critical-path stream did not recover it.  Off by default.
+# the weight-gradient stream; a high-priority critical-path stream did not recover it.  Round 3, with the
+# one-kernel global backward: still 1 % slower, and 1 % slower again with the global stream at high
+# priority (profiles/r3o_global_stream_prio_ab.txt: it gets CUs only as the data gradient drains).  Off.
 GLOBAL_ENABLED = os.environ.get("PBX_GLOBAL_STREAM", "0") == "1"
 
 _streams: Dict[Tuple[int, str], torch.cuda.Stream] = {}
@@ -63,6 +65,11 @@ def active(device: Optional[torch.device] = None) -> bool:
     if device is None:
         return any(_pending.values())
     return bool(_pending.get(_idx(device)))
+
+
+def queue_join() -> None:
+    """Queue :func:`join` at the end of the running backward pass (no-op outside one)."""
+    _queue_join()
 
 
 def _queue_join() -> None:
@@ -124,6 +131,11 @@ def mark_ready(device: torch.device, name: str, tensors: Iterable[torch.Tensor])
     for t in tensors:
         if isinstance(t, torch.Tensor):
             _ready[t.data_ptr()] = (_idx(device), name)
+
+
+def wait_for(device: torch.device, name: str) -> None:
+    """Current stream waits for the work enqueued on aux stream ``name`` so far."""
+    torch.cuda.current_stream(_idx(device)).wait_stream(_aux(device, name))
 
 
 def wait_ready(*tensors) -> None:
