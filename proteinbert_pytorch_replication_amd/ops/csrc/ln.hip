@@ -1240,34 +1240,49 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
 // dwl_slab (nullable): [slab_rows][128 * 128 + 128] scratch for per-workgroup dWl / dbl partials (else
 // atomics).  det: one workgroup per position pair for every sample (the [L, C] affine gradients then
 // have a single writer each) -- with the slab the whole kernel is run-to-run deterministic.
+// grid of ln2_linear_bwd_kernel: (position-pair groups, sample splits)
+static void ln2_bwd_grid(int B, int L, int det, int& gx, int& nsplit) {
+  const int pairs = (L + 1) / 2;
+  const int target = num_cus();
+  nsplit = (target + pairs - 1) / pairs;            // at least one workgroup per CU
+  if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
+  if (nsplit < 1 || det) nsplit = 1;
+  // long sequences: one workgroup walks several position pairs (its dWl partial is flushed once; at
+  // L = 4096 one workgroup per pair made 33 M float atomics on the 16 K dWl elements)
+  gx = pairs < target ? pairs : target;
+}
+
+// slab rows (workgroups) the dWl / dbl partials of pbx_ln2_linear_bwd occupy
+PBX_EXPORT int pbx_ln2_bwd_slab_rows(int B, int L, int det) {
+  int gx, nsplit;
+  ln2_bwd_grid(B, L, det, gx, nsplit);
+  return gx * nsplit;
+}
+
+// fold: 1 = the dWl / dbl slab partials are summed into dwl / dbl here (same stream); 0 = the caller
+// folds them later (pbx_colsum_add over pbx_ln2_bwd_slab_rows rows, e.g. on the weight-gradient stream)
 PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* st2, const float* sums2, int TS2,
                                   const float* g2, const void* pre_l, const void* s1, const float* st1, int T1,
                                   int BM1, const float* g1, const float* be1, const void* wl, float* consts,
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, float* dgb_zero, int B, int L, float eps, float* dwl_slab, int slab_rows,
-                                  int det, hipStream_t st) {
+                                  int det, int fold, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
   hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
                      consts, dgb_zero, B, L, eps);
-  const int pairs = (L + 1) / 2;
-  const int target = num_cus();
-  int nsplit = (target + pairs - 1) / pairs;        // at least one workgroup per CU
-  if (nsplit > (B + 15) / 16) nsplit = (B + 15) / 16;
-  if (nsplit < 1 || det) nsplit = 1;
-  // long sequences: one workgroup walks several position pairs (its dWl partial is flushed once; at
-  // L = 4096 one workgroup per pair made 33 M float atomics on the 16 K dWl elements)
-  const int gx = pairs < target ? pairs : target;
+  int gx, nsplit;
+  ln2_bwd_grid(B, L, det, gx, nsplit);
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;
   // dWl partials: one slab row per workgroup when the caller's slab is large enough, else atomics
   const int nwg = gx * nsplit;
   float* slab = dwl_slab != nullptr && nwg <= slab_rows ? dwl_slab : nullptr;
   float* bslab = slab != nullptr ? slab + (size_t)slab_rows * CH * CH : nullptr;    // [slab_rows][128] after dWl's
-  if (det && slab == nullptr) return (int)hipErrorInvalidValue;
+  if ((det || !fold) && slab == nullptr) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(ln2_linear_bwd_kernel, dim3(gx, nsplit), dim3(512), lds, st, (const bf16_t*)dh2,
                      (const bf16_t*)s2, g2, (const bf16_t*)pre_l, (const bf16_t*)s1, g1, be1, (const bf16_t*)wl,
                      consts, (bf16_t*)dh1, sums1, dg2, db2, dg1, db1, dwl, dbl, slab, bslab, B, L);
-  if (slab != nullptr) {
+  if (slab != nullptr && fold) {
     int rc = pbx_launch_status();
     if (rc != 0) return rc;
     rc = pbx_colsum_add(slab, nwg, CH * CH, dwl, nullptr, st);

@@ -287,12 +287,17 @@ class InputLayerFn(torch.autograd.Function):
     def backward(ctx, dg, _dgbf, dgb):
         saved = ctx.saved_tensors
         dev = saved[1].device
-        if streams.GLOBAL_ENABLED and dev.type == "cuda":
-            # weight gradients only: run on the global-track aux stream (ops/streams.py)
+        early = dev.type == "cuda" and streams.forked(dev, "ann")
+        if early and not all(_Grads(list(ctx.params)).direct):
+            streams.cancel_fork(dev, "ann")   # returned gradients are read by autograd on this stream
+            early = False
+        if (streams.GLOBAL_ENABLED or early) and dev.type == "cuda":
+            # weight gradients only: an aux stream (ops/streams.py) -- "ann", forked by the first local
+            # block's backward right after dgb was final, or the global-track stream
             extra = list(ctx.csc[:3]) if getattr(ctx, "csc", None) is not None else []
-            with streams.on_aux(dev, "global", keep=[*saved, dg, dgb, *extra]) as scope:
+            with streams.on_aux(dev, "ann" if early else "global", keep=[*saved, dg, dgb, *extra]) as scope:
                 out = InputLayerFn._backward(ctx, saved, dg, dgb)
-                scope.keep(*out)
+                scope.keep(*[t for t in out if isinstance(t, torch.Tensor)])
             return out
         return InputLayerFn._backward(ctx, saved, dg, dgb)
 

@@ -39,7 +39,9 @@ _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _P])
+                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _P])
+_lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
+_lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
@@ -123,6 +125,12 @@ def _grad_dst(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
 # the first block's weight gradient is the last kernel of the backward (the main stream only has the
 # embedding / input-layer tail left beside it): it takes every CU (PBX_WGRAD_TAIL_FULL=0: 7/8 as the rest)
 WGRAD_TAIL_FULL = os.environ.get("PBX_WGRAD_TAIL_FULL", "1") != "0"
+# the local-MLP dWl / dbl slab folds run on the weight-gradient stream (PBX_LN2_LATE_FOLD=0: on the main
+# stream right after the LN2 / MLP backward kernel)
+LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
+# the input layer's backward starts beside the first block's conv data gradient (PBX_INPUT_BWD_EARLY=0:
+# on the main stream after it)
+INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
 
 
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
@@ -240,11 +248,28 @@ class LocalBlockFn(torch.autograd.Function):
         sums1 = torch.empty((B, TS1, 2), dtype=torch.float32, device=dev)
         consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
         dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts kernel
+        det = int(fused_deterministic())
+        # the local-MLP weight / bias gradient partials are folded on the weight-gradient stream (only the
+        # optimizer and the DP all-reduce read them): a slab of this call's own, the shared one is reused
+        # by the next block's kernel while the fold may still be queued
+        late_fold = LN2_LATE_FOLD and streams.ENABLED and dev.type == "cuda" and dsts[6][1] and dsts[7][1]
+        if late_fold:
+            rows = _lib.lib().pbx_ln2_bwd_slab_rows(B, L, det)
+            fslab = torch.empty(rows * (CH * CH + CH), dtype=torch.float32, device=dev)
+            slab_args = (fslab.data_ptr(), rows)
+        else:
+            slab_args = dwl_slab(dev)
         _lib.call("pbx_ln2_linear_bwd", dh2t.data_ptr(), s2.data_ptr(), st2.data_ptr(), sums2.data_ptr(), TA,
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, *dwl_slab(dev), int(fused_deterministic()), stream)
+                  dgb.data_ptr(), B, L, LN_EPS, *slab_args, det, int(not late_fold), stream)
+        if late_fold:
+            def fold(slab=fslab, rows=rows, dwl=dwl, dbl=dbl):
+                st = _lib.stream_ptr(dev)
+                _lib.call("pbx_colsum_add", slab.data_ptr(), rows, CH * CH, dwl.data_ptr(), None, st)
+                _lib.call("pbx_colsum_add", slab[rows * CH * CH:].data_ptr(), rows, CH, dbl.data_ptr(), None, st)
+            streams.launch(dev, fold, keep=[fslab], name="wgrad")
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
@@ -257,6 +282,12 @@ class LocalBlockFn(torch.autograd.Function):
             # the previous block's global-track backward (next autograd node, aux stream) needs only
             # dgb: let it start here, beside the conv data gradient below
             streams.fork(dev, "global")
+        if ctx.tail and INPUT_BWD_EARLY and streams.ENABLED and dev.type == "cuda":
+            # first block: the input layer's backward (the last autograd node but one) needs only dgb and
+            # the global-track gradient, both final here -- it runs on the "ann" stream beside this conv
+            # data gradient, so its 18 MB weight-gradient bucket is ready ~0.2 ms earlier for the DP
+            # all-reduce (ops/global_track.py InputLayerFn.backward)
+            streams.fork(dev, "ann")
         conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer

@@ -100,6 +100,15 @@ def fork(device: torch.device, name: str) -> None:
     _forked[(_idx(device), name)] = True
 
 
+def forked(device: torch.device, name: str) -> bool:
+    """A :func:`fork` of aux stream ``name`` is pending (the next :func:`on_aux` starts from it)."""
+    return _forked.get((_idx(device), name), False)
+
+
+def cancel_fork(device: torch.device, name: str) -> None:
+    _forked.pop((_idx(device), name), None)
+
+
 @contextmanager
 def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
     """Run the body on aux stream ``name`` of ``device`` after the current stream's work (or after

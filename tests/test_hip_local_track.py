@@ -142,8 +142,9 @@ def test_full_model_loss_and_grads_vs_torch(nblocks):
         err = (got[n].float() - p.grad.float()).norm().item()
         print(f"{n:60s} |g|={norms[n]:.3e} err={err:.3e}")
         # the local-output bias is a softmax-over-batch invariant: its exact gradient
-        # is 0, so it is checked against the gradient scale of the model, not relative to itself
-        assert err < 6e-2 * norms[n] + 1e-4 * scale, f"{n}: err {err:.3e} vs |g| {norms[n]:.3e}"
+        # is 0, so it is checked against the gradient scale of the model, not relative to itself.
+        # Observed on MI355X (profiles/r3u_grad_errors.log): worst relative error 1.8e-2 (bf16 activations)
+        assert err < 3e-2 * norms[n] + 1e-4 * scale, f"{n}: err {err:.3e} vs |g| {norms[n]:.3e}"
 
 
 def test_arena_direct_grads_match_autograd_path():
@@ -169,4 +170,5 @@ def test_arena_direct_grads_match_autograd_path():
     scale = sorted(r.norm().item() for r in ref.values())[len(ref) // 2]
     for n in ref:
         err = (direct[n] - ref[n]).norm().item()
-        assert err < 6e-2 * ref[n].norm().item() + 1e-4 * scale, f"{n}: err {err:.3e} |g| {ref[n].norm().item():.3e}"
+        print(f"{n:60s} |g|={ref[n].norm().item():.3e} err={err:.3e}")
+        assert err < 3e-2 * ref[n].norm().item() + 1e-4 * scale, f"{n}: err {err:.3e} |g| {ref[n].norm().item():.3e}"

@@ -1,10 +1,15 @@
 """Data-parallel overlap evidence on ONE GPU: a 1-rank RCCL ("nccl") process group with the bucketed
 all-reduce forced on (``BucketedAllReduce(force=True)``), so every 8 MB gradient bucket's collective
-is issued on the communication stream while backward runs, exactly as on N ranks.  Run it under
-``rocprofv3 --kernel-trace`` and summarise with ``--summarize trace.csv``:
+is issued on the communication stream while backward runs, exactly as on N ranks.
 
-    rocprofv3 --kernel-trace --output-format csv -d out -- python3 tools/dp_timeline.py --steps 4
-    python3 tools/dp_timeline.py --summarize out/.../kernel_trace.csv
+RCCL launches no kernel for a 1-rank all-reduce, so the timeline is taken with HIP events: one on the
+main stream at the step start, one on the communication stream right before each bucket's
+``all_reduce`` (it completes when the bucket's gradients are final: the comm stream waits for the main
+and aux streams), one on the main stream after the last backward kernel and one after Adam.  A bucket
+whose event lands before the backward end is a collective that runs under the backward on N ranks.
+
+    python3 tools/dp_timeline.py --steps 6
+(``--summarize trace.csv`` lists collective kernels of a multi-rank rocprofv3 kernel trace.)
 """
 import argparse
 import csv
@@ -33,10 +38,42 @@ def run(a):
     ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb, force=True)
     step = PretrainStep(m, opt, ddp)
     gen = SyntheticUniRefGO(512, 8943, a.batch, dev, seed=1)
-    for _ in range(a.steps):
+    marks = []
+    orig_ar = dist.all_reduce
+
+    def all_reduce(t, *args, **kw):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))          # the communication stream
+        marks.append((ev, t.numel() * t.element_size()))
+        return orig_ar(t, *args, **kw)
+
+    dist.all_reduce = all_reduce
+    orig_finish = ddp.finish
+
+    def finish(*args, **kw):                               # called right after backward (+ aux join)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        marks.append((ev, -1))
+        return orig_finish(*args, **kw)
+
+    ddp.finish = finish
+    for i in range(a.steps):
+        marks.clear()
+        t0 = torch.cuda.Event(enable_timing=True)
+        t1 = torch.cuda.Event(enable_timing=True)
+        t0.record()
         loss = step(*gen.next_batch())
-    torch.cuda.synchronize()
-    print(f"buckets {len(ddp.buckets)}  loss {float(loss):.4f}", flush=True)
+        t1.record()
+        torch.cuda.synchronize()
+        if i == a.steps - 1:
+            total = t0.elapsed_time(t1)
+            print(f"step {total:.3f} ms, {len(ddp.buckets)} buckets of <= {a.bucket_mb:g} MB, loss {float(loss):.4f}")
+            bwd_end = next(t0.elapsed_time(ev) for ev, n in marks if n < 0)
+            for k, (ev, n) in enumerate(x for x in marks if x[1] >= 0):
+                t = t0.elapsed_time(ev)
+                print(f"  bucket {k:2d}  {n / 2**20:6.2f} MB  gradients final at {t:7.3f} ms"
+                      f"  ({'inside backward' if t < bwd_end - 1e-3 else 'after backward'})")
+            print(f"  backward (+ aux streams) ends at {bwd_end:.3f} ms; Adam ends at {total:.3f} ms")
     dist.destroy_process_group()
 
 
