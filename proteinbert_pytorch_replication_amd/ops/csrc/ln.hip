@@ -401,7 +401,7 @@ __device__ long long* pbx_stamp_buf;
 // ~248 VGPRs, two waves per SIMD).  NI: GELU pairs interleaved per core call.
 // PRENORM: s2 already holds the normalised rows (h2 from ln2_apply_kernel); no statistics, no affine
 // loads and no h2 stores (the [L, C] fp32 affine re-read per 64-position item cost ~35 us of ~175)
-template <int NWAVE, int NI, bool PRENORM>
+template <int NWAVE, int NI, bool PRENORM, bool STOREG = true>   // STOREG: GELU' fragments for attn_bwd2
 __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
     const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
@@ -469,6 +469,27 @@ __global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
     bf16x8* gdst = gfrag + ((size_t)b * 2 * TW64 + NP * tw) * NJT * 2 * 64 + lane;
     auto epi = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
       f32x2 sv = {0.f, 0.f};
+      if constexpr (!STOREG) {
+        // GELU only (the backward recomputes GELU', attn_bwd3)
+        constexpr int NPAIR = 8 * NP;
+#pragma unroll
+        for (int c8 = 0; c8 < NPAIR; c8 += NI) {
+          f32x2 xv[NI], gv[NI];
+#pragma unroll
+          for (int k = 0; k < NI; ++k) {
+            const int pi = c8 + k;
+            const f32x16_t& c = (pi >> 3) ? c1 : c0;
+            xv[k] = (f32x2){c[2 * (pi & 7)], c[2 * (pi & 7) + 1]};
+          }
+          gelu2_fast_n<NI, false>(xv, gv);
+#pragma unroll
+          for (int k = 0; k < NI; ++k) sv += gv[k];
+        }
+        float sacc = sv.x + sv.y;
+        sacc += __shfl_xor(sacc, 32, 64);
+        if (h == 0) vrow[jt * 32 + r] = sacc;
+        return;
+      }
       // GELU / GELU' of the item's 32x32 tiles: NI pairs per interleaved core call
       constexpr int NPAIR = 8 * NP;
       f32x2 gdall[NPAIR];
@@ -714,6 +735,191 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
       sums2[((size_t)b * TW + tw) * 2] = sa;
       sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
     }
+  }
+}
+
+// attention pool backward that RECOMPUTES GELU'(h2 Wv) instead of streaming the stored fragments
+// (268 MB per block at B = L = 512, the dominant traffic of attn_bwd2):
+//   zT[j][pos]  = sum_c Wv[j][c] h2[pos][c]      MFMA, A = Wv rows (LDS), B = the tile's h2 rows (registers)
+//   uT[j][pos]  = dv[b][j] GELU'(zT[j][pos])     VALU on the 16 accumulator values of each lane
+//   dh^T[c][pos] += sum_j Wv[j][c] uT[j][pos]    MFMA, A = Wv^T read transposed from LDS
+// The D layout of zT (lane = position, rows 4h + {0..3, 8..11} + 16 s of a 32-row chunk) is the B
+// operand of the second product with its K order permuted to {4h + 0..3, 8 + 4h + 0..3} per 16-step,
+// which is exactly the order the transposed Wv reads of attn_bwd2 deliver: no data movement between
+// the two MFMAs.  The GELU' of chunk jt runs while the MFMAs of chunk jt + 1's zT are in flight.
+// Epilogue (dh2 = bf16(dh2_in + dh), LN2 partials) as attn_bwd2.  One wave per SIMD.
+template <int NJT, bool FIXTW>
+__global__ void __launch_bounds__(256) attn_bwd3_kernel(
+    const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
+    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
+    const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, float eps) {
+  constexpr int NJ = NJT * 32;
+  constexpr int NDV = NJ / 256;                     // 1-KiB DMA instructions per dv row
+  constexpr int NW = 4;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  unsigned char* ws = smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int T2 = (L + BML - 1) / BML;
+  const int TW = (L + 31) / 32;
+  const int TV = (L + BMV - 1) / BMV;
+  const long items = (long)B * TW;
+  const long stride = (long)gridDim.x * NW;
+  stage_weight(ws, wv, NJ);
+  unsigned char* dvslot = ws + NJ * 256 + w * 2 * NJ * 4;
+  int woff[4], woff8[4];   // Wv^T fragment offsets at 16-step 0; step i adds 16 i rows = 4096 i bytes
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    woff[ct] = swz256e(4 * h + q, ct * 32 + tc);
+    woff8[ct] = swz256e(4 * h + q + 8, ct * 32 + tc);
+  }
+  auto dv_src = [&](long it) {
+    const int b = (int)(it / TW), tw = (int)(it - (it / TW) * TW);
+    return dvpart + ((size_t)b * TV + (tw * 32) / BMV) * NJ;
+  };
+  long item = (long)blockIdx.x * NW + w;
+  float4 gq4[4][4];
+  if constexpr (FIXTW) {
+    const int pc = min((int)(item % TW) * 32 + r, L - 1);
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ct * 32 + 8 * i + 4 * h);
+  }
+  if (item < items) {
+    const float* dvg = dv_src(item);
+#pragma unroll
+    for (int k = 0; k < NDV; ++k) glds16_ln(dvg + lane * 4 + 256 * k, dvslot + 1024 * k);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  int slot = 0;
+  for (; item < items; item += stride, slot ^= 1) {
+    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
+    const int pos = tw * 32 + r;
+    const bool okb = pos < L;
+    const float* dv = reinterpret_cast<const float*>(dvslot + slot * NJ * 4);
+    const bool has_next = item + stride < items;
+    const float* dvn = dv_src(has_next ? item + stride : item);
+    const int pc = min(pos, L - 1);
+    const size_t roff = ((size_t)b * L + pc) * CH;
+    // the tile's h2 rows as B fragments (lane: position r, channels 16 kk + 8 h ..), issued first
+    uint4 hq[8];
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) hq[kk] = *reinterpret_cast<const uint4*>(h2 + roff + kk * 16 + 8 * h);
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16_t* dsrc = dh2_in != nullptr ? dh2_in : s2;
+    const float dmask = dh2_in != nullptr ? 1.f : 0.f;
+    const float* stb = st2 + (size_t)b * T2 * 2;
+    uint2 dq[4][4], sq[4][4];
+    float2 pm0, pm1;
+    // epilogue operands and the next item's dv row: in flight during the whole MFMA / GELU' body
+    if (has_next) {
+#pragma unroll
+      for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ci0 = ct * 32 + 8 * i + 4 * h;
+        dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
+        sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
+        if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+      }
+    pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
+    pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
+    bf16x8 hf[8];
+    const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) hf[kk] = __builtin_bit_cast(bf16x8, okb ? hq[kk] : zq);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    f32x16_t y[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
+    auto zchunk = [&](int jt) {
+      f32x16_t z = zero16();
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) z = mfma32(lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h)), hf[kk], z);
+      return z;
+    };
+    f32x16_t zc = zchunk(0);
+#pragma unroll 2
+    for (int jt = 0; jt < NJT; ++jt) {
+      f32x16_t zn = zc;
+      if (jt + 1 < NJT) zn = zchunk(jt + 1);          // in flight during this chunk's GELU'
+      f32x2 xv[8], gd[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) xv[i] = (f32x2){zc[2 * i], zc[2 * i + 1]};
+      gelu2_fast_n<8, true>(xv, gd);
+      // reg 4g + e <-> j = 32 jt + 8 g + 4 h + e
+      float u[16];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const float4 d4 = *reinterpret_cast<const float4*>(dv + jt * 32 + 8 * g + 4 * h);
+        u[4 * g] = gd[2 * g].x * d4.x;
+        u[4 * g + 1] = gd[2 * g].y * d4.y;
+        u[4 * g + 2] = gd[2 * g + 1].x * d4.z;
+        u[4 * g + 3] = gd[2 * g + 1].y * d4.w;
+      }
+      const bf16x8 b0 = pack8(u), b1 = pack8(u + 8);
+#pragma unroll
+      for (int sidx = 0; sidx < 2; ++sidx) {
+        const unsigned char* wsi = ws + 4096 * (2 * jt + sidx);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct) {
+          const bf16x8 fw = cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct]));
+          y[ct] = mfma32(fw, sidx ? b1 : b0, y[ct]);
+        }
+      }
+      zc = zn;
+    }
+    // LN2 statistics of sample b (Chan merge of the tile partials; T2 <= 128 from the early loads)
+    float mean, rstd;
+    if (T2 <= 128) {
+      float n = 0.f, m = 0.f, M2 = 0.f;
+      if (lane < T2) chan_merge(n, m, M2, (float)(min(BML, L - lane * BML) * CH), pm0.x, pm0.y);
+      if (lane + 64 < T2) chan_merge(n, m, M2, (float)(min(BML, L - (lane + 64) * BML) * CH), pm1.x, pm1.y);
+      wave_chan(n, m, M2);
+      mean = m;
+      rstd = rsqrtf(M2 / n + eps);
+    } else {
+      wave_ln_stats(stb, T2, BML, L, CH, eps, mean, rstd);
+    }
+    float sa = 0.f, sc = 0.f;
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) {
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int ci0 = ct * 32 + 8 * g + 4 * h;
+        float din[4], sv[4], o[4];
+        unpack4(dq[ct][g], din);
+        unpack4(sq[ct][g], sv);
+        const float gg[4] = {gq4[ct][g].x, gq4[ct][g].y, gq4[ct][g].z, gq4[ct][g].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = bfround(fmaf(din[e], dmask, y[ct][4 * g + e]));
+          const float xh = (sv[e] - mean) * rstd;
+          const float dxh = o[e] * gg[e];
+          sa += okb ? dxh : 0.f;
+          sc += okb ? dxh * xh : 0.f;
+        }
+        if (okb) *reinterpret_cast<uint2*>(dh2 + roff + ci0) = packq4(o);
+      }
+    }
+    sa = wave_reduce_sum(sa);
+    sc = wave_reduce_sum(sc);
+    if (lane == 0) {
+      sums2[((size_t)b * TW + tw) * 2] = sa;
+      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
+    }
+    // the next item's dv row (DMA issued above) must be in LDS before its first read
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1139,6 +1345,11 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
@@ -1193,6 +1404,7 @@ PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g
   set_ln_attrs();
   constexpr int nw = 8;
   if (NJ % 64 != 0 || NJ * 256 + nw * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
+  if (!prenorm && gfrag == nullptr) return (int)hipErrorInvalidValue;   // the GELU-only form reads h2 rows
   const long items2 = (long)B * ((L + 63) / 64);
   long wg2 = (items2 + nw - 1) / nw;
   if (wg2 > num_cus()) wg2 = num_cus();
@@ -1204,9 +1416,14 @@ PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g
     nbg = min(nbg, B);
     hipLaunchKernelGGL(ln2_apply_kernel, dim3(tp, nbg), dim3(512), 0, st, (const bf16_t*)s2, st2, g2, be2,
                        (bf16_t*)h2, B, L, eps);
-    hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
-                       st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
-                       B, L, NJ, eps);
+    if (gfrag != nullptr)
+      hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
+                         st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
+                         B, L, NJ, eps);
+    else   // the backward recomputes GELU' (attn_bwd3): GELU column sums only
+      hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true, false>), dim3((int)wg2), dim3(64 * nw),
+                         NJ * 256 + nw * GT_BYTES, st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv,
+                         (bf16_t*)h2, vpart, (bf16x8*)nullptr, B, L, NJ, eps);
   } else {
     hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, false>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
                        st, (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
@@ -1232,6 +1449,25 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
   hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st,
                      (const bf16x8*)gfrag, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
                      (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
+  return pbx_launch_status();
+}
+
+// recomputing pool backward (NJ = 256 or 512): h2 = the block output rows the forward pool read
+PBX_EXPORT int pbx_attn_bwd3(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
+                             const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
+                             int NJ, float eps, hipStream_t st) {
+  set_ln_attrs();
+  const int nw = 4;
+  if ((NJ != 256 && NJ != 512) || bmv % 32 != 0) return (int)hipErrorInvalidValue;
+  const long items = (long)B * ((L + 31) / 32);
+  long wgl = (items + nw - 1) / nw;
+  if (wgl > num_cus()) wgl = num_cus();
+  const int lds = NJ * 256 + nw * 2 * NJ * 4;
+  const bool fix = ((wgl * nw) % ((L + 31) / 32)) == 0;
+  const auto kern = NJ == 512 ? (fix ? attn_bwd3_kernel<16, true> : attn_bwd3_kernel<16, false>)
+                              : (fix ? attn_bwd3_kernel<8, true> : attn_bwd3_kernel<8, false>);
+  hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st, (const bf16_t*)h2, (const bf16_t*)s2, st2, g2,
+                     (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
   return pbx_launch_status();
 }
 

@@ -38,6 +38,7 @@ _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, 
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
@@ -55,6 +56,12 @@ LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 BM1 = 128         # positions per conv-forward workgroup (= the tile of the LayerNorm-1 partials)
 # pool forward: 1 = LayerNorm-2 as its own streaming pass, the pool reads normalised rows (A/B knob)
 POOL_PRENORM = int(os.environ.get("PBX_POOL_PRENORM", "1"))
+# pool backward: 0 (default) = the forward stores GELU' as bf16 backward-operand fragments (268 MB per block at
+# B = L = 512) and attn_bwd2 streams them; 1 = memory-lean: the forward keeps only the GELU column sums
+# (83 vs 112 us) and attn_bwd3 recomputes GELU'(h2 Wv) on MFMA + VALU from the h2 rows (263 vs 208 us beside the
+# weight gradient): ~1 % slower per step, 1.6 GB less activation memory per step
+# (profiles/r3x_pool_recompute_ab.txt)
+POOL_RECOMPUTE = int(os.environ.get("PBX_POOL_RECOMPUTE", "0"))
 
 
 def attn_pool_supported(NJ: int) -> bool:
@@ -197,18 +204,23 @@ class LocalBlockFn(torch.autograd.Function):
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
+        recompute = need_bwd and POOL_RECOMPUTE and POOL_PRENORM
         if need_bwd:
-            # GELU' of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
-            gfrag = torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
+            # recompute: GELU column sums only, the backward re-derives GELU' from h2 (attn_bwd3); else GELU'
+            # of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
+            gfrag = None if recompute else torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
             _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), gfrag.data_ptr(), B, L, NJ, LN_EPS,
+                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), _p(gfrag), B, L, NJ, LN_EPS,
                       POOL_PRENORM, stream)
         else:
             # forward-only pool (GELU only, 8 independent waves per workgroup)
             gfrag = None
             _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
-        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2)
+        # the pool backward's operand: the GELU' fragments, or the block output rows h2 it recomputes them from
+        ctx.recompute = recompute
+        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw, wl_b,
+                              wv_bf16, g1, be1, g2)
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
         ctx.tail = bool(tail) and WGRAD_TAIL_FULL
         ctx.set_materialize_grads(False)
@@ -239,9 +251,9 @@ class LocalBlockFn(torch.autograd.Function):
         TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                  dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                  stream)
+        _lib.call("pbx_attn_bwd3" if ctx.recompute else "pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(),
+                  st2.data_ptr(), g2.data_ptr(), _p(dh2), dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(),
+                  sums2.data_ptr(), B, L, NJ, LN_EPS, stream)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
         dh1 = torch.empty_like(x)
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)

@@ -156,7 +156,9 @@ def wait_ready(*tensors) -> None:
         if isinstance(t, torch.Tensor):
             key = _ready.pop(t.data_ptr(), None)
             if key is not None:
-                torch.cuda.current_stream(t.device).wait_stream(_streams[key])
+                cur = torch.cuda.current_stream(t.device)
+                if cur != _streams[key]:      # a stream waiting on itself is a no-op (and breaks graph capture)
+                    cur.wait_stream(_streams[key])
 
 
 def join() -> None:
