@@ -748,14 +748,17 @@ __global__ void __launch_bounds__(256) attn_bwd2_kernel(
 // which is exactly the order the transposed Wv reads of attn_bwd2 deliver: no data movement between
 // the two MFMAs.  The GELU' of chunk jt runs while the MFMAs of chunk jt + 1's zT are in flight.
 // Epilogue (dh2 = bf16(dh2_in + dh), LN2 partials) as attn_bwd2.  One wave per SIMD.
-template <int NJT, bool FIXTW>
-__global__ void __launch_bounds__(256) attn_bwd3_kernel(
+template <int NJT, bool FIXTW, int NW>
+__global__ void __launch_bounds__(64 * NW) attn_bwd3_kernel(
     const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
     const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, float eps) {
   constexpr int NJ = NJT * 32;
   constexpr int NDV = NJ / 256;                     // 1-KiB DMA instructions per dv row
-  constexpr int NW = 4;
+  // NW = 4: one wave per SIMD, every load of an item issued up front; NW = 8: two waves per SIMD sharing
+  // one Wv image (LDS 128 + 32 KB), the epilogue operands loaded after the MFMA / GELU' body (<= 256
+  // registers a wave) -- the other wave's VALU / MFMA work covers that latency
+  constexpr bool EARLY = NW == 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* ws = smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -815,22 +818,25 @@ __global__ void __launch_bounds__(256) attn_bwd3_kernel(
     const float* stb = st2 + (size_t)b * T2 * 2;
     uint2 dq[4][4], sq[4][4];
     float2 pm0, pm1;
-    // epilogue operands and the next item's dv row: in flight during the whole MFMA / GELU' body
-    if (has_next) {
+    // epilogue operands and the next item's dv row
+    auto epi_loads = [&]() {
+      if (has_next) {
 #pragma unroll
-      for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
-    }
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ci0 = ct * 32 + 8 * i + 4 * h;
-        dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
-        sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
-        if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+        for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
       }
-    pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
-    pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ci0 = ct * 32 + 8 * i + 4 * h;
+          dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
+          sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
+          if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
+        }
+      pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
+      pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
+    };
+    if constexpr (EARLY) epi_loads();   // in flight during the whole MFMA / GELU' body
     bf16x8 hf[8];
     const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -847,7 +853,7 @@ __global__ void __launch_bounds__(256) attn_bwd3_kernel(
       return z;
     };
     f32x16_t zc = zchunk(0);
-#pragma unroll 2
+#pragma unroll EARLY ? 2 : 1
     for (int jt = 0; jt < NJT; ++jt) {
       f32x16_t zn = zc;
       if (jt + 1 < NJT) zn = zchunk(jt + 1);          // in flight during this chunk's GELU'
@@ -877,6 +883,7 @@ __global__ void __launch_bounds__(256) attn_bwd3_kernel(
       }
       zc = zn;
     }
+    if constexpr (!EARLY) epi_loads();
     // LN2 statistics of sample b (Chan merge of the tile partials; T2 <= 128 from the early loads)
     float mean, rstd;
     if (T2 <= 128) {
@@ -1345,10 +1352,12 @@ static void set_ln_attrs() {
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -1455,17 +1464,21 @@ PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2
 // recomputing pool backward (NJ = 256 or 512): h2 = the block output rows the forward pool read
 PBX_EXPORT int pbx_attn_bwd3(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
                              const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
-                             int NJ, float eps, hipStream_t st) {
+                             int NJ, float eps, int wide, hipStream_t st) {
   set_ln_attrs();
-  const int nw = 4;
+  const int nw = wide ? 8 : 4;
   if ((NJ != 256 && NJ != 512) || bmv % 32 != 0) return (int)hipErrorInvalidValue;
   const long items = (long)B * ((L + 31) / 32);
   long wgl = (items + nw - 1) / nw;
   if (wgl > num_cus()) wgl = num_cus();
   const int lds = NJ * 256 + nw * 2 * NJ * 4;
   const bool fix = ((wgl * nw) % ((L + 31) / 32)) == 0;
-  const auto kern = NJ == 512 ? (fix ? attn_bwd3_kernel<16, true> : attn_bwd3_kernel<16, false>)
-                              : (fix ? attn_bwd3_kernel<8, true> : attn_bwd3_kernel<8, false>);
+  decltype(&attn_bwd3_kernel<16, true, 4>) kern;
+  if (wide)   // two waves per SIMD: the gamma rows are loaded per item (no FIXTW registers)
+    kern = NJ == 512 ? attn_bwd3_kernel<16, false, 8> : attn_bwd3_kernel<8, false, 8>;
+  else
+    kern = NJ == 512 ? (fix ? attn_bwd3_kernel<16, true, 4> : attn_bwd3_kernel<16, false, 4>)
+                     : (fix ? attn_bwd3_kernel<8, true, 4> : attn_bwd3_kernel<8, false, 4>);
   hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st, (const bf16_t*)h2, (const bf16_t*)s2, st2, g2,
                      (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
   return pbx_launch_status();

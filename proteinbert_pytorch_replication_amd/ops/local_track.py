@@ -38,7 +38,7 @@ _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, 
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
-_lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
@@ -62,6 +62,8 @@ POOL_PRENORM = int(os.environ.get("PBX_POOL_PRENORM", "1"))
 # weight gradient): ~1 % slower per step, 1.6 GB less activation memory per step
 # (profiles/r3x_pool_recompute_ab.txt)
 POOL_RECOMPUTE = int(os.environ.get("PBX_POOL_RECOMPUTE", "0"))
+# attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
+POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
 
 
 def attn_pool_supported(NJ: int) -> bool:
@@ -251,9 +253,14 @@ class LocalBlockFn(torch.autograd.Function):
         TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        _lib.call("pbx_attn_bwd3" if ctx.recompute else "pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(),
-                  st2.data_ptr(), g2.data_ptr(), _p(dh2), dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(),
-                  sums2.data_ptr(), B, L, NJ, LN_EPS, stream)
+        if ctx.recompute:
+            _lib.call("pbx_attn_bwd3", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
+                      POOL_BWD3_WIDE, stream)
+        else:
+            _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
+                      stream)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
         dh1 = torch.empty_like(x)
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)

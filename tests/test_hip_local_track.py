@@ -68,12 +68,14 @@ def test_local_block_forward(L, B, frozen):
     assert e_v < 1.5e-2
 
 
-@pytest.mark.parametrize("recompute", [1, 0])      # pool backward: attn_bwd3 (GELU' recomputed) / attn_bwd2
+# pool backward: attn_bwd2 (stored GELU' fragments) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD
+@pytest.mark.parametrize("recompute,wide", [(0, 1), (1, 1), (1, 0)])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
-def test_local_block_backward(L, B, recompute, monkeypatch):
+def test_local_block_backward(L, B, recompute, wide, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     monkeypatch.setattr(local_track, "POOL_RECOMPUTE", recompute)
+    monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
