@@ -57,9 +57,10 @@ class FlatArena:
             p.grad = self.grad[o:o + n].view(p.shape)
 
     def grads_attached(self) -> bool:
+        base, es = self.grad.data_ptr(), self.grad.element_size()
         for p, (o, _) in zip(self.params, self.offsets):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad[o:].data_ptr():
+            if g is None or g.data_ptr() != base + o * es:
                 return False
         return True
 
