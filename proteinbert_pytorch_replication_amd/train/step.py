@@ -9,7 +9,6 @@ a GPU the forward/backward run through the fused HIP kernels
 """
 from __future__ import annotations
 
-import os
 from typing import Dict, Optional
 
 import torch
@@ -41,9 +40,6 @@ class PretrainStep:
         self.grad_clip = grad_clip
         self.skip_nonfinite = skip_nonfinite
         self.fused = isinstance(optimizer, FusedAdam)
-        self._hp = None
-        if self.device.type == "cuda" and os.environ.get("PBX_MAIN_PRIO", "0") == "1":
-            self._hp = torch.cuda.Stream(device=self.device, priority=-1)
         if self.fused and ddp is not None and ddp.enabled:
             optimizer.grad_scale = 1.0 / ddp.world
 
@@ -60,18 +56,6 @@ class PretrainStep:
                                    None if self.standard_loss else self.global_loss_fn, return_parts)
 
     def __call__(self, X, Y, W) -> torch.Tensor:
-        if self._hp is not None:
-            # the critical path on a high-priority stream: its workgroups are dispatched ahead of the
-            # aux-stream weight-gradient kernels (PBX_MAIN_PRIO=1, A/B knob)
-            cur = torch.cuda.current_stream(self.device)
-            self._hp.wait_stream(cur)
-            with torch.cuda.stream(self._hp):
-                loss = self._step(X, Y, W)
-            cur.wait_stream(self._hp)
-            return loss
-        return self._step(X, Y, W)
-
-    def _step(self, X, Y, W) -> torch.Tensor:
         opt = self.optimizer
         opt.zero_grad()
         loss = self.loss(X, Y, W)
