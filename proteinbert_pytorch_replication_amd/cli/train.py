@@ -62,6 +62,7 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     _common(ap)
     ap.add_argument("--resume", choices=["none", "latest"], default="latest")
     ap.add_argument("--metrics", default=None, help="JSONL metrics file (rank 0)")
+    ap.add_argument("--tensorboard", default=None, help="TensorBoard event-file directory (rank 0)")
     ap.add_argument("--log-every", type=int, default=10)
     ap.add_argument("--async-checkpoint", action="store_true")
     ap.add_argument("--profile-steps", default=None, help="START[:COUNT] steps traced with torch.profiler")
@@ -115,6 +116,7 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
                    optim_scheduler_patience=cfg.optim.plateau_patience, warmup_duration=cfg.optim.warmup_duration,
                    device=dev, log_every=a.log_every, bucket_mb=cfg.dist.bucket_mb, compute_dtype=cfg.kernel.dtype,
                    grad_clip=cfg.optim.grad_clip, async_checkpoint=a.async_checkpoint, metrics_path=a.metrics,
+                   tensorboard_dir=a.tensorboard,
                    resume=a.resume, profile_steps=a.profile_steps, profile_dir=a.profile_dir,
                    zero_optimizer=a.zero, comm_dtype=cfg.dist.comm_dtype)
     if info.is_main:

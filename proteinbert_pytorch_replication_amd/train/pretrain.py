@@ -71,7 +71,7 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
              async_checkpoint: bool = False, metrics_path: Optional[str] = None, resume: str = "none",
              fuse_optimizer: bool = True, final_save: bool = True, profile_steps: Optional[str] = None,
              profile_dir: Optional[str] = None, zero_optimizer: bool = False,
-             comm_dtype="fp32") -> Dict[str, Any]:
+             comm_dtype="fp32", tensorboard_dir: Optional[str] = None) -> Dict[str, Any]:
     info = pdist.init_distributed()
     if device is None:
         device = info.device
@@ -107,6 +107,10 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
     step_fn = PretrainStep(model, optimizer, ddp, local_loss_fn, global_loss_fn, compute_dtype, grad_clip)
     writer = CheckpointWriter(save_path, async_checkpoint, is_main=info.is_main)
     metrics = MetricsWriter(metrics_path if info.is_main else None)
+    tb = None
+    if tensorboard_dir and info.is_main:
+        from ..utils.tensorboard import SummaryWriter
+        tb = SummaryWriter(tensorboard_dir)
 
     if loaded_checkpoint is None and resume == "latest":
         path = latest_checkpoint(save_path)
@@ -173,8 +177,12 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
                     logging.info(f"Current batch iteration: {current} | Train loss: {last_loss:.4f} | "
                                  f"Learning rate: {scheduler.get_last_lr()[0]} | "
                                  f"Batch Iteration time: {dt:.4f} seconds")
+                    seq_s = X["local"].shape[0] * info.world_size / max(dt, 1e-9)
                     metrics.write(step=current, loss=last_loss, lr=scheduler.get_last_lr()[0], step_time_s=dt,
-                                  seq_per_s=X["local"].shape[0] * info.world_size / max(dt, 1e-9))
+                                  seq_per_s=seq_s)
+                    if tb is not None:
+                        tb.add_scalars({"train/loss": last_loss, "train/lr": scheduler.get_last_lr()[0],
+                                        "perf/step_time_s": dt, "perf/seq_per_s": seq_s}, current)
                 if not scheduler.in_warmup:
                     # plateau patience counts log intervals (== steps at log_every=1, the reference)
                     scheduler.step(last_loss)
@@ -192,6 +200,8 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             raise RuntimeError("train_dataloader yielded no batches")
     writer.wait()
     metrics.close()
+    if tb is not None:
+        tb.close()
     if final_save:
         results["final_model_path"] = save_final_model(model, save_path, info.is_main)
     return results
