@@ -128,7 +128,7 @@ def main():
             from proteinbert_pytorch_replication_amd.train.losses import pretrain_loss_torch
             h, g = model.encode_torch(X["local"], X["global"], torch.float32, faithful_attention=True)
             pl, pg = model.heads_torch(h, g)
-            return pretrain_loss_torch(pl, pg, Y, W)
+            return pretrain_loss_torch(pl, pg, Y, W, return_parts=return_parts)
         step.loss = faithful_loss
     gen = SyntheticUniRefGO(L, mcfg.num_annotations, B, dev, seed=a.seed + 1000 * info.rank)
 

@@ -139,6 +139,9 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
     fault_rank = int(os.environ.get("PBX_FAULT_RANK", "0") or 0)
     model.train()
     loss_acc = torch.zeros((), dtype=torch.float32, device=device)
+    parts_acc = torch.zeros(2, dtype=torch.float32, device=device)      # local (CE), global (BCE)
+    from ..utils.flops import mfu, train_flops_per_sequence
+    cfg = getattr(model, "config", None)
     n_acc = 0
     t_last = time.time()
     last_loss = float("nan")
@@ -153,6 +156,9 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             with marker("pbx/step"):
                 loss = step_fn(X, Y, W)
             loss_acc += loss.float()
+            if step_fn.last_parts is not None:
+                parts_acc[0] += step_fn.last_parts[0].float()
+                parts_acc[1] += step_fn.last_parts[1].float()
             n_acc += 1
             current += 1
             if profiler is not None:
@@ -167,7 +173,9 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
             if current % log_every == 0 or current >= max_batch_iterations:
                 if info.distributed:
                     pdist.all_reduce_mean_(loss_acc)
+                    pdist.all_reduce_mean_(parts_acc)
                 last_loss = float(loss_acc.item()) / max(1, n_acc)
+                part_l, part_g = (float(v) / max(1, n_acc) for v in parts_acc.tolist())
                 now = time.time()
                 dt = (now - t_last) / max(1, n_acc)
                 t_last = now
@@ -178,8 +186,15 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
                                  f"Learning rate: {scheduler.get_last_lr()[0]} | "
                                  f"Batch Iteration time: {dt:.4f} seconds")
                     seq_s = X["local"].shape[0] * info.world_size / max(dt, 1e-9)
-                    metrics.write(step=current, loss=last_loss, lr=scheduler.get_last_lr()[0], step_time_s=dt,
-                                  seq_per_s=seq_s)
+                    Ls = X["local"].shape[1]
+                    rec = dict(step=current, loss=last_loss, loss_local=part_l, loss_global=part_g,
+                               lr=scheduler.get_last_lr()[0], step_time_s=dt, seq_per_s=seq_s,
+                               tokens_per_s=seq_s * Ls)
+                    if cfg is not None:
+                        rec["mfu"] = mfu(train_flops_per_sequence(cfg, Ls), seq_s, n_devices=info.world_size)
+                    if device.type == "cuda":
+                        rec["max_mem_gb"] = torch.cuda.max_memory_allocated(device) / 2 ** 30
+                    metrics.write(**rec)
                     if tb is not None:
                         tb.add_scalars({"train/loss": last_loss, "train/lr": scheduler.get_last_lr()[0],
                                         "perf/step_time_s": dt, "perf/seq_per_s": seq_s}, current)
@@ -187,6 +202,7 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
                     # plateau patience counts log intervals (== steps at log_every=1, the reference)
                     scheduler.step(last_loss)
                 loss_acc.zero_()
+                parts_acc.zero_()
                 n_acc = 0
             if current >= max_batch_iterations:
                 break

@@ -40,6 +40,7 @@ class PretrainStep:
         self.grad_clip = grad_clip
         self.skip_nonfinite = skip_nonfinite
         self.fused = isinstance(optimizer, FusedAdam)
+        self.last_parts = None
         if self.fused and ddp is not None and ddp.enabled:
             optimizer.grad_scale = 1.0 / ddp.world
 
@@ -58,7 +59,9 @@ class PretrainStep:
     def __call__(self, X, Y, W) -> torch.Tensor:
         opt = self.optimizer
         opt.zero_grad()
-        loss = self.loss(X, Y, W)
+        loss, l_local, l_global = self.loss(X, Y, W, return_parts=True)
+        # device scalars (no host sync): the per-head losses of the last step, for the metrics
+        self.last_parts = (l_local.detach(), l_global.detach())
         if self.model.resolved_backend(self.device) == "hip":
             from ..ops.global_track import unit_loss_grad
             from ..ops import streams

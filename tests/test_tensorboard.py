@@ -45,8 +45,9 @@ def test_pretrain_writes_tensorboard(tmp_path):
     loader = [gen.next_batch() for _ in range(3)]
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     tb = str(tmp_path / "tb")
+    mpath = str(tmp_path / "m.jsonl")
     res = pretrain(m, loader, opt, max_batch_iterations=3, save_path=str(tmp_path), tensorboard_dir=tb,
-                   final_save=False, device="cpu")
+                   final_save=False, device="cpu", metrics_path=mpath)
     files = glob.glob(os.path.join(tb, "events.out.tfevents.*"))
     assert len(files) == 1
     got = read_scalars(files[0])
@@ -54,3 +55,10 @@ def test_pretrain_writes_tensorboard(tmp_path):
     assert [s for s, t, _ in got if t == "train/loss"] == [1, 2, 3]
     assert all(abs(a - b) < 1e-5 * abs(b) for a, b in zip(losses, res["train_loss"]))
     assert {t for _, t, _ in got} == {"train/loss", "train/lr", "perf/step_time_s", "perf/seq_per_s"}
+    # the JSONL record of each log interval: per-head losses summing to the total, tokens/s and MFU
+    import json
+    recs = [json.loads(x) for x in open(mpath)]
+    assert len(recs) == 3
+    for r in recs:
+        assert abs(r["loss_local"] + r["loss_global"] - r["loss"]) < 1e-5 * max(1.0, abs(r["loss"]))
+        assert r["tokens_per_s"] == r["seq_per_s"] * L and 0 < r["mfu"] < 1
