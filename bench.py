@@ -47,8 +47,8 @@ REFERENCE_CFG1_CPU_SEQ_PER_S = 179.5  # reference cfg 1 step, 8-cor
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)   # 20-step runs spread up to 4 % on one box (r3_final2)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: preset)")
     ap.add_argument("--seq-len", type=int, default=None)
     ap.add_argument("--preset", default=None, help="config preset (default: cfg2_paper_l512, or "

@@ -152,6 +152,8 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     # (R = 56 on 256 CUs): the aux-stream weight gradient runs beside the main-stream backward, and
     # leaving it a few CUs measured +2.4 % on the step over R = 64 (R = 48: +1.3 %, 32: -0.4 %)
     R = max(8, (7 * _num_cus(dev) // (16 * nconv)) // 8 * 8)
+    if os.environ.get("PBX_WGRAD_R"):       # sweep knob (tools/gpu_r3_rs.sh)
+        R = int(os.environ["PBX_WGRAD_R"])
     if full_chip:
         R = max(8, (_num_cus(dev) // (2 * nconv)) // 8 * 8)
     R = min(R, ntiles)

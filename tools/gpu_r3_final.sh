@@ -1,14 +1,14 @@
 # Round 3 final tree: full GPU suite, smoke, headline bench (x2) and the other BASELINE configurations
 R=$GRAFT_REPO_ROOT
 cd $R
-mkdir -p gpurun_out/r3_final
-O=gpurun_out/r3_final
+mkdir -p gpurun_out/r3_final2
+O=gpurun_out/r3_final2
 T="timeout -k 10"
 $T 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 $T 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 tail -1 $O/smoke.log
-for i in 1 2; do $T 300 python -u bench.py > $O/bench_l512_run$i.json 2> $O/bench_l512_run$i.err || exit 1; done
+for i in 1 2 3; do $T 300 python -u bench.py > $O/bench_l512_run$i.json 2> $O/bench_l512_run$i.err || exit 1; done
 cat $O/bench_l512_run*.json
 $T 300 python -u bench.py --semantics paper > $O/bench_paper.json 2> $O/bench_paper.err || exit 1
 $T 300 python -u bench.py --preset cfg3_paper_l1024_dp8 > $O/bench_l1024.json 2> $O/bench_l1024.err || exit 1
