@@ -92,11 +92,31 @@ class _AuxScope:
 _forked: Dict[Tuple[int, str], bool] = {}
 
 
+_events: Dict[Tuple[int, int], torch.cuda.Event] = {}
+# PBX_STREAM_FAST=0: per-call wait_stream events and the torch.cuda.stream context (A/B of the host cost)
+_FAST = os.environ.get("PBX_STREAM_FAST", "1") != "0"
+
+
+def _wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
+    """``dst`` waits for the work enqueued on ``src`` so far.  ``Stream.wait_stream`` creates a new
+    event per call (~20 such hand-offs per step); a wait binds to the event's latest record at the
+    time it is enqueued, so one cached event per (dst, src) pair is reused."""
+    if not _FAST:
+        dst.wait_stream(src)
+        return
+    key = (dst.cuda_stream, src.cuda_stream)
+    ev = _events.get(key)
+    if ev is None:
+        ev = _events[key] = torch.cuda.Event()
+    ev.record(src)
+    dst.wait_event(ev)
+
+
 def fork(device: torch.device, name: str) -> None:
     """Make aux stream ``name`` wait for the current stream's work enqueued SO FAR; the next
     :func:`on_aux` on it starts from this point instead of the current stream's later tail (the
     main stream can enqueue more work that the aux body does not need)."""
-    _aux(device, name).wait_stream(torch.cuda.current_stream(_idx(device)))
+    _wait(_aux(device, name), torch.cuda.current_stream(_idx(device)))
     _forked[(_idx(device), name)] = True
 
 
@@ -117,13 +137,23 @@ def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
     main = torch.cuda.current_stream(idx)
     aux = _aux(device, name)
     if not _forked.pop((idx, name), False):
-        aux.wait_stream(main)
+        _wait(aux, main)
     scope = _AuxScope(idx)
     scope.keep(*keep)
     _used.setdefault(idx, set()).add(name)
     _main[idx] = main
-    with torch.cuda.stream(aux):
+    # set_stream in place of the torch.cuda.stream context (the step enters ~20 of these scopes;
+    # the context manager's device bookkeeping cost ~20 us of host time each)
+    if not _FAST:
+        with torch.cuda.stream(aux):
+            yield scope
+        _queue_join()
+        return
+    torch.cuda.set_stream(aux)
+    try:
         yield scope
+    finally:
+        torch.cuda.set_stream(main)
     _queue_join()
 
 
@@ -144,7 +174,7 @@ def mark_ready(device: torch.device, name: str, tensors: Iterable[torch.Tensor])
 
 def wait_for(device: torch.device, name: str) -> None:
     """Current stream waits for the work enqueued on aux stream ``name`` so far."""
-    torch.cuda.current_stream(_idx(device)).wait_stream(_aux(device, name))
+    _wait(torch.cuda.current_stream(_idx(device)), _aux(device, name))
 
 
 def wait_ready(*tensors) -> None:
@@ -158,7 +188,7 @@ def wait_ready(*tensors) -> None:
             if key is not None:
                 cur = torch.cuda.current_stream(t.device)
                 if cur != _streams[key]:      # a stream waiting on itself is a no-op (and breaks graph capture)
-                    cur.wait_stream(_streams[key])
+                    _wait(cur, _streams[key])
 
 
 def join() -> None:
@@ -169,7 +199,7 @@ def join() -> None:
             continue
         main = _main.get(idx) or torch.cuda.current_stream(idx)
         for name in _used.get(idx, ()):
-            main.wait_stream(_streams[(idx, name)])
+            _wait(main, _streams[(idx, name)])
         keep.clear()
         _used[idx] = set()
     _ready.clear()
