@@ -1,8 +1,8 @@
 # Round 3 final tree: full GPU suite, smoke, headline bench (x2) and the other BASELINE configurations
 R=$GRAFT_REPO_ROOT
 cd $R
-mkdir -p gpurun_out/r3_final3
-O=gpurun_out/r3_final3
+mkdir -p gpurun_out/r3_final4
+O=gpurun_out/r3_final4
 T="timeout -k 10"
 $T 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
