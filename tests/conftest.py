@@ -36,3 +36,34 @@ def reference_modules():
     finally:
         sys.path.remove(REFERENCE_DIR)
     return modules
+
+
+def _exported_launchers():
+    """Every ``PBX_EXPORT int pbx_*`` entry point of libpbx_hip.so (read from the HIP sources)."""
+    import glob
+    import re
+    names = set()
+    for f in glob.glob(os.path.join(ROOT, "proteinbert_pytorch_replication_amd", "ops", "csrc", "*.hip")):
+        with open(f) as fh:
+            names.update(re.findall(r"PBX_EXPORT\s+int\s+(pbx_\w+)\s*\(", fh.read()))
+    return names
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """GPU runs: report which kernel launchers the session reached through ``_lib.call``.
+
+    ``_lib.call`` caches a ctypes function object on first use, so the cache keys are exactly the
+    launchers that ran.  Written to ``$PBX_LAUNCHER_REPORT`` when set (evidence under profiles/)."""
+    mod = sys.modules.get("proteinbert_pytorch_replication_amd.ops._lib")
+    if mod is None or not getattr(mod, "_FN", None):
+        return
+    exported = _exported_launchers()
+    called = set(mod._FN)
+    lines = [f"kernel launchers reached: {len(called & exported)} of {len(exported)} exported"]
+    lines += [f"  not reached via _lib.call: {n}" for n in sorted(exported - called)]
+    for ln in lines:
+        terminalreporter.write_line(ln)
+    out = os.environ.get("PBX_LAUNCHER_REPORT")
+    if out:
+        with open(out, "w") as fh:
+            fh.write("\n".join(lines) + "\n")
