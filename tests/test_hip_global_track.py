@@ -111,3 +111,37 @@ def test_glob3_deterministic(monkeypatch):
     for x, y in zip(a, b):
         if x is not None:
             assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("B,G,NGL,TV", [(37, 512, 128, 4), (24, 384, 128, 2), (16, 256, 0, 1)])
+def test_general_global_block_vs_fp32(B, G, NGL, TV):
+    """The general-shape global track (GlobalBlockFn: in-tree GEMMs + the row LayerNorm kernels of
+    csrc/glob.hip), used when the fused kernels do not cover (G, NGL), e.g. G = 384."""
+    from proteinbert_pytorch_replication_amd.ops.global_track import GlobalBlockFn
+    dev = torch.device("cuda")
+    params = _params(G, NGL, 64, dev)
+    torch.manual_seed(7)
+    g0 = torch.randn(B, G, device=dev)
+    vp0 = torch.randn(B, TV, G, device=dev) * 0.05
+    dg2 = torch.randn(B, G, device=dev)
+    dgb = torch.randn(B, NGL, device=dev) if NGL else None
+
+    def general(g, vp):
+        g2, _, gb = GlobalBlockFn.apply(g, g.detach().to(torch.bfloat16), vp, *params)
+        return g2, gb
+
+    out_f, grad_f = _run(general, params, g0, vp0, dg2, dgb, NGL)
+    out_r, grad_r = _run(lambda g, vp: _reference(g, vp, *params), params, g0, vp0, dg2, dgb, NGL)
+    for name, a, b in zip(["g2", "gb"], out_r, out_f):
+        if a.numel():
+            err = float((a - b).abs().max())
+            print(f"{name}: max |err| {err:.3e} (max |ref| {float(a.abs().max()):.3e})")
+            assert err <= 1.5e-2 * float(a.abs().max()) + 1e-4, (name, err)
+    names = ["g", "vpart", "w1", "b1", "n1w", "n1b", "w2", "b2", "n2w", "n2b", "wp", "wgl", "bgl"]
+    for n, a, b in zip(names, grad_r, grad_f):
+        if a is None:
+            assert b is None, n
+            continue
+        rel = float((a - b).norm() / (a.norm() + 1e-30))
+        print(f"d{n}: rel-l2 {rel:.2e}")
+        assert rel <= 1.2e-2, (n, rel)
