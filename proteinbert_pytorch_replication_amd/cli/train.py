@@ -81,7 +81,7 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
         import dataclasses
         cfg.model = dataclasses.replace(cfg.model, sequences_length=max(int(x) for x in cfg.data.lengths),
                                         variable_length=True)
-    model = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
+    model = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend, cfg.model))
     B, L = cfg.train.batch_size, cfg.model.sequences_length
     corr = CorruptionParams(cfg.data.token_corruption_p, cfg.data.annotation_positive_p,
                             cfg.data.annotation_negative_p, cfg.data.blank_annotation_p)
@@ -162,9 +162,9 @@ def finetune_main(argv: Optional[List[str]] = None) -> dict:
     torch.manual_seed(cfg.train.seed)
     if a.pretrained:
         from ..train.checkpoint import load_model
-        enc = load_model(a.pretrained, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
+        enc = load_model(a.pretrained, device=dev, backend=determinism.backend_for(cfg.kernel.backend, cfg.model))
     else:
-        enc = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend))
+        enc = build_model(cfg.model, device=dev, backend=determinism.backend_for(cfg.kernel.backend, cfg.model))
     L = enc.config["sequences_length"]
     model = ProteinBERTForTokenClassification(enc, n_classes=len(a.classes), freeze_encoder=not a.unfreeze)
     from torch.utils.data import DataLoader

@@ -83,7 +83,7 @@ class KernelConfig:
     backend: str = "auto"               # auto | hip | torch
     dtype: str = "bf16"                 # compute dtype on GPU
     hip_graph: bool = False             # capture the whole train step
-    deterministic: bool = False         # bitwise-reproducible run (PyTorch path, utils/determinism.py)
+    deterministic: bool = False         # bitwise-reproducible run (fixed-order HIP forms; paper semantics -> PyTorch path)
 
 
 @dataclass

@@ -306,7 +306,8 @@ class ProteinBERT(nn.Module):
         self.config = dict(sequences_length=sequences_length, num_annotations=num_annotations,
                            local_dim=local_dim, global_dim=global_dim, key_dim=key_dim, num_heads=num_heads,
                            num_blocks=num_blocks, conv_kernel_size=conv_kernel_size,
-                           wide_conv_dilation=wide_conv_dilation, vocab_size=vocab_size, semantics=semantics)
+                           wide_conv_dilation=wide_conv_dilation, vocab_size=vocab_size, semantics=semantics,
+                           variable_length=variable_length)
         self.semantics = semantics
         self.variable_length = variable_length
         self.sequences_length = sequences_length

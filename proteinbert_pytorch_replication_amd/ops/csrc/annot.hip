@@ -320,7 +320,8 @@ __global__ void __launch_bounds__(256) ann_wgrad_kernel(const float* __restrict_
 }  // namespace
 
 PBX_EXPORT int pbx_ann_supported(int B, int A, int G) {
-  return B >= 1 && B <= 8192 && A >= 1 && A <= 256 * CSR_NCH && G >= 64 && G % 64 == 0 && G <= 4096;
+  // B <= 8180: ann_wgrad_kernel holds 2 x B floats of dynamic LDS + red[2][4] within the 64 KB default
+  return B >= 1 && B <= 8180 && A >= 1 && A <= 256 * CSR_NCH && G >= 64 && G % 64 == 0 && G <= 4096;
 }
 
 // ann fp32 [B, A]; cnt int [B]; ent int2 [B * A]

@@ -55,6 +55,9 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, ta: bool = False, 
     N = b.shape[0] if tb else b.shape[1]
     Kb = b.shape[1] if tb else b.shape[0]
     if k is not None:
+        if k < K and k % 8:
+            # the padded path loads whole 8-element chunks: past a ragged k they hold real data
+            pad_a = pad_b = False
         K = k
     assert K <= Kb and out.shape[0] >= M and out.shape[1] >= N, (a.shape, b.shape, out.shape, ta, tb)
     dev = a.device

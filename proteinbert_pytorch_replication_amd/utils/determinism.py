@@ -17,8 +17,14 @@ heads and their loss partials, the fused Adam and the gradient clipping.
 fixed-order forms on the same kernels: per-workgroup partial slabs folded by a column-sum launch, and
 a single writer per destination for the LayerNorm-affine / ``dgb`` gradients.  The cost is a few
 extra small launches per block (``profiles/`` records it).  It also sets
-``torch.use_deterministic_algorithms`` for the PyTorch ops around the kernels.  The paper-semantics
-kernels and the PyTorch-op fallback for unsupported shapes are not covered by the fixed-order forms.
+``torch.use_deterministic_algorithms`` for the PyTorch ops around the kernels.
+
+The fixed-order forms exist for the reference-semantics kernels with the fused global track
+(``glob_fused_ok`` shapes).  The paper-semantics kernels (``csrc/paper_local.hip``) and the general-shape
+global track (``csrc/glob.hip``) still reduce with float atomics, so :func:`backend_for` routes those
+configurations to the PyTorch path while the mode is on: the bitwise guarantee holds for every config.
+
+``PBX_DETERMINISTIC=1`` in the environment is equivalent to calling :func:`enable` at import.
 """
 from __future__ import annotations
 
@@ -26,7 +32,7 @@ import os
 
 import torch
 
-_STATE = {"on": os.environ.get("PBX_DETERMINISTIC", "0") == "1"}
+_STATE = {"on": False}
 
 
 def enable(seed: int = None) -> None:
@@ -53,6 +59,29 @@ def fused_deterministic() -> bool:
     return _STATE["on"]
 
 
-def backend_for(requested: str) -> str:
-    """Kernel backend to use (the fused HIP path has a deterministic form: the request stands)."""
+def fixed_order_supported(model_cfg) -> bool:
+    """The fused HIP path has fixed-order forms for this model configuration."""
+    if model_cfg is None:
+        return True
+    get = (lambda k, d=None: model_cfg.get(k, d)) if isinstance(model_cfg, dict) else \
+        (lambda k, d=None: getattr(model_cfg, k, d))
+    if get("semantics", "reference") == "paper":
+        return False
+    from ..ops.global_track import glob_fused_ok
+    return glob_fused_ok(int(get("global_dim", 512)), int(get("local_dim", 128)))
+
+
+def backend_for(requested: str, model_cfg=None) -> str:
+    """Kernel backend to use.  In deterministic mode a HIP request for a configuration without
+    fixed-order kernel forms (paper semantics, unsupported global-track shapes) runs on the PyTorch
+    path instead, which ``torch.use_deterministic_algorithms`` makes reproducible."""
+    if _STATE["on"] and requested in ("hip", "auto") and not fixed_order_supported(model_cfg):
+        import logging
+        logging.getLogger(__name__).warning(
+            "deterministic mode: no fixed-order HIP kernels for this configuration; using the PyTorch backend")
+        return "torch"
     return requested
+
+
+if os.environ.get("PBX_DETERMINISTIC", "0") == "1":
+    enable()

@@ -95,3 +95,22 @@ def test_cli_deterministic_flag_reproduces_losses(tmp_path, capsys):
         torch.use_deterministic_algorithms(prev)
         determinism._STATE["on"] = False
     assert outs[0]["final_loss"] == outs[1]["final_loss"]
+
+
+def test_backend_routing_without_fixed_order_kernels():
+    """Deterministic mode keeps its bitwise guarantee for configurations whose HIP kernels only have
+    float-atomic reductions (paper semantics, non-fused global-track shapes): they run on the PyTorch
+    path; reference semantics at the fused shapes stay on HIP."""
+    from proteinbert_pytorch_replication_amd.config import get_preset
+    prev = torch.are_deterministic_algorithms_enabled()
+    try:
+        assert determinism.backend_for("hip", {"semantics": "paper"}) == "hip"      # mode off: request stands
+        determinism.enable()
+        cfg = get_preset("cfg2_paper_l512").model
+        assert determinism.backend_for("hip", cfg) == "hip"
+        assert determinism.backend_for("hip", dict(semantics="paper", global_dim=512, local_dim=128)) == "torch"
+        assert determinism.backend_for("auto", dict(semantics="reference", global_dim=384, local_dim=128)) == "torch"
+        assert determinism.backend_for("torch", dict(semantics="paper")) == "torch"
+    finally:
+        determinism.disable()
+        torch.use_deterministic_algorithms(prev)

@@ -92,3 +92,16 @@ def test_hip_variable_length_matches_torch():
             assert float(got[n][200:].abs().max()) == 0.0, n
             err = (got[n][:200] - p.grad[:200]).norm().item()
             assert err < 3e-2 * p.grad[:200].norm().item() + 1e-6, n
+
+
+def test_variable_length_model_roundtrips_through_checkpoint(tmp_path):
+    """variable_length is part of model.config: a multi-length model saved with save_final_model
+    reloads as a multi-length model that still accepts L < L_max."""
+    from proteinbert_pytorch_replication_amd.train.checkpoint import load_model, save_final_model
+    torch.manual_seed(0)
+    m = ProteinBERT(sequences_length=48, variable_length=True, backend="torch", **CFG)
+    path = save_final_model(m, str(tmp_path))
+    r = load_model(path, device="cpu", backend="torch")
+    assert r.variable_length and r.config["variable_length"]
+    batch = SyntheticUniRefGO(20, 40, 2, "cpu", seed=2, use_kernel=False).next_batch()
+    assert torch.allclose(_loss(m, batch), _loss(r, batch), rtol=1e-6, atol=1e-7)
