@@ -39,6 +39,8 @@ _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _I, _P])
+_lib.register("pbx_attn_bwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
+_lib.register("pbx_pack_wvt_frag", [_P, _P, _I, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
@@ -62,6 +64,11 @@ POOL_PRENORM = int(os.environ.get("PBX_POOL_PRENORM", "1"))
 # weight gradient): ~1 % slower per step, 1.6 GB less activation memory per step
 # (profiles/r3x_pool_recompute_ab.txt)
 POOL_RECOMPUTE = int(os.environ.get("PBX_POOL_RECOMPUTE", "0"))
+# pool backward: 1 (default) = weight-stationary attn_bwd4 (csrc/pool_bwd.hip: dv folded into the
+# register-resident Wv^T operand, GELU' tiles DMA'd into a 64 KB LDS double buffer, two workgroups per
+# CU); 0 = attn_bwd2 (whole Wv in 128 KB of LDS, dv applied per streamed fragment on the VALU)
+POOL_BWD4 = int(os.environ.get("PBX_POOL_BWD4", "1"))
+POOL_BWD4_TPW = int(os.environ.get("PBX_POOL_BWD4_TPW", "0"))   # tiles per workgroup (0: launcher's choice)
 # attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
 POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
 
@@ -254,8 +261,15 @@ class LocalBlockFn(torch.autograd.Function):
         # attention pool + LN2 partials
         TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
         dh2t = torch.empty_like(x)
+        bwd4 = POOL_BWD4 and not ctx.recompute and dvpart.dim() == 2
+        if bwd4:
+            TA *= 4                              # attn_bwd4: one partial per (tile, wave)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        if ctx.recompute:
+        if bwd4:
+            _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
+                      LN_EPS, POOL_BWD4_TPW, stream)
+        elif ctx.recompute:
             _lib.call("pbx_attn_bwd3", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
                       POOL_BWD3_WIDE, stream)
@@ -367,6 +381,20 @@ def _wv_bf16(att) -> torch.Tensor:
         cached = (key, att.value_weight_cat().t().to(torch.bfloat16).contiguous())
         att._pbx_wv_cache = cached
     return cached[1]
+
+
+def wvt_frag(wv_bf16: torch.Tensor) -> torch.Tensor:
+    """Wv^T MFMA A-operand fragment image of a bf16 ``[NJ, 128]`` value weight (attn_bwd4's stationary
+    operand), cached on the tensor: in reference semantics the value weights are untrained buffers and
+    their bf16 copy is itself cached across steps (:func:`_wv_bf16`), so the image is built once."""
+    key = (wv_bf16._version, wv_bf16.data_ptr())
+    cached = getattr(wv_bf16, "_pbx_wvt", None)
+    if cached is not None and cached[0] == key:
+        return cached[1]
+    out = torch.empty_like(wv_bf16)
+    _lib.call("pbx_pack_wvt_frag", wv_bf16.data_ptr(), out.data_ptr(), wv_bf16.shape[0], _lib.stream_ptr(wv_bf16.device))
+    wv_bf16._pbx_wvt = (key, out)
+    return out
 
 
 def conv_images(wn: torch.Tensor, ww: torch.Tensor):

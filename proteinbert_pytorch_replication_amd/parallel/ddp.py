@@ -18,6 +18,14 @@ collectives per step.
   backward on RCCL's own stream.
 * ``SUM`` reduction; the 1/world factor is folded into the fused Adam
   (``FusedAdam.grad_scale``) instead of an extra pass.
+* :meth:`finish_and_step` (the training step's default with the fused Adam) hides the optimizer
+  behind the exposed tail: the last bucket (global input layer + block 0, ~20 MB, ready only after
+  backward) is still on the wire when the Adam update of every other bucket runs on the compute
+  stream; only the last bucket's update trails its all-reduce.  The group-wide non-finite decision is
+  taken BEFORE any update: each bucket's local gradients are tested as it is launched, and one 4-byte
+  MAX all-reduce of the OR of those flags is queued ahead of the last bucket's all-reduce, so every rank
+  skips or commits every bucket together.  (The test is on local gradients: a sum of finite per-rank
+  gradients that overflows fp32 is not caught, where the previous post-reduction test caught it.)
 * ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
   bf16-rounded gradient sums); the default is fp32.  (A bf16 reduction of only the last, exposed
   bucket -- the 18 MB global input layer -- was an unmeasured option and has been removed: no
@@ -26,6 +34,7 @@ collectives per step.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import List, Optional
 
 import torch
@@ -70,6 +79,14 @@ class BucketedAllReduce:
         # both launched buckets before their last gradient was written
         self._ready = [False] * len(arena.params)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
+        # overlapped optimizer (finish_and_step): per-bucket local non-finite flags, group-wide OR.
+        # PBX_DP_OVERLAP_OPT=0: finish() + one whole-arena update after every all-reduce (A/B knob)
+        self.overlap_optimizer = os.environ.get("PBX_DP_OVERLAP_OPT", "1") != "0"
+        self.track_nonfinite = False
+        self._flags: Optional[torch.Tensor] = None
+        self._gflag: Optional[torch.Tensor] = None
+        self._flag_work = None
+        self._nf_ws: Optional[torch.Tensor] = None
         self._tmp: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
         self._next = 0
         self._hooks = []
@@ -101,6 +118,21 @@ class BucketedAllReduce:
                 self._mark(i)
         self._launch_ready()
 
+    def _local_flag(self, b: int, view: torch.Tensor) -> None:
+        """flags[b] = 1 when this rank's gradients of bucket b hold a NaN / Inf (before the in-place
+        all-reduce overwrites them), on the stream the collective is ordered on."""
+        if self._flags is None or self._flags.device != view.device:
+            self._flags = torch.zeros(len(self.buckets), dtype=torch.int32, device=view.device)
+        if view.is_cuda:
+            from ..ops import _lib
+            if self._nf_ws is None:
+                self._nf_ws = torch.empty(1024, dtype=torch.int32, device=view.device)
+            _lib.call("pbx_nonfinite_flag", view.data_ptr(), view.numel(), self._nf_ws.data_ptr(),
+                      self._flags[b:].data_ptr(), _lib.stream_ptr(view.device))
+        else:
+            bad = not bool(torch.isfinite(torch.dot(view, torch.zeros_like(view))))
+            self._flags[b] = 1 if bad else 0
+
     def _launch(self, b: int) -> None:
         s, e = self.buckets[b]
         view = self.arena.grad[s:e]
@@ -109,12 +141,30 @@ class BucketedAllReduce:
         # (ops/streams.py): enqueue the collective behind both streams without stalling this one
         ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()
         with ctx:
+            if self.track_nonfinite:
+                self._local_flag(b, view)
+                if b == len(self.buckets) - 1:
+                    # every bucket's local flag is in: the group-wide decision travels ahead of the last
+                    # (largest, exposed) bucket, so the other buckets' updates need not wait for it
+                    self._gflag = self._flags.amax().reshape(1)
+                    self._flag_work = dist.all_reduce(self._gflag, op=dist.ReduceOp.MAX, group=self.pg,
+                                                      async_op=True)
             if dt != torch.float32:
                 tmp = view.to(dt)
                 self._tmp[b] = tmp
                 self._works[b] = dist.all_reduce(tmp, group=self.pg, async_op=True)
             else:
                 self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
+
+    def _land(self, b: int) -> None:
+        """Current stream waits for bucket b's all-reduce (and copies a reduced bf16 bucket back)."""
+        w = self._works[b]
+        if w is not None:
+            w.wait()
+        if self._tmp[b] is not None:
+            s, e = self.buckets[b]
+            self.arena.grad[s:e].copy_(self._tmp[b])
+            self._tmp[b] = None
 
     def _launch_ready(self) -> None:
         while self._next < len(self.buckets) and self._pending[self._next] <= 0:
@@ -136,16 +186,46 @@ class BucketedAllReduce:
         for b in range(self._next, len(self.buckets)):
             self._launch(b)
         self._next = len(self.buckets)
-        for b, w in enumerate(self._works):
-            if w is not None:
-                w.wait()
-            if self._tmp[b] is not None:
-                s, e = self.buckets[b]
-                self.arena.grad[s:e].copy_(self._tmp[b])
-                self._tmp[b] = None
+        for b in range(len(self.buckets)):
+            self._land(b)
         if average:
             self.arena.grad.div_(self.world)
         self.start_step()
+
+    def finish_and_step(self, opt, skip_nonfinite: bool = True) -> None:
+        """End of backward for the fused Adam: buckets 0..n-2 are updated as soon as the group-wide
+        non-finite flag (queued ahead of the last bucket) has landed, beside the last bucket's
+        all-reduce; the last bucket's update follows its all-reduce.  Bitwise the same parameters as
+        :meth:`finish` + a whole-arena ``opt.step()`` (Adam is element-wise).  Call
+        :meth:`begin_overlapped_step` before backward."""
+        if not self.enabled:
+            if skip_nonfinite:
+                opt.set_nonfinite_skip()
+            opt.step()
+            return
+        if self.arena.grad.is_cuda:
+            streams.join()
+        for b in range(self._next, len(self.buckets)):
+            self._launch(b)
+        self._next = len(self.buckets)
+        last = len(self.buckets) - 1
+        for b in range(last):
+            self._land(b)
+        if self._flag_work is not None:
+            self._flag_work.wait()
+        opt.skip_flag = self._gflag if skip_nonfinite else None
+        opt.begin_step()
+        split = self.buckets[last][0]
+        opt.step_range(0, split)
+        self._land(last)
+        opt.step_range(split, self.arena.numel)
+        self.track_nonfinite = False
+        self._flag_work = None
+        self.start_step()
+
+    def begin_overlapped_step(self) -> None:
+        """The coming backward's buckets carry local non-finite flags (for :meth:`finish_and_step`)."""
+        self.track_nonfinite = self.enabled
 
     def broadcast_parameters(self, module: Optional[torch.nn.Module] = None, src: int = 0) -> None:
         if not self.enabled:

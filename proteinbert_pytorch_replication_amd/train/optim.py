@@ -84,31 +84,44 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
+        self.begin_step()
+        self.step_range(0, self.arena.numel)
+        return loss
+
+    @torch.no_grad()
+    def begin_step(self) -> None:
+        """Advance the step counters once per optimizer step; the update itself is one or more
+        :meth:`step_range` launches (the DP path updates gradient buckets as their all-reduce lands)."""
         self.step_count += 1
         a = self.arena
         if not a.grads_attached():
             a.attach_grads()
         if _hip_ok(a.data):
-            from ..ops import _lib
             if not torch.cuda.is_current_stream_capturing():
                 self.prepare()
             self._step_dev.add_(1.0)
-            _lib.call("pbx_adam_flat", a.data.data_ptr(), a.grad.data_ptr(), self.exp_avg.data_ptr(),
-                      self.exp_avg_sq.data_ptr(), _lib.ptr(self.shadow), a.numel, self._hp_dev.data_ptr(),
-                      _lib.ptr(self.skip_flag), self._step_dev.data_ptr(), _lib.stream_ptr(a.data.device))
-        else:
-            self._step_host(a)
-        return loss
 
-    def _step_host(self, a: FlatArena) -> None:
-        """CPU update: one in-place pass of PyTorch's fused CPU Adam kernel over the flat arena (same
-        update as the HIP kernel: L2 weight decay, bias corrections at ``step_count``).  The skip
-        decision is a host bool here (a CPU tensor read, no device sync)."""
-        if skip_requested(self.skip_flag):
+    @torch.no_grad()
+    def step_range(self, start: int, end: int) -> None:
+        """Adam on arena elements ``[start, end)`` (element-wise, so any split of the arena gives the
+        bitwise result of one whole-arena launch); ``start`` is a segment boundary (16-B aligned)."""
+        a = self.arena
+        if end <= start:
             return
-        adam_update_host(self, a.data, a.grad, self.exp_avg, self.exp_avg_sq)
-        if self.shadow is not None:
-            self.shadow.copy_(a.data)
+        if _hip_ok(a.data):
+            from ..ops import _lib
+            f4, b2 = 4 * start, 2 * start
+            _lib.call("pbx_adam_flat", a.data.data_ptr() + f4, a.grad.data_ptr() + f4, self.exp_avg.data_ptr() + f4,
+                      self.exp_avg_sq.data_ptr() + f4, None if self.shadow is None else self.shadow.data_ptr() + b2,
+                      end - start, self._hp_dev.data_ptr(), _lib.ptr(self.skip_flag), self._step_dev.data_ptr(),
+                      _lib.stream_ptr(a.data.device))
+        else:
+            if skip_requested(self.skip_flag):
+                return
+            sl = slice(start, end)
+            adam_update_host(self, a.data[sl], a.grad[sl], self.exp_avg[sl], self.exp_avg_sq[sl])
+            if self.shadow is not None:
+                self.shadow[sl].copy_(a.data[sl])
 
     @torch.no_grad()
     def set_nonfinite_skip(self) -> torch.Tensor:

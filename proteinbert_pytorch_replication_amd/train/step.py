@@ -56,9 +56,19 @@ class PretrainStep:
                                    None if self.standard_loss else self.local_loss_fn,
                                    None if self.standard_loss else self.global_loss_fn, return_parts)
 
+    def overlapped_optimizer(self) -> bool:
+        """DP with the fused Adam and no gradient clipping (which needs the global norm first): the
+        update of every gradient bucket but the last runs beside the last bucket's all-reduce
+        (:meth:`..parallel.ddp.BucketedAllReduce.finish_and_step`)."""
+        return (self.ddp is not None and self.ddp.enabled and type(self.optimizer) is FusedAdam
+                and self.grad_clip is None and getattr(self.ddp, "overlap_optimizer", True))
+
     def __call__(self, X, Y, W) -> torch.Tensor:
         opt = self.optimizer
         opt.zero_grad()
+        overlap = self.overlapped_optimizer()
+        if overlap:
+            self.ddp.begin_overlapped_step()
         loss, l_local, l_global = self.loss(X, Y, W, return_parts=True)
         # device scalars (no host sync): the per-head losses of the last step, for the metrics
         self.last_parts = (l_local.detach(), l_global.detach())
@@ -70,6 +80,9 @@ class PretrainStep:
             streams.join()                      # conv weight gradients ran on the aux stream
         else:
             loss.backward()
+        if overlap:
+            self.ddp.finish_and_step(opt, self.skip_nonfinite)
+            return loss.detach()
         if self.ddp is not None:
             self.ddp.finish(average=not self.fused)
         if self.grad_clip is not None:

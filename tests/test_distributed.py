@@ -32,8 +32,9 @@ def _env(rank, world, port):
                       MASTER_PORT=str(port))
 
 
-def _dp_worker(rank, world, port, out_dir, steps, comm="fp32"):
+def _dp_worker(rank, world, port, out_dir, steps, comm="fp32", overlap=True):
     _env(rank, world, port)
+    os.environ["PBX_DP_OVERLAP_OPT"] = "1" if overlap else "0"
     torch.set_num_threads(1)
     from proteinbert_pytorch_replication_amd.parallel import dist as pdist
     from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce
@@ -50,6 +51,7 @@ def _dp_worker(rank, world, port, out_dir, steps, comm="fp32"):
                             use_kernel=False)
     for _ in range(steps):
         step(*gen.next_batch())
+    assert step.overlapped_optimizer() == overlap
     torch.save({k: v.detach().clone() for k, v in m.state_dict().items()},
                os.path.join(out_dir, f"rank{rank}.pt"))
     pdist.destroy()
@@ -91,6 +93,48 @@ def test_dp_bucketed_allreduce_equals_averaged_gradients(tmp_path, comm):
             assert float((d > 1e-3).float().mean()) < 0.05, k
             continue
         torch.testing.assert_close(r0[k], v, rtol=1e-4, atol=2e-5, msg=k)
+
+
+def test_dp_overlapped_optimizer_bitwise_equals_whole_arena_step(tmp_path):
+    """Per-bucket Adam beside the last bucket's all-reduce (BucketedAllReduce.finish_and_step) gives
+    bitwise the parameters of finish() + one whole-arena update (Adam is element-wise)."""
+    steps, world = 3, 2
+    for tag, ov in (("ov", True), ("whole", False)):
+        d = tmp_path / tag
+        d.mkdir()
+        mp.start_processes(_dp_worker, args=(world, _free_port(), str(d), steps, "fp32", ov), nprocs=world,
+                           start_method="spawn", join=True)
+    a = torch.load(tmp_path / "ov" / "rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "whole" / "rank0.pt", weights_only=True)
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def _nonfinite_worker(rank, world, port, out_dir):
+    """Rank 1 poisons one gradient of the FIRST bucket: every rank must skip every bucket's update."""
+    _env(rank, world, port)
+    torch.set_num_threads(1)
+    from proteinbert_pytorch_replication_amd.parallel import dist as pdist
+    from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce
+    pdist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    m = ProteinBERT(backend="torch", **CFG)
+    opt = FusedAdam(m.parameters(), lr=1e-2)
+    ddp = BucketedAllReduce(opt.arena, bucket_mb=0.004)
+    step = PretrainStep(m, opt, ddp)
+    before = opt.arena.data.clone()
+    first = opt.arena.params[0]
+    if rank == 1:
+        first.register_hook(lambda g: g * float("nan"))
+    step(*SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=100 + rank,
+                            use_kernel=False).next_batch())
+    assert torch.equal(opt.arena.data, before), f"rank {rank} updated despite a non-finite gradient"
+    pdist.destroy()
+
+
+def test_dp_overlapped_optimizer_skips_all_buckets_on_nonfinite(tmp_path):
+    mp.start_processes(_nonfinite_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn",
+                       join=True)
 
 
 def _pretrain_worker(rank, world, port, save, zero=False):

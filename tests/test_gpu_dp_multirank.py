@@ -38,8 +38,12 @@ def _batch(rank):
     return SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], B, "cuda", seed=100 + rank).next_batch()
 
 
-def _worker(rank, world, port, out, semantics):
+def _worker(rank, world, port, out, semantics, overlap=True, deterministic=False):
     import datetime
+    os.environ["PBX_DP_OVERLAP_OPT"] = "1" if overlap else "0"
+    if deterministic:
+        from proteinbert_pytorch_replication_amd.utils import determinism
+        determinism.enable()
     import torch.distributed as dist
     from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce
     from proteinbert_pytorch_replication_amd.train.optim import FusedAdam
@@ -54,6 +58,7 @@ def _worker(rank, world, port, out, semantics):
         assert ddp.enabled and len(ddp.buckets) > 4
         ddp.broadcast_parameters(m)
         step = PretrainStep(m, opt, ddp)
+        assert step.overlapped_optimizer() == overlap
         loss = step(*_batch(rank))
         torch.cuda.synchronize()
         torch.save({"params": opt.arena.data.cpu(), "loss": float(loss)}, os.path.join(out, f"r{rank}.pt"))
@@ -91,3 +96,17 @@ def test_two_rank_dp_step_equals_mean_gradient_step(tmp_path, semantics):
     d = (res[0]["params"] - ref).abs()
     assert float(d.max()) <= 2e-3
     assert float((d > 1e-5).float().mean()) < 0.02, float((d > 1e-5).float().mean())
+
+
+def test_two_rank_overlapped_optimizer_bitwise_equals_whole_arena_step(tmp_path):
+    """Per-bucket Adam beside the last bucket's all-reduce == all-reduce everything, then one
+    whole-arena Adam: bitwise, with the fused backward in its fixed-order (deterministic) form."""
+    world = 2
+    for tag, ov in (("ov", True), ("whole", False)):
+        d = tmp_path / tag
+        d.mkdir()
+        mp.start_processes(_worker, args=(world, _port(), str(d), "reference", ov, True), nprocs=world,
+                           start_method="spawn", join=True)
+    a = torch.load(tmp_path / "ov" / "r0.pt", weights_only=True)
+    b = torch.load(tmp_path / "whole" / "r0.pt", weights_only=True)
+    assert torch.equal(a["params"], b["params"])

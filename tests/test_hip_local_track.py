@@ -68,14 +68,18 @@ def test_local_block_forward(L, B, frozen):
     assert e_v < 1.5e-2
 
 
-# pool backward: attn_bwd2 (stored GELU' fragments) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD
-@pytest.mark.parametrize("recompute,wide", [(0, 1), (1, 1), (1, 0)])
+# pool backward: attn_bwd4 (weight-stationary, csrc/pool_bwd.hip) / attn_bwd2 (stored GELU' fragments, Wv in
+# LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup
+@pytest.mark.parametrize("recompute,wide,bwd4,tpw", [(0, 1, 1, 0), (0, 1, 1, 3), (0, 1, 0, 0), (1, 1, 0, 0),
+                                                     (1, 0, 0, 0)])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
-def test_local_block_backward(L, B, recompute, wide, monkeypatch):
+def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     monkeypatch.setattr(local_track, "POOL_RECOMPUTE", recompute)
     monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
+    monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
+    monkeypatch.setattr(local_track, "POOL_BWD4_TPW", tpw)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
@@ -169,6 +173,7 @@ def test_arena_direct_grads_match_autograd_path():
     direct = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
     opt.zero_grad()
     m.backend = "torch"
+    step.compute_dtype = torch.float32          # plain fp32 PyTorch oracle (not the bf16 eager path)
     step.loss(X, Y, W).backward()
     ref = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
     torch.cuda.synchronize()

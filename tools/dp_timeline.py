@@ -57,7 +57,29 @@ def run(a):
         return orig_finish(*args, **kw)
 
     ddp.finish = finish
+    orig_fs = ddp.finish_and_step
+
+    def finish_and_step(*args, **kw):                      # overlapped optimizer (PretrainStep default)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(torch.cuda.current_stream(dev))
+        marks.append((ev, -1))
+        return orig_fs(*args, **kw)
+
+    ddp.finish_and_step = finish_and_step
+    orig_range = opt.step_range
+    ranges = []
+
+    def step_range(s0, e0):                                # Adam launches: (start event, end event, elements)
+        e_a = torch.cuda.Event(enable_timing=True)
+        e_b = torch.cuda.Event(enable_timing=True)
+        e_a.record(torch.cuda.current_stream(dev))
+        orig_range(s0, e0)
+        e_b.record(torch.cuda.current_stream(dev))
+        ranges.append((e_a, e_b, e0 - s0))
+
+    opt.step_range = step_range
     for i in range(a.steps):
+        ranges.clear()
         marks.clear()
         t0 = torch.cuda.Event(enable_timing=True)
         t1 = torch.cuda.Event(enable_timing=True)
@@ -74,6 +96,10 @@ def run(a):
                 print(f"  bucket {k:2d}  {n / 2**20:6.2f} MB  gradients final at {t:7.3f} ms"
                       f"  ({'inside backward' if t < bwd_end - 1e-3 else 'after backward'})")
             print(f"  backward (+ aux streams) ends at {bwd_end:.3f} ms; Adam ends at {total:.3f} ms")
+            last_ar = t0.elapsed_time([ev for ev, n in marks if n >= 0][-1])
+            for e_a, e_b, n in ranges:
+                print(f"  Adam over {n * 4 / 2**20:6.2f} MB of parameters: {t0.elapsed_time(e_a):7.3f} -> "
+                      f"{t0.elapsed_time(e_b):7.3f} ms (last bucket's all-reduce enqueued at {last_ar:7.3f} ms)")
     dist.destroy_process_group()
 
 

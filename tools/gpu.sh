@@ -58,7 +58,7 @@ run_task() {
     prof)
       local tag=$1; shift
       rm -rf gpurun_out/$tag
-      $T 400 rocprofv3 --kernel-trace --stats -d gpurun_out/$tag -o run -- python3 -u bench.py --steps 10 --warmup 3 "$@" \
+      $T 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 -u bench.py --steps 10 --warmup 3 "$@" \
         > gpurun_out/$tag.log 2>&1 || fatal $? "prof $tag"
       local st tr
       st=$(find gpurun_out/$tag -name '*kernel_stats.csv' | head -1)
@@ -69,7 +69,7 @@ run_task() {
     pmc)
       local tag=$1 ctr=$2; shift 2
       rm -rf gpurun_out/$tag
-      timeout -s KILL 300 rocprofv3 --kernel-trace --pmc ${ctr//,/ } -d gpurun_out/$tag -o run -- \
+      timeout -s KILL 300 rocprofv3 --kernel-trace --output-format csv --pmc ${ctr//,/ } -d gpurun_out/$tag -o run -- \
         python3 -u bench.py --steps 3 --warmup 2 "$@" > gpurun_out/$tag.log 2>&1 || fatal $? "pmc $tag"
       echo "pmc $tag done" ;;
     py)
