@@ -104,19 +104,36 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   // chunk 2 kb + h) is rowb + 8192 pt + ((32 kb) ^ gs) with rowb / gs fixed per tap, so a step costs one
   // v_xad_u32 instead of the ~7 VALU of the general swizzle; the weight fragment address is a scalar
   // base + the lane offset (no per-step 64-bit vector add)
-  for (int k = 0; k < KS; ++k) {
+  // B fragments (the x rows) are read one K-step ahead into a 2-deep register ring, so an MFMA never
+  // waits on the LDS read issued right before it (the previous form read them in front of their own
+  // MFMAs: an s_waitcnt lgkmcnt per MFMA pair, the LDS latency exposed on every step)
+  bf16x8 bq[2][NPT];
+  auto rows_of = [&](int k, int& rowb, int& gs) {
     const int rb = halo + r + (k - half) * d;
-    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+    rowb = rb << 8;
+    gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+  };
+  int rowb, gs;
+  rows_of(0, rowb, gs);
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) bq[0][pt] = lds_frag(xs, (0 ^ gs) + rowb + pt * 8192);
+  for (int k = 0; k < KS; ++k) {
+    int rowbn, gsn;
+    rows_of(min(k + 1, KS - 1), rowbn, gsn);
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const int it = k * 8 + kb;
       const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
       fr[(kb + 3) & 3] = fwk[lane];
-      __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
-      const int off = ((32 * kb) ^ gs) + rowb;
+      const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
 #pragma unroll
-      for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(xs, off + pt * 8192), acc[pt]);
+      for (int pt = 0; pt < NPT; ++pt) bq[(kb + 1) & 1][pt] = lds_frag(xs, noff + pt * 8192);
+      __builtin_amdgcn_sched_barrier(0);          // keep both prefetches ahead of this step's MFMAs
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], bq[kb & 1][pt], acc[pt]);
     }
+    rowb = rowbn;
+    gs = gsn;
   }
 
   // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
@@ -298,19 +315,33 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   const int d = cv ? dil : 1;
   const unsigned char* as = cv ? aw : an;
   const int halo = cv ? halo_w : halo_n;
-  for (int k = 0; k < KS; ++k) {                  // tap loop / unrolled channel blocks, as in conv_fwd3
+  bf16x8 bq[2][4];                                // B fragments one K-step ahead, as in conv_fwd3
+  auto rows_of = [&](int k, int& rowb, int& gs) {
     const int rb = halo + r - (k - half) * d;
-    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+    rowb = rb << 8;
+    gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+  };
+  int rowb, gs;
+  rows_of(0, rowb, gs);
+#pragma unroll
+  for (int pt = 0; pt < 4; ++pt) bq[0][pt] = lds_frag(as, (0 ^ gs) + rowb + pt * 8192);
+  for (int k = 0; k < KS; ++k) {                  // tap loop / unrolled channel blocks, as in conv_fwd3
+    int rowbn, gsn;
+    rows_of(min(k + 1, KS - 1), rowbn, gsn);
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const int it = k * 8 + kb;
       const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
       fr[(kb + 3) & 3] = fwk[lane];
-      __builtin_amdgcn_sched_barrier(0);          // keep the prefetch ahead of this step's MFMAs
-      const int off = ((32 * kb) ^ gs) + rowb;
+      const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
 #pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(as, off + pt * 8192), acc[pt]);
+      for (int pt = 0; pt < 4; ++pt) bq[(kb + 1) & 1][pt] = lds_frag(as, noff + pt * 8192);
+      __builtin_amdgcn_sched_barrier(0);          // keep both prefetches ahead of this step's MFMAs
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], bq[kb & 1][pt], acc[pt]);
     }
+    rowb = rowbn;
+    gs = gsn;
   }
 
   // epilogue: the wide half stages its fp32 partial ([BM][128] fp32, 16-B chunks XOR-swizzled by

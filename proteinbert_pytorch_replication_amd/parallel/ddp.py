@@ -19,11 +19,11 @@ collectives per step.
 * ``SUM`` reduction; the 1/world factor is folded into the fused Adam
   (``FusedAdam.grad_scale``) instead of an extra pass.
 * :meth:`finish_and_step` (the training step's default with the fused Adam) hides the optimizer
-  behind the exposed tail: the last bucket (global input layer + block 0, ~20 MB, ready only after
-  backward) is still on the wire when the Adam update of every other bucket runs on the compute
-  stream; only the last bucket's update trails its all-reduce.  The group-wide non-finite decision is
-  taken BEFORE any update: each bucket's local gradients are tested as it is launched, and one 4-byte
-  MAX all-reduce of the OR of those flags is queued ahead of the last bucket's all-reduce, so every rank
+  behind the exposed tail: the buckets whose gradients are final only after backward (the global input
+  layer + block 0, ~20 MB) are still on the wire when the Adam update of every other bucket runs on the
+  compute stream; only the tail buckets' update trails their all-reduce.  The group-wide non-finite
+  decision is taken BEFORE any update: each bucket's local gradients are tested as it is launched, and
+  one 4-byte MAX all-reduce of the OR of those flags is queued ahead of the tail buckets, so every rank
   skips or commits every bucket together.  (The test is on local gradients: a sum of finite per-rank
   gradients that overflows fp32 is not caught, where the previous post-reduction test caught it.)
 * ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
@@ -68,7 +68,15 @@ class BucketedAllReduce:
                 self.buckets.append([start, cur_end])
                 start = None
         if start is not None:
-            self.buckets.append([start, cur_end])
+            if self.buckets and cur_end - start < limit // 4:
+                # a small remainder (the embedding / input-layer bias, last to finish) joins the last
+                # bucket: one collective instead of two latency-bound ones at the exposed end of backward
+                self.buckets[-1][1] = cur_end
+                for i in range(len(self.param_bucket)):
+                    if self.param_bucket[i] == len(self.buckets):
+                        self.param_bucket[i] = len(self.buckets) - 1
+            else:
+                self.buckets.append([start, cur_end])
         self.bucket_nparams = [0] * len(self.buckets)
         for b in self.param_bucket:
             self.bucket_nparams[b] += 1
@@ -133,7 +141,7 @@ class BucketedAllReduce:
             bad = not bool(torch.isfinite(torch.dot(view, torch.zeros_like(view))))
             self._flags[b] = 1 if bad else 0
 
-    def _launch(self, b: int) -> None:
+    def _launch(self, b: int, flag_done: bool = False) -> None:
         s, e = self.buckets[b]
         view = self.arena.grad[s:e]
         dt = self.comm_dtype
@@ -141,20 +149,30 @@ class BucketedAllReduce:
         # (ops/streams.py): enqueue the collective behind both streams without stalling this one
         ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()
         with ctx:
-            if self.track_nonfinite:
+            if self.track_nonfinite and not flag_done:
                 self._local_flag(b, view)
-                if b == len(self.buckets) - 1:
-                    # every bucket's local flag is in: the group-wide decision travels ahead of the last
-                    # (largest, exposed) bucket, so the other buckets' updates need not wait for it
-                    self._gflag = self._flags.amax().reshape(1)
-                    self._flag_work = dist.all_reduce(self._gflag, op=dist.ReduceOp.MAX, group=self.pg,
-                                                      async_op=True)
             if dt != torch.float32:
                 tmp = view.to(dt)
                 self._tmp[b] = tmp
                 self._works[b] = dist.all_reduce(tmp, group=self.pg, async_op=True)
             else:
                 self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
+
+    def _flag_reduce_and_launch_rest(self) -> None:
+        """Local flags of the buckets not launched yet, the group-wide MAX of every bucket's flag (4 bytes,
+        queued ahead), then those buckets' all-reduces."""
+        rest = range(self._next, len(self.buckets))
+        dev = self.arena.grad.device
+        ctx = streams.collective_stream(dev) if self.arena.grad.is_cuda else contextlib.nullcontext()
+        with ctx:
+            for b in rest:
+                s, e = self.buckets[b]
+                self._local_flag(b, self.arena.grad[s:e])
+            self._gflag = self._flags.amax().reshape(1)
+            self._flag_work = dist.all_reduce(self._gflag, op=dist.ReduceOp.MAX, group=self.pg, async_op=True)
+        for b in rest:
+            self._launch(b, flag_done=True)
+        self._next = len(self.buckets)
 
     def _land(self, b: int) -> None:
         """Current stream waits for bucket b's all-reduce (and copies a reduced bf16 bucket back)."""
@@ -205,19 +223,21 @@ class BucketedAllReduce:
             return
         if self.arena.grad.is_cuda:
             streams.join()
-        for b in range(self._next, len(self.buckets)):
-            self._launch(b)
-        self._next = len(self.buckets)
-        last = len(self.buckets) - 1
-        for b in range(last):
+        if self._flags is None:
+            self._flags = torch.zeros(len(self.buckets), dtype=torch.int32, device=self.arena.grad.device)
+        # the exposed tail: buckets whose gradients were not final during backward (launched only now)
+        # (all of them launched already: the update waits only for the flag, queued behind them)
+        split_b = self._next
+        self._flag_reduce_and_launch_rest()
+        for b in range(split_b):
             self._land(b)
-        if self._flag_work is not None:
-            self._flag_work.wait()
+        self._flag_work.wait()
         opt.skip_flag = self._gflag if skip_nonfinite else None
         opt.begin_step()
-        split = self.buckets[last][0]
-        opt.step_range(0, split)
-        self._land(last)
+        split = self.buckets[split_b][0] if split_b < len(self.buckets) else self.arena.numel
+        opt.step_range(0, split)              # beside the tail buckets' all-reduce
+        for b in range(split_b, len(self.buckets)):
+            self._land(b)
         opt.step_range(split, self.arena.numel)
         self.track_nonfinite = False
         self._flag_work = None
