@@ -48,8 +48,9 @@ def register(name: str, argtypes) -> None:
     """Kernel modules declare their launchers here (before first use)."""
     _SIGS[name] = argtypes
     if _lib is not None:
-        fn = getattr(_lib, name)
-        fn.argtypes, fn.restype = argtypes, ctypes.c_int
+        fn = getattr(_lib, name, None)
+        if fn is not None:
+            fn.argtypes, fn.restype = argtypes, ctypes.c_int
 
 
 def lib() -> ctypes.CDLL:
@@ -61,7 +62,9 @@ def lib() -> ctypes.CDLL:
         _ = torch.cuda.is_available()  # make sure torch's HIP runtime is loaded first
         _lib = ctypes.CDLL(HIP_LIB, mode=ctypes.RTLD_LOCAL)
         for name, args in _SIGS.items():
-            fn = getattr(_lib, name)
+            fn = getattr(_lib, name, None)
+            if fn is None:       # an older A/B build (PBX_HIP_LIB) without this launcher: call() raises
+                continue
             fn.argtypes, fn.restype = args, ctypes.c_int
     return _lib
 
@@ -95,7 +98,10 @@ def call(name: str, *args) -> None:
     if fn is None:
         if name not in _SIGS:   # ctypes would pass Python ints as 32-bit C ints and truncate device pointers
             raise HipError(f"{name}: launcher not registered (import the ops module that declares it)")
-        fn = _FN[name] = getattr(lib(), name)
+        fn = getattr(lib(), name, None)
+        if fn is None:
+            raise HipError(f"{name}: not exported by {HIP_LIB}")
+        _FN[name] = fn
     rc = fn(*args)
     if rc != 0:
         raise HipError(f"{name} failed with hipError {rc}")

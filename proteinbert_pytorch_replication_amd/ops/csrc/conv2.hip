@@ -14,9 +14,9 @@
 //
 //   conv_fwd3   : 128 positions / workgroup; waves 0-3 = narrow conv, 4-7 = wide conv; wave q owns
 //                 output channels q*32..+32 for all 128 positions (4 accumulators of 32x32).
-//                 Epilogue: pre_n and pre_w staged through LDS; all 8 waves then write them and
-//                 s1 = x + GELU(pre_n) + GELU(pre_w) + gb with row-contiguous 16-B stores, plus the
-//                 tile's LayerNorm (mean, M2) partial.
+//                 Epilogue: the pre-activations staged through LDS; all 8 waves then write
+//                 s1 = x + GELU(pre_n) + GELU(pre_w) + gb and (training) GELU'(pre_n), GELU'(pre_w)
+//                 with row-contiguous 16-B stores, plus the tile's LayerNorm (mean, M2) partial.
 //   conv_dgrad3 : both convs' dpre = dS1 * GELU'(pre) tiles (with their halos) staged once and their
 //                 central rows written for the weight gradient; waves 0-3 = narrow, 4-7 = wide, wave
 //                 q owns input channels q*32..+32; the two halves are summed through LDS in the
@@ -53,6 +53,7 @@ __device__ __forceinline__ int frag_index(int k, int kb, int mb) { return (k * 8
 
 // TBM = 128 positions per workgroup: two workgroups per CU at <= 128 VGPRs (a 256-position form, one
 // workgroup per CU with every weight fragment feeding 8 MFMAs, measured slower in the full step)
+template <bool STORE>   // STORE: write GELU'(pre) of both convs for the backward (training forward)
 __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
@@ -104,6 +105,22 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   // chunk 2 kb + h) is rowb + 8192 pt + ((32 kb) ^ gs) with rowb / gs fixed per tap, so a step costs one
   // v_xad_u32 instead of the ~7 VALU of the general swizzle; the weight fragment address is a scalar
   // base + the lane offset (no per-step 64-bit vector add)
+#ifdef PBX_CONV_BPF0   // ablation: B fragments read right before their MFMAs (round-3 form)
+  for (int k = 0; k < KS; ++k) {
+    const int rb = halo + r + (k - half) * d;
+    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int it = k * 8 + kb;
+      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;
+      fr[(kb + 3) & 3] = fwk[lane];
+      __builtin_amdgcn_sched_barrier(0);
+      const int off = ((32 * kb) ^ gs) + rowb;
+#pragma unroll
+      for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(xs, off + pt * 8192), acc[pt]);
+    }
+  }
+#else
   // B fragments (the x rows) are read one K-step ahead into a 2-deep register ring, so an MFMA never
   // waits on the LDS read issued right before it (the previous form read them in front of their own
   // MFMAs: an s_waitcnt lgkmcnt per MFMA pair, the LDS latency exposed on every step)
@@ -135,6 +152,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     rowb = rowbn;
     gs = gsn;
   }
+#endif
 
   // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
   // Both pre-activation tiles are staged in LDS (narrow -> ot, wide -> over the x tile, whose 4 rows
@@ -180,10 +198,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     const uint4 pnq = *reinterpret_cast<const uint4*>(ot + swz256(row, c));
     const uint4 pwq = *reinterpret_cast<const uint4*>(smem + swz256(row, c));
     const size_t off = ((size_t)b * L + pos0 + row) * CH + c * 8;
-    if (ok && pre_n != nullptr) {                  // null: no backward will read them (inference)
-      *reinterpret_cast<uint4*>(pre_n + off) = pnq;
-      *reinterpret_cast<uint4*>(pre_w + off) = pwq;
-    }
     float xv[8], pn[8], pw[8];
     unpack8(xq[i], xv);
     unpack8(pnq, pn);
@@ -195,9 +209,40 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       gi[4 + e] = (f32x2){pw[2 * e], pw[2 * e + 1]};
     }
     // scalar A&S stages (gelu_scalar_n): this epilogue runs beside the other waves' MFMAs, where the
-    // packed form measured 3 % slower on the kernel (tools/gpu_scalar_ab.sh)
-    gelu_scalar_n<4, 0>(gi, go, nullptr);
-    gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
+    // packed form measured 3 % slower on the kernel.  Training: GELU AND GELU' from one shared core
+    // (+2 VALU per value); GELU' is what the data gradient multiplies by, so it is stored instead of the
+    // pre-activation and conv_dgrad3 no longer evaluates a GELU' core per value (~14 VALU + 2
+    // transcendentals, on 1.2x the values for the halo rows)
+#ifdef PBX_CONV_PRE   // ablation: store the pre-activation, the data gradient evaluates GELU' (round-3 form)
+    if (STORE && ok) {
+      *reinterpret_cast<uint4*>(pre_n + off) = pnq;
+      *reinterpret_cast<uint4*>(pre_w + off) = pwq;
+    }
+    if (true) {
+      gelu_scalar_n<4, 0>(gi, go, nullptr);
+      gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
+    } else
+#endif
+    if constexpr (STORE) {
+      f32x2 gd[8];
+      gelu_scalar_n<4, 2>(gi, go, gd);
+      gelu_scalar_n<4, 2>(gi + 4, go + 4, gd + 4);
+      float dn[8], dw[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        dn[2 * e] = gd[e].x;
+        dn[2 * e + 1] = gd[e].y;
+        dw[2 * e] = gd[4 + e].x;
+        dw[2 * e + 1] = gd[4 + e].y;
+      }
+      if (ok) {
+        *reinterpret_cast<uint4*>(pre_n + off) = packq8(dn);
+        *reinterpret_cast<uint4*>(pre_w + off) = packq8(dw);
+      }
+    } else {
+      gelu_scalar_n<4, 0>(gi, go, nullptr);
+      gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
+    }
     float o[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -289,17 +334,22 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
         const int pos = pos0 - halo + j;
         float g[8], pv[8], o[8];
         unpack8(gq[i], g);
-        unpack8(pq[i], pv);
-        // GELU' of the 8 values as interleaved scalar A&S stages (gelu_scalar_n, as in the forward)
-        f32x2 pp[4], gd[4];
+        unpack8(pq[i], pv);                         // GELU'(pre), stored by the forward
+#ifdef PBX_CONV_PRE
+        {
+          f32x2 pp[4], gd[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) pp[e] = (f32x2){pv[2 * e], pv[2 * e + 1]};
-        gelu_scalar_n<4, 1>(pp, nullptr, gd);
+          for (int e = 0; e < 4; ++e) pp[e] = (f32x2){pv[2 * e], pv[2 * e + 1]};
+          gelu_scalar_n<4, 1>(pp, nullptr, gd);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[2 * e] = gd[e].x * g[2 * e];
-          o[2 * e + 1] = gd[e].y * g[2 * e + 1];
+          for (int e = 0; e < 4; ++e) {
+            pv[2 * e] = gd[e].x;
+            pv[2 * e + 1] = gd[e].y;
+          }
         }
+#endif
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = pv[e] * g[e];
         const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
         if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
           *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
@@ -315,6 +365,22 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
   const int d = cv ? dil : 1;
   const unsigned char* as = cv ? aw : an;
   const int halo = cv ? halo_w : halo_n;
+#ifdef PBX_CONV_BPF0   // ablation: B fragments read right before their MFMAs (round-3 form)
+  for (int k = 0; k < KS; ++k) {
+    const int rb = halo + r - (k - half) * d;
+    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+#pragma unroll
+    for (int kb = 0; kb < 8; ++kb) {
+      const int it = k * 8 + kb;
+      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;
+      fr[(kb + 3) & 3] = fwk[lane];
+      __builtin_amdgcn_sched_barrier(0);
+      const int off = ((32 * kb) ^ gs) + rowb;
+#pragma unroll
+      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(as, off + pt * 8192), acc[pt]);
+    }
+  }
+#else
   bf16x8 bq[2][4];                                // B fragments one K-step ahead, as in conv_fwd3
   auto rows_of = [&](int k, int& rowb, int& gs) {
     const int rb = halo + r - (k - half) * d;
@@ -343,6 +409,7 @@ __global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
     rowb = rowbn;
     gs = gsn;
   }
+#endif
 
   // epilogue: the wide half stages its fp32 partial ([BM][128] fp32, 16-B chunks XOR-swizzled by
   // row), the narrow half adds its own in place, then dx = ds1 + sum, row-contiguous 16-B accesses.
@@ -418,14 +485,16 @@ int dgrad3_lds(int KS, int dil) {
 static bool conv3_attrs_set = false;
 static void set_conv3_attrs() {
   if (conv3_attrs_set) return;
-  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+  (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   conv3_attrs_set = true;
 }
 
 // LayerNorm partials in `stats` are per 128-position tile: [B][ceil(L/128)][2].  fwn/fww: forward
 // fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels; gb [B][128] fp32.
-// pre_n / pre_w may be null (inference: no backward reads them).
+// pre_n / pre_w: GELU'(pre-activation) of the narrow / wide conv as bf16 (what conv_dgrad3 multiplies the
+// incoming gradient by), or both null (inference: no backward reads them).
 PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
                              int dil, hipStream_t st) {
@@ -433,7 +502,9 @@ PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, co
   const int lds = fwd3_lds(KS, dil, BM);
   if (lds > 163840 || dil < 1 || KS < 2 || gb == nullptr) return (int)hipErrorInvalidValue;
   const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_fwd3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
+  if ((pre_n == nullptr) != (pre_w == nullptr)) return (int)hipErrorInvalidValue;
+  const auto kern = pre_n != nullptr ? conv_fwd3_kernel<true> : conv_fwd3_kernel<false>;
+  hipLaunchKernelGGL(kern, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
                      (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
   return pbx_launch_status();
 }

@@ -101,25 +101,20 @@ __device__ __forceinline__ float block_sum256(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
-template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
-__global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B,
-                                                      long ldb, float* __restrict__ C, long ldc, int M, int N, int K,
-                                                      int kchunks_per_split, int accumulate, GoArgs go) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+// The K loop of one 128 x 128 output tile (rows m0.., cols n0.., K chunks kc0 .. kc1) into acc.
+template <int TA, int TB, bool AL_A, bool AL_B>
+__device__ __forceinline__ void gemm_mainloop(f32x16_t (&acc)[2][2], unsigned char* smem, const bf16_t* __restrict__ A,
+                                              long lda, const bf16_t* __restrict__ B, long ldb, int M, int N, int K,
+                                              int m0, int n0, int kc0, int kc1) {
   unsigned char* As = smem;
   unsigned char* Bs = smem + TILE;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int q = tr_q(lane), tc = tr_c(lane);
   const int wm = w >> 1, wn = w & 1;
-  const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
-  const int nkc = (K + BK - 1) / BK;
-  const int kc0 = blockIdx.z * kchunks_per_split;
-  const int kc1 = min(nkc, kc0 + kchunks_per_split);
   constexpr bool AK = TA == 0, BKM = TB == 1;     // K runs along memory
   Stager<AK, AL_A> sa;
   Stager<BKM, AL_B> sb;
-  f32x16_t acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -147,43 +142,66 @@ __global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__
       acc[1][1] = mfma32(a1, b1, acc[1][1]);
     }
   }
-  // D layout: lane (r, h), register e -> row (e & 3) + 8 (e >> 2) + 4 h, column r of each 32 x 32 tile
-  if constexpr (EPI == EPI_STORE) {
-    // accumulate: all 64 reads of C are issued before the first store (C is not restrict, so a fused
-    // load-add-store per element serialises 64 memory round trips: 42 vs 15 us on a cold 512^3 GEMM)
-    float* dst = C + (size_t)blockIdx.z * M * ldc;   // split-K slab (z > 0 only when gridDim.z > 1)
-    if (accumulate) {
-      float old[2][2][16];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int n = n0 + wn * 64 + j * 32 + r;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-            old[i][j][e] = (n < N && m < M) ? __builtin_nontemporal_load(dst + (size_t)m * ldc + n) : 0.f;
-          }
-        }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] += old[i][j][e];
-    }
+}
+
+// D layout: lane (r, h), register e -> row (e & 3) + 8 (e >> 2) + 4 h, column r of each 32 x 32 tile.
+// accumulate: all 64 reads of C are issued before the first store (C is not restrict, so a fused
+// load-add-store per element serialises 64 memory round trips: 42 vs 15 us on a cold 512^3 GEMM)
+__device__ __forceinline__ void gemm_store(f32x16_t (&acc)[2][2], float* dst, long ldc, int M, int N, int m0, int n0,
+                                           int accumulate) {
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  if (accumulate) {
+    float old[2][2][16];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int n = n0 + wn * 64 + j * 32 + r;
-        if (n >= N) continue;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          if (m < M) dst[(size_t)m * ldc + n] = acc[i][j][e];
+          old[i][j][e] = (n < N && m < M) ? __builtin_nontemporal_load(dst + (size_t)m * ldc + n) : 0.f;
         }
       }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] += old[i][j][e];
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + r;
+      if (n >= N) continue;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (m < M) dst[(size_t)m * ldc + n] = acc[i][j][e];
+      }
+    }
+}
+
+template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
+__global__ void __launch_bounds__(256, 2) gemm_kernel(const bf16_t* __restrict__ A, long lda, const bf16_t* __restrict__ B,
+                                                      long ldb, float* __restrict__ C, long ldc, int M, int N, int K,
+                                                      int kchunks_per_split, int accumulate, GoArgs go) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wm = w >> 1, wn = w & 1;
+  const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
+  const int nkc = (K + BK - 1) / BK;
+  const int kc0 = blockIdx.z * kchunks_per_split;
+  const int kc1 = min(nkc, kc0 + kchunks_per_split);
+  f32x16_t acc[2][2];
+  gemm_mainloop<TA, TB, AL_A, AL_B>(acc, smem, A, lda, B, ldb, M, N, K, m0, n0, kc0, kc1);
+  if constexpr (EPI == EPI_STORE) {
+    gemm_store(acc, C + (size_t)blockIdx.z * M * ldc, ldc, M, N, m0, n0, accumulate);   // split-K slab z
   } else {
     // GO head.  The 128 x 128 fp32 tile goes through LDS (row stride 132 floats) so the epilogue
     // runs on row-contiguous 8-column chunks: 2 x 16-B loads of y, one 16-B dz store, per thread a fixed
@@ -322,6 +340,49 @@ __global__ void __launch_bounds__(256) gemm_reduce_kernel(const float* __restric
     if (n + e < N) c[e] = accumulate ? c[e] + s[e] : s[e];
 }
 
+// Up to 4 independent GEMMs of one transpose / alignment class in ONE launch: grid.z = problem,
+// (grid.x, grid.y) = the largest problem's tiles (smaller problems' surplus tiles exit at once).  The
+// global-track weight gradients of a block (dW1, dW2, dWgl: K = B rows, accumulated into the arena)
+// were three split-K GEMMs + three slab folds on the weight-gradient stream; at K = B = 512 one
+// pass per output tile without split-K is cheaper than the slabs, and one launch instead of six.
+struct GemmBatch {
+  const bf16_t* A[4];
+  const bf16_t* B[4];
+  float* C[4];
+  long lda[4], ldb[4], ldc[4];
+  int M[4], N[4], K[4];
+};
+
+template <int TA, int TB, bool AL_A, bool AL_B>
+__global__ void __launch_bounds__(256, 2) gemm_batch_kernel(GemmBatch gb, int accumulate) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int z = blockIdx.z;
+  const int M = gb.M[z], N = gb.N[z], K = gb.K[z];
+  const int m0 = blockIdx.y * BT, n0 = blockIdx.x * BT;
+  if (m0 >= M || n0 >= N) return;                  // workgroup-uniform
+  f32x16_t acc[2][2];
+  gemm_mainloop<TA, TB, AL_A, AL_B>(acc, smem, gb.A[z], gb.lda[z], gb.B[z], gb.ldb[z], M, N, K, m0, n0, 0,
+                                    (K + BK - 1) / BK);
+  gemm_store(acc, gb.C[z], gb.ldc[z], M, N, m0, n0, accumulate);
+}
+
+template <int TA, int TB, bool AL_A, bool AL_B>
+int launch_batch(const GemmBatch& gb, int n, int accumulate, hipStream_t st) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm_batch_kernel<TA, TB, AL_A, AL_B>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 2 * TILE);
+    attr = true;
+  }
+  int mt = 1, nt = 1;
+  for (int i = 0; i < n; ++i) {
+    mt = max(mt, (gb.M[i] + BT - 1) / BT);
+    nt = max(nt, (gb.N[i] + BT - 1) / BT);
+  }
+  hipLaunchKernelGGL((gemm_batch_kernel<TA, TB, AL_A, AL_B>), dim3(nt, mt, n), dim3(256), 2 * TILE, st, gb, accumulate);
+  return pbx_launch_status();
+}
+
 template <int TA, int TB, bool AL_A, bool AL_B, int EPI>
 int launch(const void* A, long lda, const void* B, long ldb, float* C, long ldc, int M, int N, int K, int splitk,
            int accumulate, const GoArgs& go, hipStream_t st) {
@@ -392,4 +453,41 @@ PBX_EXPORT int pbx_go_head_fused(const void* x, long ldx, const void* w, long ld
   GoArgs go{bias, y, ldy, wrow, wfull, (bf16_t*)dz, lddz, dbias_part, loss_part, 1.0f / ((float)M * (float)N)};
   const bool aa = aligned(x, ldx, K, false), ab = aligned(w, ldw, K, false);
   return dispatch_al<0, 1, EPI_GO>(aa, ab, x, ldx, w, ldw, nullptr, 0, M, N, K, 1, 0, go, st);
+}
+
+// n (<= 4) GEMMs C_i (+)= op(A_i) op(B_i) of one (ta, tb) class in one launch (no split-K).
+// Arrays: A, B, C device pointers; lda, ldb, ldc, M, N, K per problem.
+PBX_EXPORT int pbx_gemm_batch(int n, const void* const* A, const long* lda, const void* const* B, const long* ldb,
+                              float* const* C, const long* ldc, const int* M, const int* N, const int* K, int ta, int tb,
+                              int accumulate, hipStream_t st) {
+  if (n < 1 || n > 4) return (int)hipErrorInvalidValue;
+  GemmBatch gb{};
+  bool aa = true, ab = true;
+  for (int i = 0; i < n; ++i) {
+    if (M[i] <= 0 || N[i] <= 0 || K[i] <= 0) return (int)hipErrorInvalidValue;
+    gb.A[i] = (const bf16_t*)A[i];
+    gb.B[i] = (const bf16_t*)B[i];
+    gb.C[i] = C[i];
+    gb.lda[i] = lda[i];
+    gb.ldb[i] = ldb[i];
+    gb.ldc[i] = ldc[i];
+    gb.M[i] = M[i];
+    gb.N[i] = N[i];
+    gb.K[i] = K[i];
+    aa = aa && aligned(A[i], lda[i], ta == 0 ? K[i] : M[i], false);
+    ab = ab && aligned(B[i], ldb[i], tb == 1 ? K[i] : N[i], false);
+  }
+#define PBX_GB(TA_, TB_)                                                        \
+  if (ta == TA_ && tb == TB_) {                                                  \
+    if (aa && ab) return launch_batch<TA_, TB_, true, true>(gb, n, accumulate, st);   \
+    if (aa) return launch_batch<TA_, TB_, true, false>(gb, n, accumulate, st);        \
+    if (ab) return launch_batch<TA_, TB_, false, true>(gb, n, accumulate, st);        \
+    return launch_batch<TA_, TB_, false, false>(gb, n, accumulate, st);               \
+  }
+  PBX_GB(1, 0)
+  PBX_GB(0, 0)
+  PBX_GB(0, 1)
+  PBX_GB(1, 1)
+#undef PBX_GB
+  return (int)hipErrorInvalidValue;
 }

@@ -75,6 +75,34 @@ def gemm(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor, ta: bool = False, 
     return out
 
 
+_lib.register("pbx_gemm_batch", [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+
+
+def gemm_batch(problems, ta: bool, tb: bool, accumulate: bool = True) -> None:
+    """``out_i[:M, :N] (+)= op(a_i) @ op(b_i)`` for up to 4 ``(a, b, out)`` problems of one transpose class
+    in ONE launch without split-K (``csrc/gemm.hip`` gemm_batch_kernel)."""
+    n = len(problems)
+    assert 1 <= n <= 4
+    arr = lambda ct, vals: (ct * n)(*vals)  # noqa: E731
+    A, B, C, lda, ldb, ldc, M, N, K = ([] for _ in range(9))
+    for a, b, out in problems:
+        assert a.dtype == torch.bfloat16 and b.dtype == torch.bfloat16 and out.dtype == torch.float32
+        assert a.stride(1) == 1 and b.stride(1) == 1 and out.stride(1) == 1
+        m = a.shape[1] if ta else a.shape[0]
+        k = a.shape[0] if ta else a.shape[1]
+        nn = b.shape[0] if tb else b.shape[1]
+        assert (b.shape[1] if tb else b.shape[0]) == k and out.shape[0] >= m and out.shape[1] >= nn
+        A.append(a.data_ptr()); B.append(b.data_ptr()); C.append(out.data_ptr())
+        lda.append(a.stride(0)); ldb.append(b.stride(0)); ldc.append(out.stride(0))
+        M.append(m); N.append(nn); K.append(k)
+    P, L64, I32 = ctypes.c_void_p, ctypes.c_long, ctypes.c_int
+    _lib.call("pbx_gemm_batch", n, arr(P, A), arr(L64, lda), arr(P, B), arr(L64, ldb), arr(P, C), arr(L64, ldc),
+              arr(I32, M), arr(I32, N), arr(I32, K), int(ta), int(tb), int(accumulate),
+              _lib.stream_ptr(problems[0][0].device))
+
+
 def mm(a: torch.Tensor, b: torch.Tensor, ta: bool = False, tb: bool = False, **kw) -> torch.Tensor:
     """New fp32 ``op(a) @ op(b)``."""
     M = a.shape[1] if ta else a.shape[0]

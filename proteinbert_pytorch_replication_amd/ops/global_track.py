@@ -20,7 +20,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from . import _lib, streams
-from .gemm import gemm as _gemm
+from .gemm import gemm as _gemm, gemm_batch
 from .gemm import go_head_parts
 from ..train.arena import notify_grads_ready
 from ..utils.determinism import fused_deterministic
@@ -356,6 +356,10 @@ GLOB3 = os.environ.get("PBX_GLOB3", "1") != "0"              # forward
 GLOB3_BWD = os.environ.get("PBX_GLOB3_BWD", "0") != "0"      # backward
 
 
+# global-track weight gradients as one batched GEMM launch (PBX_BATCH_WGRAD=0: three split-K GEMMs + folds)
+BATCH_WGRAD = os.environ.get("PBX_BATCH_WGRAD", "1") != "0"
+
+
 def glob_fused_ok(G: int, NGL: int) -> bool:
     """Shapes the fused global-track kernels are compiled for (pbx_glob_supported)."""
     return GLOBAL_FUSED and G in (256, 512) and NGL in (0, 128)
@@ -496,10 +500,14 @@ class FusedGlobalBlockFn(torch.autograd.Function):
                 # the per-row-tile column sums (bias / LayerNorm affine / attention-weight gradients)
                 _lib.call("pbx_glob3_fold", slab.data_ptr(), B, G, NGL, wp.numel(),
                           _ptrs(db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl if NGL else None, dwp), _s(dev))
-            addmm_into(dw1, du1.t(), g_bf)
-            addmm_into(dw2, du2.t(), g1_bf)
-            if NGL:
-                addmm_into(dwgl, dugl.t(), g2_bf)
+            # dW = dU^T X for W1, W2 and the next block's global->local weight: one batched launch,
+            # K = B rows, accumulated straight into the gradient destinations (no split-K slabs)
+            probs = [(du1, g_bf, dw1), (du2, g1_bf, dw2)] + ([(dugl, g2_bf, dwgl)] if NGL else [])
+            if BATCH_WGRAD and all(d.is_contiguous() and d.dtype == F32 for _, _, d in probs):
+                gemm_batch(probs, ta=True, tb=False, accumulate=True)
+            else:
+                for a, b, d in probs:
+                    addmm_into(d, a.t(), b)
 
         direct = all(gr.direct[i] for i in (0, 4)) and (not NGL or gr.direct[9])
         if slab is not None:

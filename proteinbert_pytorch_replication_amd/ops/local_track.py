@@ -31,6 +31,7 @@ from .global_track import bf16_of
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
@@ -86,9 +87,14 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+# conv forward: 1 (default) = persistent conv_fwd4 (csrc/conv4.hip: the epilogue of tile i-1 runs inside the
+# K loop of tile i); 0 = conv_fwd3 (csrc/conv2.hip, epilogue after each tile's MFMAs)
+CONV_FWD4 = int(os.environ.get("PBX_CONV_FWD4", "1"))
+
+
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream) -> None:
-    """``pre_n``/``pre_w`` None: the pre-activations are not stored (no backward)."""
-    _lib.call("pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+    """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward)."""
+    _lib.call("pbx_conv_fwd4" if CONV_FWD4 and KS == 9 else "pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
               gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, stream)
 
 

@@ -99,3 +99,23 @@ def test_go_head_fused_vs_fp32(B, A, per_row):
     assert abs(got_loss - loss.item()) < 1e-4 * abs(loss.item()) + 1e-9
     assert rel(dz, z.grad) < 5e-3                      # bf16 rounding of dz
     assert rel(dbp.sum(0), z.grad.sum(0)) < 5e-3
+
+
+@pytest.mark.parametrize("ta,tb", [(True, False), (False, False), (False, True), (True, True)])
+def test_gemm_batch_vs_fp32(ta, tb):
+    """One launch, several independent problems of different shapes (the global-track weight gradients:
+    two 512 x 512 and one 128 x 512 with K = B), accumulated in place; plus odd extents."""
+    from proteinbert_pytorch_replication_amd.ops.gemm import gemm_batch
+    torch.manual_seed(7)
+    shapes = [(512, 512, 512), (512, 512, 512), (128, 512, 512), (77, 130, 300)]
+    probs, refs = [], []
+    for M, N, K in shapes:
+        a = torch.randn((K, M) if ta else (M, K), device="cuda").to(torch.bfloat16)
+        b = torch.randn((N, K) if tb else (K, N), device="cuda").to(torch.bfloat16)
+        out = torch.randn(M, N, device="cuda")
+        refs.append(out.clone() + _op(a, ta) @ _op(b, tb))
+        probs.append((a, b, out))
+    gemm_batch(probs, ta, tb, accumulate=True)
+    torch.cuda.synchronize()
+    for (_, _, out), ref in zip(probs, refs):
+        assert rel(out, ref) < 1e-5

@@ -48,12 +48,32 @@ pre_n, pre_w, s1 = (torch.empty_like(x) for _ in range(3))
 stt = torch.empty(B, (L + 127) // 128, 2, device=dev)
 fwd = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
                         bias.data_ptr(), gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(),
-                        stt.data_ptr(), B, L, KS, dil, 128, st)
+                        stt.data_ptr(), B, L, KS, dil, st)
 us = timeit(fwd)
 print(f"[{a.tag}] conv_fwd3   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+ref = [t.clone() for t in (pre_n, pre_w, s1, stt)]
+fwd4 = lambda: _lib.call("pbx_conv_fwd4", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
+                         bias.data_ptr(), gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(),
+                         stt.data_ptr(), B, L, KS, dil, st)
+try:
+    us = timeit(fwd4)
+    err = [float((u.float() - v.float()).abs().max()) for u, v in zip(ref, (pre_n, pre_w, s1, stt))]
+    print(f"[{a.tag}] conv_fwd4   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s  max|fwd4 - fwd3| {err}", flush=True)
+except Exception as ex:  # older library builds have no conv_fwd4
+    print(f"[{a.tag}] conv_fwd4 unavailable: {ex}")
 ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
 dx, dpn, dpw = (torch.empty_like(x) for _ in range(3))
 dg = lambda: _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
                        ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, st)
 us = timeit(dg)
 print(f"[{a.tag}] conv_dgrad3 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+slab = torch.empty(64 * 2 * KS * C * C, device=dev)
+bslab = torch.empty(64 * 2 * C, device=dev)
+dwn, dww = torch.zeros(C, C, KS, device=dev), torch.zeros(C, C, KS, device=dev)
+dbn, dbw = torch.zeros(C, device=dev), torch.zeros(C, device=dev)
+for R in (56, 64):
+    wg = lambda: _lib.call("pbx_wgrad2", dpn.data_ptr(), dpw.data_ptr(), x.data_ptr(), slab.data_ptr(),  # noqa
+                           bslab.data_ptr(), dwn.data_ptr(), dww.data_ptr(), dbn.data_ptr(), dbw.data_ptr(), B, L, dil,
+                           2, R, st)
+    us = timeit(wg)
+    print(f"[{a.tag}] wgrad2 R={R} {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s (incl. slab fold)", flush=True)
