@@ -6,7 +6,8 @@
 // ProteinBERT/utils.py:293-294 (CE applied to the local probabilities, BCE with log clamp -100,
 // weighted means over B*L and B*A).
 //
-// The [B, G] GEMMs run on hipBLASLt (bf16 in, fp32 out); everything around them is fused here:
+// General-shape path (global dims the one-launch kernels of glob2/glob3.hip are not built for): the [B, G]
+// GEMMs run on the in-tree MFMA GEMM (csrc/gemm.hip, bf16 in, fp32 out); everything around them is fused here:
 //   row_ln_fwd  : z = res + GELU(u + b) [+ scale * sum_t vpart] -> LayerNorm(G)  (one row / workgroup)
 //   row_ln_bwd  : LayerNorm + GELU backward, affine/bias gradients (accumulated in place), the
 //                 attention-scale gradient and the gradient of the attention partial sums

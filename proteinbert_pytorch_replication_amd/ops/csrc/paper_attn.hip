@@ -3,8 +3,9 @@
 // GlobalAttentionHead (modules.py:49-60) was meant to compute.  The reference's own softmax runs
 // over the key axis and collapses to a mean pool (reference semantics live in ln.hip's pool).
 //
-// The K/V projections [B*L, C] x [C, H*(K+VD)] are one plain library GEMM (hipBLASLt) producing
-// the bf16 pre-activations `pre`; everything after it is here:
+// (Split form, PBX_PAPER_ATTN=split: the K/V projections [B*L, C] x [C, H*(K+VD)] are one in-tree MFMA
+// GEMM, csrc/gemm.hip, producing the bf16 pre-activations `pre`; the default fused form computes them
+// inside csrc/paper_fused.hip.)  Everything after the projection is here:
 //
 //   forward   split-L flash-decoding: per (b, h, L-chunk) one workgroup of 4 waves; each wave owns
 //             one position per step (lane k <-> key channel k, lane j <-> value channels 2j, 2j+1),

@@ -1,9 +1,13 @@
 """HIP execution of the whole ProteinBERT forward (+ loss) on MI355X.
 
 Reference forward: ``ProteinBERT/modules.py:295-304``; loss ``ProteinBERT/utils.py:293-294``.
-The local track of every block runs as :class:`.local_track.LocalBlockFn` (fused CDNA4 kernels);
-the embedding gather/scatter is a HIP kernel pair; the global track (``[B, 512]`` vectors, ~0.1 %
-of FLOPs), the 8943-wide GO input/output GEMMs (hipBLASLt) and the heads run as PyTorch ops.
+Every piece runs on in-tree CDNA4 HIP kernels (``csrc/*.hip``), none on library GEMMs:
+the local track of a block is :class:`.local_track.LocalBlockFn` (reference semantics) or
+:class:`.paper_track.PaperBlockFn` (paper semantics); the global track is one fused forward and one
+fused backward launch per block (:class:`.global_track.FusedGlobalBlockFn`, ``csrc/glob3.hip`` /
+``csrc/glob2.hip``); the multi-hot GO input layer is a CSR embedding-bag (``csrc/annot.hip``); the
+embedding is a gather/one-hot-GEMM pair; the heads + loss are ``csrc/lhead.hip`` (reference) /
+``csrc/phead.hip`` (paper) and the fused GO head in ``csrc/gemm.hip``.
 """
 from __future__ import annotations
 

@@ -1,4 +1,4 @@
-"""Paper-semantics global attention on MI355X (``csrc/paper_attn.hip`` + hipBLASLt).
+"""Paper-semantics global attention as a differentiable composition around the split-L HIP core.
 
 The published ProteinBERT attention (one query per head from the global track, softmax over the
 sequence axis, pad-masked) that the reference's ``GlobalAttentionHead`` (``ProteinBERT/modules.py:49-60``)
@@ -7,10 +7,14 @@ which is what ``semantics="reference"`` reproduces.
 
 Split of the work:
 
-* ``q = tanh(g Wq) / sqrt(K)``            tiny ``[B, G] x [G, H*K]`` GEMM, torch;
-* ``pre = h [Wk | Wv]``                    one ``[B*L, C] x [C, H*(K+VD)]`` library GEMM (hipBLASLt);
+* ``q = tanh(g Wq) / sqrt(K)`` and ``pre = h [Wk | Wv]`` are autograd matmuls (this function serves the
+  eager model's ``use_kernel`` path, :meth:`..models.proteinbert.GlobalAttention.forward_paper`);
 * tanh / GELU / scores / masked softmax / P.V, and the whole backward of that chain, are the
-  split-L HIP kernels (:func:`paper_attention_core`); the GEMM backwards go back through hipBLASLt.
+  split-L HIP kernels (:func:`paper_attention_core`).
+
+The training executor does not use this composition: :class:`.paper_track.PaperBlockFn` runs the
+K/V projections inside the fused attention kernels (``csrc/paper_fused.hip``) and every remaining GEMM
+on the in-tree MFMA GEMM (``csrc/gemm.hip``).
 
 The torch oracle is :meth:`...models.proteinbert.GlobalAttention.forward_paper` with ``use_kernel=False``.
 """

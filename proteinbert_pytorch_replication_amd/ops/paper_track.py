@@ -35,6 +35,8 @@ _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _
 _lib.register("pbx_pc_ln_linear_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
                                        _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_pa_fused_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_paper_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_long, _I, _F, _P])
+_lib.register("pbx_paper_head_parts", [ctypes.c_long])
 _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 
 # paper attention form: "fused" (csrc/paper_fused.hip: K/V projections on MFMA inside the attention
@@ -104,7 +106,10 @@ class PaperBlockFn(torch.autograd.Function):
                   bl.data_ptr(), g2.data_ptr(), be2.data_ptr(), h2.data_ptr(), stats.data_ptr(), B, L, LN_EPS, stream)
         # attention: q from the global track, K/V projection as one library GEMM, split-L core
         gf = g.detach().float()
-        q = torch.tanh(torch.einsum("bg,hgk->bhk", gf, Wq.detach().float()))             # [B, H, K]
+        # q = tanh(g Wq): [B, G] x [G, H*K] on the in-tree MFMA GEMM (bf16 operands, fp32 out)
+        wq_cat = Wq.detach().permute(1, 0, 2).reshape(gf.shape[1], -1).to(BF16).contiguous()   # [G, H*K]
+        g_bf = gf.to(BF16)
+        q = torch.tanh(mm32(g_bf, wq_cat)).view(B, H, K)                                 # [B, H, K]
         qs = (q * (1.0 / math.sqrt(K))).contiguous()
         o = torch.empty(B, H * VD, device=dev, dtype=F32)
         lse = torch.empty(B * H, device=dev, dtype=F32)
@@ -121,14 +126,15 @@ class PaperBlockFn(torch.autograd.Function):
         else:
             wcat = torch.cat([Wk.detach().permute(1, 0, 2).reshape(C, H * K),
                               Wv.detach().permute(1, 0, 2).reshape(C, H * VD)], dim=1).to(BF16)   # [C, H*(K+VD)]
-            pre = torch.mm(h2.view(B * L, C), wcat)                                       # [R, N] bf16
+            pre = mm32(h2.view(B * L, C), wcat).to(BF16)                                  # [R, N] bf16
             ns = _nsplit(B, H, L)
             part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
             _lib.call("pbx_paper_attn_fwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), part.data_ptr(),
                       o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
             wsave = wcat
         ctx.fused = fused
-        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wsave, pre, mk, o, lse, h2)
+        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
+                              wq_cat)
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
         ctx.set_materialize_grads(False)
@@ -136,7 +142,8 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, do):
-        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, gf, q, qs, wsave, pre, mk, o, lse, h2) = ctx.saved_tensors
+        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
+         wq_cat) = ctx.saved_tensors
         B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
@@ -168,7 +175,7 @@ class PaperBlockFn(torch.autograd.Function):
                 _lib.call("pbx_paper_attn_bwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), lse.data_ptr(),
                           o.data_ptr(), dO.data_ptr(), dpre.data_ptr(), dq_part.data_ptr(), B, L, H, K, VD, ns,
                           stream)
-                dh2_att = [torch.mm(dpre, wsave.t()), None]                               # [R, C] bf16
+                dh2_att = [mm32(dpre, wsave.t()).to(BF16), None]                          # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
             if PAPER_WGRAD_GEMM:
                 # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
@@ -180,9 +187,11 @@ class PaperBlockFn(torch.autograd.Function):
                                   out_dtype=F32).sum(dim=0)                               # [C, N] fp32
             dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
             dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
-            dqpre = dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)                              # [B, H, K]
-            dWq.add_(torch.einsum("bg,bhk->hgk", gf, dqpre))
-            dg = torch.einsum("bhk,hgk->bg", dqpre, Wq.detach().float())
+            dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K).to(BF16)   # [B, H*K]
+            G = g_bf.shape[1]
+            dwq = mm32(g_bf.t(), dqpre)                                                    # [G, H*K], K = B
+            dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
+            dg = mm32(dqpre, wq_cat.t())                                                   # [B, G]
         ds1 = torch.empty_like(x)
         T = (L + TR - 1) // TR
         dgbp = torch.empty((B, T, CH), dtype=F32, device=dev)
@@ -255,27 +264,31 @@ class PaperHeadsLossFn(torch.autograd.Function):
         V = wo.shape[0]
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
-        hb = h.reshape(B * L, C)
-        logits = torch.addmm(bo.float(), hb, bf16_of(wo).t(), out_dtype=F32)       # [R, V] fp32
-        lse = torch.logsumexp(logits, dim=1)
-        y = y_l.reshape(-1)
-        wl = w_l.reshape(-1).float()
-        nll = lse - logits.gather(1, y.unsqueeze(1)).squeeze(1)
-        inv = 1.0 / float(B * L)
-        loss[0] = (nll * wl).sum() * inv
-        dlog = torch.softmax(logits, dim=1)
-        dlog.scatter_add_(1, y.unsqueeze(1), torch.full_like(wl, -1.0).unsqueeze(1))
-        dlog.mul_((wl * inv).unsqueeze(1))
-        dlog_bf = dlog.to(BF16)
-        # (the [B*L, 26] local-head products stay on the library GEMM: V = 26 is not an MFMA-tile shape)
-        dh = torch.mm(dlog_bf, bf16_of(wo)).view(B, L, C)                             # bf16
+        R = B * L
+        hb = h.reshape(R, C)
+        # one launch (csrc/phead.hip): logits, row softmax over V, weighted NLL, dZ, dh = dZ Wo, bias-gradient
+        # and loss partials; dWo = dZ^T h is the in-tree split-K GEMM over the K = B*L rows
+        parts = _lib.lib().pbx_paper_head_parts(R)
+        dh = torch.empty((B, L, C), dtype=BF16, device=dev)
+        dzl = torch.empty((R, 32), dtype=BF16, device=dev)
+        dbo_part = torch.empty((parts, V), dtype=F32, device=dev)
+        loss_part = torch.empty(parts, dtype=F32, device=dev)
+        y = y_l.reshape(-1).contiguous()
+        wl = w_l.reshape(-1).float().contiguous()
+        _lib.call("pbx_paper_head", hb.data_ptr(), wo.detach().float().contiguous().data_ptr(),
+                  bo.detach().float().contiguous().data_ptr(), y.data_ptr(), wl.data_ptr(), dh.data_ptr(),
+                  dzl.data_ptr(), dbo_part.data_ptr(), loss_part.data_ptr(), R, V, 1.0 / float(R), st)
+        _lib.call("pbx_colsum_add", loss_part.data_ptr(), parts, 1, loss.data_ptr(), None, st)
+        dbo = torch.zeros(V, dtype=F32, device=dev)
+        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), parts, V, dbo.data_ptr(), None, st)
         if PAPER_WGRAD_GEMM:
-            dwo = torch.empty((V, C), dtype=F32, device=dev)
-            _gemm(dlog_bf, hb.reshape(B * L, C), dwo, ta=True, tb=False)                 # K = B*L: split-K
+            dwo32 = torch.empty((32, C), dtype=F32, device=dev)
+            _gemm(dzl, hb, dwo32, ta=True, tb=False)                                        # K = B*L: split-K
+            dwo = dwo32[:V]
         else:
-            nc = _split_k_chunks(B * L)
-            dwo = torch.bmm(dlog_bf.view(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C), out_dtype=F32).sum(dim=0)
-        dbo = dlog.sum(dim=0)
+            nc = _split_k_chunks(R)
+            dwo = torch.bmm(dzl[:, :V].reshape(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C),
+                            out_dtype=F32).sum(dim=0)
         dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
         ctx.save_for_backward(dh, dwo, dbo, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)

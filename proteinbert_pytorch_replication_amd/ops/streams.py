@@ -33,8 +33,8 @@ from typing import Dict, Iterable, List, Optional, Tuple
 import torch
 
 ENABLED = os.environ.get("PBX_AUX_STREAM", "1") != "0"            # conv weight gradient
-# The global-track backward on its own stream measured SLOWER on MI355X (5.2 -> 5.4-5.8 ms/step,
-# paper config): its small hipBLASLt GEMMs take CUs from the critical-path conv data gradient beside
+# The global-track backward on its own stream measured SLOWER on MI355X (round 2, when it still ran on
+# library GEMMs: 5.2 -> 5.4-5.8 ms/step, paper config): its small GEMMs took CUs from the critical-path conv data gradient beside
 # the weight-gradient stream; a high-priority critical-path stream did not recover it.  Round 3, with the
 # one-kernel global backward: still 1 % slower, and 1 % slower again with the global stream at high
 # priority (profiles/r3o_global_stream_prio_ab.txt: it gets CUs only as the data gradient drains).  Off.
