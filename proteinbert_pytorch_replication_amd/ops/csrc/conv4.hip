@@ -320,7 +320,187 @@ __global__ void __launch_bounds__(512, 1) conv_fwd4_kernel(
 }
 
 bool conv4_attr_set = false;
+
+// ------------------------------------------------------------------------------------------------
+// Data gradient, one wave per 32 input channels over BOTH convolutions (reference modules.py:205-206
+// backward):  dx[pos][ci] = ds1[pos][ci] + sum_conv sum_tap sum_co W[co][ci][tap] dpre_conv[pos - shift][co]
+//
+// conv_dgrad3 (conv2.hip) split the two convolutions over two wave groups (8 waves, waves 4-7 = wide)
+// and summed their fp32 partials through a 64 KB LDS tile with two extra barriers before the dx pass.
+// Here each of the 4 waves runs the K loop of both convolutions (2 x 72 K-steps, 4 MFMAs each) into
+// ONE accumulator set, so the cross-wave reduction disappears; the weight-fragment ring (buffer loads,
+// scalar offsets) runs straight from the narrow into the wide image.  dpre = ds1 * GELU'(pre) tiles
+// (GELU' stored by the forward) with their halos are staged once per workgroup; their central rows go
+// to global for the weight gradient.  ~78 KB of LDS: two workgroups (8 waves) per CU.
+__global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
+    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ gdn, const bf16_t* __restrict__ gdw,
+    const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw, bf16_t* __restrict__ dx,
+    bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int dil) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int T = (L + BM - 1) / BM;
+  int tid0;
+  {
+    const int n = gridDim.x, orig = blockIdx.x, xcd = orig & 7, qq = n >> 3, rr = n & 7;
+    tid0 = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (orig >> 3);   // XCD-contiguous tiles
+  }
+  const int b = tid0 / T, t = tid0 - (tid0 / T) * T;
+  const int pos0 = t * BM;
+  const int half = KS >> 1;
+  const int halo_n = half, halo_w = half * dil;
+  const int RN = BM + 2 * halo_n;
+  unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
+  unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
+  const int tid = threadIdx.x, lane = tid & 63, cq = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const size_t sbase = (size_t)b * L * CH;
+  const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16x8*>(ftn + cq * 64), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16x8*>(ftw + cq * 64), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
+  auto wfrag = [&](int it) {      // K-step it of 2 NI: narrow image for it < NI, then the wide one
+    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+    const int li = it < NI ? it : it - NI;
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(it < NI ? rn : rw, lane * 16, li * 4096, 0);
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  bf16x8 fr[4];
+  fr[0] = wfrag(0);
+  fr[1] = wfrag(1);
+  fr[2] = wfrag(2);
+
+  // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
+#pragma unroll 1
+  for (int c = 0; c < 2; ++c) {
+    const int halo = c ? halo_w : halo_n;
+    const bf16_t* gd = c ? gdw : gdn;
+    bf16_t* dpo = c ? dpre_w : dpre_n;
+    unsigned char* tile = c ? aw : an;
+    const int nch = (BM + 2 * halo) * 16;
+    for (int base = tid; base < nch; base += 4 * 256) {
+      uint4 gq[4], pq[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = base + i * 256;
+        const int pos = pos0 - halo + (idx >> 4);
+        const bool ok = idx < nch && pos >= 0 && pos < L;
+        const size_t off = sbase + (size_t)(ok ? pos : 0) * CH + (idx & 15) * 8;
+        gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
+        pq[i] = ok ? *reinterpret_cast<const uint4*>(gd + off) : make_uint4(0u, 0u, 0u, 0u);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = base + i * 256;
+        if (idx >= nch) break;
+        const int j = idx >> 4, ch = idx & 15;
+        const int pos = pos0 - halo + j;
+        float g[8], pv[8], o[8];
+        unpack8(gq[i], g);
+        unpack8(pq[i], pv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = pv[e] * g[e];
+        const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
+        if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
+          *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
+        *reinterpret_cast<uint4*>(tile + swz256(j, ch)) = v;
+      }
+    }
+  }
+  __syncthreads();
+
+  f32x16_t acc[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) acc[i] = zero16();
+  // transposed conv: output row pos reads dpre row pos - (k - half) d, i.e. tile row halo + r - (k - half) d
+  auto rows_of = [&](int c, int k, int& rowb, int& gs) {
+    const int rb = (c ? halo_w : halo_n) + r - (k - half) * (c ? dil : 1);
+    rowb = rb << 8;
+    gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
+  };
+  bf16x8 bq[2][NPT];
+  int rowb, gs;
+  rows_of(0, 0, rowb, gs);
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt) bq[0][pt] = lds_frag(an, (0 ^ gs) + rowb + pt * 8192);
+#pragma unroll 1
+  for (int c = 0; c < 2; ++c) {
+    const unsigned char* as = c ? aw : an;
+    for (int k = 0; k < KS; ++k) {
+      // the step after this tap: next tap of this conv, or the wide conv's first tap
+      const int cn = k + 1 < KS ? c : 1, kn = k + 1 < KS ? k + 1 : 0;
+      const unsigned char* asn = cn ? aw : an;
+      int rowbn, gsn;
+      rows_of(cn, kn, rowbn, gsn);
+#pragma unroll
+      for (int kb = 0; kb < 8; ++kb) {
+        const int it = c * NI + k * 8 + kb;
+        fr[(kb + 3) & 3] = wfrag(min(it + 3, 2 * NI - 1));
+        const unsigned char* nb = kb < 7 ? as : asn;
+        const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) bq[(kb + 1) & 1][pt] = lds_frag(nb, noff + pt * 8192);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], bq[kb & 1][pt], acc[pt]);
+      }
+      rowb = rowbn;
+      gs = gsn;
+    }
+  }
+
+  // dx = ds1 + acc: the fp32 tile goes through LDS (over the dpre tiles) for row-contiguous 16-B accesses
+  const int vrows = min(BM, L - pos0);
+  float* ft = reinterpret_cast<float*>(smem);
+  auto fidx = [&](int p, int c4) { return p * CH + ((c4 ^ (p & 31)) << 2); };
+  __syncthreads();                                // every wave is done reading the dpre tiles
+#pragma unroll
+  for (int pt = 0; pt < NPT; ++pt)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c4 = (cq * 32 + 8 * g + 4 * h) >> 2;
+      *reinterpret_cast<float4*>(ft + fidx(pt * 32 + r, c4)) =
+          make_float4(acc[pt][4 * g], acc[pt][4 * g + 1], acc[pt][4 * g + 2], acc[pt][4 * g + 3]);
+    }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < BM * 16 / 256; ++i) {
+    const int idx = tid + 256 * i;
+    const int row = idx >> 4, cc = idx & 15;
+    if (row >= vrows) continue;
+    const size_t off = sbase + (size_t)(pos0 + row) * CH + cc * 8;
+    float gv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
+    const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * cc));
+    const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * cc + 1));
+    const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
+    *reinterpret_cast<uint4*>(dx + off) = packq8(o);
+  }
+}
+
+bool dgrad4_attr_set = false;
 }  // namespace
+
+int conv_dgrad4_lds(int dil) {
+  const int a = (2 * BM + 8 * (1 + dil)) * 256;
+  return a > BM * CH * 4 ? a : BM * CH * 4;
+}
+
+// Same contract as pbx_conv_dgrad3 (KS = 9): gdn / gdw are the GELU'(pre) images the forward stored.
+PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
+                               void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
+  const int lds = conv_dgrad4_lds(dil);
+  if (KS_ != KS || dil < 1 || lds > 163840 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  if (!dgrad4_attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    dgrad4_attr_set = true;
+  }
+  const int T = (L + BM - 1) / BM;
+  hipLaunchKernelGGL(conv_dgrad4_kernel, dim3(B * T), dim3(256), lds, st, (const bf16_t*)ds1, (const bf16_t*)gdn,
+                     (const bf16_t*)gdw, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n,
+                     (bf16_t*)dpre_w, L, dil);
+  return pbx_launch_status();
+}
 
 int conv_fwd4_lds(int dil) { return 2 * (BM + 8 * dil) * 256 + 2 * BM * 256 + (2 * CH + 16) * 4; }
 

@@ -32,6 +32,7 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_fwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_dgrad4", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
@@ -98,8 +99,14 @@ def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st
               gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, stream)
 
 
+# conv data gradient: 1 (default) = conv_dgrad4 (csrc/conv4.hip: 4 waves, each over both convs into one
+# accumulator set, no cross-wave LDS reduction); 0 = conv_dgrad3 (csrc/conv2.hip)
+CONV_DGRAD4 = int(os.environ.get("PBX_CONV_DGRAD4", "1"))
+
+
 def conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream) -> None:
-    _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+    """``pre_n``/``pre_w``: the GELU'(pre-activation) images :func:`conv_fwd` stored."""
+    _lib.call("pbx_conv_dgrad4" if CONV_DGRAD4 and KS == 9 else "pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
               wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, stream)
 
 

@@ -126,3 +126,39 @@ def test_paper_model_fused_loss_and_grads_vs_torch(L, attn, monkeypatch):
         err = (got[n].float() - m.get_parameter(n).grad.float()).norm().item()
         print(f"{n:60s} |g|={norms[n]:.3e} err={err:.3e}")
         assert err < 6e-2 * norms[n] + 1e-4 * scale, f"{n}: err {err:.3e} vs |g| {norms[n]:.3e}"
+
+
+@pytest.mark.parametrize("B,L", [(8, 512), (3, 77)])
+def test_paper_heads_loss_vs_fp32(B, L):
+    """The one-launch paper local head (csrc/phead.hip: row softmax over V, weighted NLL, dh, dbo, dWo
+    through the in-tree GEMM) + the fused GO head at A = 8943, against plain fp32 PyTorch."""
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.ops.global_track import bf16_of
+    from proteinbert_pytorch_replication_amd.ops.paper_track import PaperHeadsLossFn
+    torch.manual_seed(3)
+    m = ProteinBERT(sequences_length=L, num_annotations=8943, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
+                    num_blocks=1, device="cuda", backend="hip", semantics="paper")
+    _, Y, W = SyntheticUniRefGO(L, 8943, B, "cuda", seed=5).next_batch()
+    h = (torch.randn(B, L, 128, device="cuda") * 0.7).to(torch.bfloat16).requires_grad_(True)
+    g2 = torch.randn(B, 512, device="cuda").requires_grad_(True)
+    lo, go = m.pretraining_local_output[0], m.pretraining_global_output[0]
+    total, parts = PaperHeadsLossFn.apply(h, g2, g2.detach().to(torch.bfloat16), lo.weight, lo.bias, go.weight,
+                                          go.bias, Y["local"], Y["global"], W["local"], W["global"])
+    total.backward()
+    # fp32 oracle of the same math (bf16-rounded inputs, as the kernels see them)
+    hr = h.detach().float().requires_grad_(True)
+    g2r = g2.detach().to(torch.bfloat16).float().requires_grad_(True)
+    wo = lo.weight.detach().clone().requires_grad_(True)
+    bo = lo.bias.detach().clone().requires_grad_(True)
+    logits = hr @ wo.t() + bo
+    nll = F.cross_entropy(logits.reshape(-1, logits.shape[-1]), Y["local"].reshape(-1), reduction="none")
+    ll = (nll * W["local"].reshape(-1).float()).mean()
+    p = torch.sigmoid(g2r @ bf16_of(go.weight).float().t() + go.bias)
+    lg = (F.binary_cross_entropy(p, Y["global"].float(), reduction="none") * W["global"].float()).mean()
+    (ll + lg).backward()
+    torch.cuda.synchronize()
+    assert abs(parts[0].item() - ll.item()) < 2e-3 * abs(ll.item()) + 1e-6
+    assert abs(parts[1].item() - lg.item()) < 2e-3 * abs(lg.item()) + 1e-6
+    assert rel(h.grad, hr.grad) < 2e-2
+    assert rel(lo.weight.grad, wo.grad) < 2e-2
+    assert rel(lo.bias.grad, bo.grad) < 2e-2

@@ -67,6 +67,15 @@ dg = lambda: _lib.call("pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_
                        ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, st)
 us = timeit(dg)
 print(f"[{a.tag}] conv_dgrad3 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+dref = [t.clone() for t in (dx, dpn, dpw)]
+dg4 = lambda: _lib.call("pbx_conv_dgrad4", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
+                        ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, st)
+try:
+    us = timeit(dg4)
+    err = [float((u.float() - v.float()).abs().max()) for u, v in zip(dref, (dx, dpn, dpw))]
+    print(f"[{a.tag}] conv_dgrad4 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s  max|dgrad4 - dgrad3| {err}", flush=True)
+except Exception as ex:
+    print(f"[{a.tag}] conv_dgrad4 unavailable: {ex}")
 slab = torch.empty(64 * 2 * KS * C * C, device=dev)
 bslab = torch.empty(64 * 2 * C, device=dev)
 dwn, dww = torch.zeros(C, C, KS, device=dev), torch.zeros(C, C, KS, device=dev)
