@@ -73,7 +73,7 @@ __global__ void __launch_bounds__(512, 1) conv_fwd4_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gbv,
     bf16_t* __restrict__ gdn, bf16_t* __restrict__ gdw, bf16_t* __restrict__ s1, float* __restrict__ stats,
-    int B, int L, int dil) {
+    int B, int L, int dil, int xlo, int xhi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int half = KS >> 1;
   const int halo = half * dil;
@@ -97,13 +97,13 @@ __global__ void __launch_bounds__(512, 1) conv_fwd4_kernel(
   auto stage_x = [&](long tile, unsigned char* buf) {
     const int b = (int)(tile / T), t = (int)(tile - (tile / T) * T);
     const int pos0 = t * BM;
-    const bf16_t* xs = x + (size_t)b * L * CH;
+    const bf16_t* xs = x + ((size_t)b * (L + xlo + xhi) + xlo) * CH;   // logical position 0
     const int n = XR >> 2;                      // 4 rows (1 KiB) per DMA instruction
     for (int j = w; j < n; j += 8) {
       const int row = 4 * j + (lane >> 4);
       const int chunk = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));   // swz256 image
       const int pos = pos0 - halo + row;
-      const void* src = (pos >= 0 && pos < L) ? (const void*)(xs + (size_t)pos * CH + chunk * 8)
+      const void* src = (pos >= -xlo && pos < L + xhi) ? (const void*)(xs + (ptrdiff_t)pos * CH + chunk * 8)
                                               : (const void*)g_zero16_c4;
       glds16_c4(src, buf + j * 1024);
     }
@@ -162,7 +162,7 @@ __global__ void __launch_bounds__(512, 1) conv_fwd4_kernel(
     e.pn = *reinterpret_cast<const uint4*>(stn + swz256(row, tid & 15));
     e.pw = *reinterpret_cast<const uint4*>(stw + swz256(row, tid & 15));
     const int prow = min(ppos0 + row, L - 1);
-    e.xq = *reinterpret_cast<const uint4*>(x + ((size_t)pb * L + prow) * CH + ch8);
+    e.xq = *reinterpret_cast<const uint4*>(x + ((size_t)pb * (L + xlo + xhi) + xlo + prow) * CH + ch8);
 #pragma unroll
     for (int k = 0; k < 8; ++k) e.s[k] = 0.f;
   };
@@ -335,7 +335,7 @@ bool conv4_attr_set = false;
 __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ gdn, const bf16_t* __restrict__ gdw,
     const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw, bf16_t* __restrict__ dx,
-    bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int dil) {
+    bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int dil, int ilo, int ihi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = (L + BM - 1) / BM;
   int tid0;
@@ -352,7 +352,8 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
   unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
   const int tid = threadIdx.x, lane = tid & 63, cq = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
-  const size_t sbase = (size_t)b * L * CH;
+  const size_t sbase = (size_t)b * L * CH;                          // outputs: [B][L][128]
+  const ptrdiff_t ibase = ((ptrdiff_t)b * (L + ilo + ihi) + ilo) * CH;   // inputs: logical position 0
   const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<bf16x8*>(ftn + cq * 64), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
@@ -382,8 +383,8 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
       for (int i = 0; i < 4; ++i) {
         const int idx = base + i * 256;
         const int pos = pos0 - halo + (idx >> 4);
-        const bool ok = idx < nch && pos >= 0 && pos < L;
-        const size_t off = sbase + (size_t)(ok ? pos : 0) * CH + (idx & 15) * 8;
+        const bool ok = idx < nch && pos >= -ilo && pos < L + ihi;
+        const ptrdiff_t off = ibase + (ptrdiff_t)(ok ? pos : 0) * CH + (idx & 15) * 8;
         gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
         pq[i] = ok ? *reinterpret_cast<const uint4*>(gd + off) : make_uint4(0u, 0u, 0u, 0u);
       }
@@ -398,7 +399,7 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
         unpack8(pq[i], pv);
 #pragma unroll
         for (int e = 0; e < 8; ++e) o[e] = pv[e] * g[e];
-        const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
+        const uint4 v = (pos >= -ilo && pos < L + ihi) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
         if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
           *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
         *reinterpret_cast<uint4*>(tile + swz256(j, ch)) = v;
@@ -468,7 +469,7 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     if (row >= vrows) continue;
     const size_t off = sbase + (size_t)(pos0 + row) * CH + cc * 8;
     float gv[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
+    unpack8(*reinterpret_cast<const uint4*>(ds1 + ibase + (ptrdiff_t)(pos0 + row) * CH + cc * 8), gv);
     const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * cc));
     const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * cc + 1));
     const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
@@ -487,10 +488,13 @@ int conv_dgrad4_lds(int dil) {
 }
 
 // Same contract as pbx_conv_dgrad3 (KS = 9): gdn / gdw are the GELU'(pre) images the forward stored.
-PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
-                               void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
+// ilo / ihi: halo rows of ds1 and GELU' from the neighbouring shards (context parallelism; both inputs
+// [B][ilo + L + ihi][128]); outputs dx, dpre_n, dpre_w are [B][L][128].  0 / 0 for a whole sequence.
+PBX_EXPORT int pbx_conv_dgrad4x(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
+                                void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, int ilo, int ihi,
+                                hipStream_t st) {
   const int lds = conv_dgrad4_lds(dil);
-  if (KS_ != KS || dil < 1 || lds > 163840 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  if (KS_ != KS || dil < 1 || lds > 163840 || B < 1 || L < 1 || ilo < 0 || ihi < 0) return (int)hipErrorInvalidValue;
   if (!dgrad4_attr_set) {
     (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
     dgrad4_attr_set = true;
@@ -498,18 +502,27 @@ PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw
   const int T = (L + BM - 1) / BM;
   hipLaunchKernelGGL(conv_dgrad4_kernel, dim3(B * T), dim3(256), lds, st, (const bf16_t*)ds1, (const bf16_t*)gdn,
                      (const bf16_t*)gdw, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n,
-                     (bf16_t*)dpre_w, L, dil);
+                     (bf16_t*)dpre_w, L, dil, ilo, ihi);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
+                               void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
+  return pbx_conv_dgrad4x(ds1, gdn, gdw, ftn, ftw, dx, dpre_n, dpre_w, B, L, KS_, dil, 0, 0, st);
 }
 
 int conv_fwd4_lds(int dil) { return 2 * (BM + 8 * dil) * 256 + 2 * BM * 256 + (2 * CH + 16) * 4; }
 
 // Same contract as pbx_conv_fwd3 (KS = 9 only); gdn / gdw: GELU'(pre) outputs, or both null.
-PBX_EXPORT int pbx_conv_fwd4(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                             const float* gb, void* gdn, void* gdw, void* s1, float* stats, int B, int L, int KS_,
-                             int dil, hipStream_t st) {
+// xlo / xhi: rows of neighbouring sequence shards stored before / after each sample's L rows of x
+// (context parallelism: x is [B][xlo + L + xhi][128], logical positions -xlo .. L + xhi - 1 are real,
+// anything beyond is the conv's zero padding); 0 / 0 for a whole sequence.
+PBX_EXPORT int pbx_conv_fwd4x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                              const float* gb, void* gdn, void* gdw, void* s1, float* stats, int B, int L, int KS_,
+                              int dil, int xlo, int xhi, hipStream_t st) {
   const int lds = conv_fwd4_lds(dil);
-  if (KS_ != KS || dil < 1 || lds > 163840 || gb == nullptr || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  if (KS_ != KS || dil < 1 || lds > 163840 || gb == nullptr || B < 1 || L < 1 || xlo < 0 || xhi < 0)
+    return (int)hipErrorInvalidValue;
   if ((gdn == nullptr) != (gdw == nullptr)) return (int)hipErrorInvalidValue;
   if (!conv4_attr_set) {
     (void)hipFuncSetAttribute((const void*)conv_fwd4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
@@ -522,6 +535,12 @@ PBX_EXPORT int pbx_conv_fwd4(const void* x, const void* fwn, const void* fww, co
   const int grid = (int)(NT < ncu ? NT : ncu);
   const auto kern = gdn != nullptr ? conv_fwd4_kernel<true> : conv_fwd4_kernel<false>;
   hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn, (const bf16x8*)fww,
-                     bn, bw, gb, (bf16_t*)gdn, (bf16_t*)gdw, (bf16_t*)s1, stats, B, L, dil);
+                     bn, bw, gb, (bf16_t*)gdn, (bf16_t*)gdw, (bf16_t*)s1, stats, B, L, dil, xlo, xhi);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_conv_fwd4(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                             const float* gb, void* gdn, void* gdw, void* s1, float* stats, int B, int L, int KS_,
+                             int dil, hipStream_t st) {
+  return pbx_conv_fwd4x(x, fwn, fww, bn, bw, gb, gdn, gdw, s1, stats, B, L, KS_, dil, 0, 0, st);
 }

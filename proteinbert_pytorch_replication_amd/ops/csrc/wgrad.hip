@@ -111,7 +111,7 @@ __device__ __forceinline__ void wgrad_tiles(unsigned char* smem, int buf_bytes, 
 __global__ void __launch_bounds__(512, 1) wgrad2_kernel(const bf16_t* __restrict__ dy0, const bf16_t* __restrict__ dy1,
                                                         const bf16_t* __restrict__ x, float* __restrict__ slab,
                                                         float* __restrict__ bslab, int B, int L, int dil1,
-                                                        int nconv, int R, int buf_bytes) {
+                                                        int nconv, int R, int buf_bytes, int xlo, int xhi) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int ntypes = nconv * 2;
   int type, chunk;
@@ -158,8 +158,9 @@ __global__ void __launch_bounds__(512, 1) wgrad2_kernel(const bf16_t* __restrict
         const int j = i - 16, row = j * 4 + (lane >> 4);
         const int chunk16 = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
         const int pos = pos0 - halo + row;
-        const void* src = (pos >= 0 && pos < L) ? (const void*)(x + sbase + (size_t)pos * CH + chunk16 * 8)
-                                                : (const void*)g_zero16;
+        const void* src = (pos >= -xlo && pos < L + xhi)
+                              ? (const void*)(x + ((ptrdiff_t)b * (L + xlo + xhi) + xlo + pos) * CH + chunk16 * 8)
+                              : (const void*)g_zero16;
         glds16(src, buf + BM * 128 + j * 1024);
       }
     }
@@ -265,10 +266,11 @@ bool wgrad2_attr_set = false;
 }  // namespace
 
 // KS = 9 only.  slab: R * nconv * 9 * 128 * 128 floats; bslab: R * nconv * 128 floats.
-PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float* slab, float* bslab, float* dw0,
-                          float* dw1, float* db0, float* db1, int B, int L, int dil1, int nconv, int R,
-                          hipStream_t st) {
-  if (nconv < 1 || nconv > 2 || R < 1 || dil1 < 1) return (int)hipErrorInvalidValue;
+// xlo / xhi: x carries neighbouring shards' rows ([B][xlo + L + xhi][128], context parallelism); 0 / 0 otherwise.
+PBX_EXPORT int pbx_wgrad2x(const void* dy0, const void* dy1, const void* x, float* slab, float* bslab, float* dw0,
+                           float* dw1, float* db0, float* db1, int B, int L, int dil1, int nconv, int R, int xlo,
+                           int xhi, hipStream_t st) {
+  if (nconv < 1 || nconv > 2 || R < 1 || dil1 < 1 || xlo < 0 || xhi < 0) return (int)hipErrorInvalidValue;
   const int halo_max = (KS / 2) * (nconv > 1 ? dil1 : 1);
   const int buf = BM * 128 + (BM + 2 * halo_max) * 256;
   if (2 * buf > 163840) return (int)hipErrorInvalidValue;
@@ -277,10 +279,16 @@ PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float
     wgrad2_attr_set = true;
   }
   hipLaunchKernelGGL(wgrad2_kernel, dim3(nconv * 2 * R), dim3(512), 2 * buf, st, (const bf16_t*)dy0,
-                     (const bf16_t*)dy1, (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R, buf);
+                     (const bf16_t*)dy1, (const bf16_t*)x, slab, bslab, B, L, dil1, nconv, R, buf, xlo, xhi);
   const int total4 = nconv * KS * CH * CH / 4;
   const int nblk = (total4 + 63) / 64 + (nconv * CH + 255) / 256;
   hipLaunchKernelGGL(wgrad2_reduce_kernel, dim3(nblk), dim3(256), 0, st, (const float4*)slab,
                      bslab, dw0, dw1, db0, db1, R, nconv);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float* slab, float* bslab, float* dw0,
+                          float* dw1, float* db0, float* db1, int B, int L, int dil1, int nconv, int R,
+                          hipStream_t st) {
+  return pbx_wgrad2x(dy0, dy1, x, slab, bslab, dw0, dw1, db0, db1, B, L, dil1, nconv, R, 0, 0, st);
 }

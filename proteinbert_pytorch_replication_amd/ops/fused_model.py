@@ -46,10 +46,21 @@ def _check(model) -> None:
 
 
 def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
-                 return_bf16: bool = False):
-    """Encoder on the HIP path: returns ``h [B, L, 128]`` (bf16) and ``g [B, G]`` (fp32)."""
+                 return_bf16: bool = False, cp=None):
+    """Encoder on the HIP path: returns ``h [B, L, 128]`` (bf16) and ``g [B, G]`` (fp32).
+
+    ``cp`` (:class:`..parallel.cp_fused.CPShard`): ``tokens`` is this rank's slice of the sequence;
+    the local track runs on the slice (halo rows and LayerNorm statistics exchanged inside the block),
+    the global track is replicated from the group-wide attention-pool sum."""
     _check(model)
-    model.check_length(tokens.shape[1])   # the kernels index the [L, C] LayerNorm affine by position
+    if cp is None:
+        model.check_length(tokens.shape[1])   # the kernels index the [L, C] LayerNorm affine by position
+    else:
+        if model.semantics != "reference":
+            raise NotImplementedError("context parallelism on the fused executor: reference semantics only")
+        model.check_length(cp.L)
+        if tokens.shape[1] != cp.shard_len:
+            raise ValueError(f"expected a {cp.shard_len}-residue shard, got {tokens.shape[1]}")
     blocks = list(model.proteinBERT_blocks)
     lin = model.global_linear_layer[0]
     gl0 = blocks[0].global_to_local_linear_layer[0]
@@ -89,7 +100,9 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:
-            h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0))
+            h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0), cp=cp)
+            if cp is not None:
+                vpart = cp.pool_sum(vpart)      # [B, 1, NJ]: the group-wide sum over every shard's tiles
             wp = att.W_parameter
         nxt = blocks[i + 1].global_to_local_linear_layer[0] if i + 1 < len(blocks) else None
         l1, l2 = blk.global_linear_layer_1[0], blk.global_linear_layer_2[0]
@@ -111,9 +124,13 @@ def fused_forward(model, tokens: torch.Tensor, annotations: torch.Tensor):
 
 
 def fused_pretrain_loss(model, X: Dict[str, torch.Tensor], Y: Dict[str, torch.Tensor], W: Dict[str, torch.Tensor],
-                        return_parts: bool = False):
-    """Reference loss (utils.py:293-294) through the fused heads: one HIP pass per head."""
-    h, g, g_bf = fused_encode(model, X["local"], X["global"], return_bf16=True)
+                        return_parts: bool = False, cp=None):
+    """Reference loss (utils.py:293-294) through the fused heads: one HIP pass per head.  With ``cp`` the
+    local inputs / targets / weights are this rank's slice and the local (CE) term is this rank's share
+    of the group's mean over B * L (see :mod:`..parallel.cp_fused`)."""
+    h, g, g_bf = fused_encode(model, X["local"], X["global"], return_bf16=True, cp=cp)
+    if cp is not None:
+        W = dict(W, local=W["local"].float() * (cp.shard_len / cp.L))
     lo, go = model.pretraining_local_output[0], model.pretraining_global_output[0]
     fn = PaperHeadsLossFn if model.semantics == "paper" else HeadsLossFn
     total, parts = fn.apply(h, g, g_bf, lo.weight, lo.bias, go.weight, go.bias, Y["local"], Y["global"],

@@ -33,6 +33,9 @@ _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_fwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd4x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_dgrad4x", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
@@ -93,8 +96,15 @@ def _p(t: Optional[torch.Tensor]):
 CONV_FWD4 = int(os.environ.get("PBX_CONV_FWD4", "1"))
 
 
-def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream) -> None:
-    """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward)."""
+def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream, xlo: int = 0,
+             xhi: int = 0) -> None:
+    """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward).
+    ``xlo``/``xhi``: rows of the neighbouring sequence shards around each sample's L rows of ``x``
+    (context parallelism, :mod:`..parallel.cp_fused`)."""
+    if xlo or xhi:
+        _lib.call("pbx_conv_fwd4x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                  gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, xlo, xhi, stream)
+        return
     _lib.call("pbx_conv_fwd4" if CONV_FWD4 and KS == 9 else "pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
               gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, stream)
 
@@ -104,8 +114,13 @@ def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st
 CONV_DGRAD4 = int(os.environ.get("PBX_CONV_DGRAD4", "1"))
 
 
-def conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream) -> None:
-    """``pre_n``/``pre_w``: the GELU'(pre-activation) images :func:`conv_fwd` stored."""
+def conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream, ilo: int = 0, ihi: int = 0) -> None:
+    """``pre_n``/``pre_w``: the GELU'(pre-activation) images :func:`conv_fwd` stored; ``ilo``/``ihi``:
+    neighbouring shards' rows around ``ds1`` / GELU' (context parallelism)."""
+    if ilo or ihi:
+        _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, ilo, ihi, stream)
+        return
     _lib.call("pbx_conv_dgrad4" if CONV_DGRAD4 and KS == 9 else "pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
               wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, stream)
 
@@ -163,7 +178,7 @@ INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
 
 
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
-           B: int, L: int, outs, full_chip: bool = False):
+           B: int, L: int, outs, full_chip: bool = False, xlo: int = 0, xhi: int = 0):
     """outs: [(dw, db)] destinations (accumulated into).  Returns the scratch tensors (the caller keeps
     them alive while the launch may still be running on another stream)."""
     dev = x.device
@@ -181,8 +196,12 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     bslab = torch.empty((R, nconv, CH), dtype=torch.float32, device=dev)
     (dw0, db0) = outs[0]
     (dw1, db1) = outs[1] if nconv > 1 else (None, None)
-    _lib.call("pbx_wgrad2", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
-              dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, dil, nconv, R, _lib.stream_ptr(dev))
+    if xlo or xhi:
+        _lib.call("pbx_wgrad2x", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
+                  dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, dil, nconv, R, xlo, xhi, _lib.stream_ptr(dev))
+    else:
+        _lib.call("pbx_wgrad2", dy0.data_ptr(), _p(dy1), x.data_ptr(), slab.data_ptr(), bslab.data_ptr(),
+                  dw0.data_ptr(), _p(dw1), db0.data_ptr(), _p(db1), B, L, dil, nconv, R, _lib.stream_ptr(dev))
     return [slab, bslab]
 
 
@@ -191,10 +210,16 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None,
-                tail: bool = False):
+                tail: bool = False, cp=None):
         """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch);
-        ``tail``: the first block (its backward ends the step: the conv weight gradient gets every CU)."""
+        ``tail``: the first block (its backward ends the step: the conv weight gradient gets every CU);
+        ``cp``: a :class:`..parallel.cp_fused.CPShard` -- ``x`` is this rank's slice of the sequence, the
+        conv reads the neighbours' halo rows and the (L, C) LayerNorm statistics are group-wide."""
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
+        ctx.cp = cp
+        if cp is not None:
+            # this shard's rows of the [L, C] LayerNorm affine (contiguous row slices of the parameters)
+            g1, be1, g2, be2 = (cp.rows(t) for t in (g1, be1, g2, be2))
         B, L, C = x.shape
         assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
         NJ = wv_bf16.shape[0]
@@ -219,12 +244,20 @@ class LocalBlockFn(torch.autograd.Function):
         s1 = torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
         gb = gb.detach().float().contiguous()
-        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream)
+        if cp is None:
+            x_ext, hlo = x, 0
+            conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream)
+        else:
+            x_ext, hlo = cp.halo_rows(x), cp.halo
+            conv_fwd(x_ext, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream, hlo, hlo)
+            cp.fix_stats(st1, BM1)
         pre_l = torch.empty_like(x) if need_bwd else None
         s2 = torch.empty_like(x)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_linear_fwd", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
                   wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS, stream)
+        if cp is not None:
+            cp.fix_stats(st2, PB)
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(x)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
@@ -243,8 +276,9 @@ class LocalBlockFn(torch.autograd.Function):
                       wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
         # the pool backward's operand: the GELU' fragments, or the block output rows h2 it recomputes them from
         ctx.recompute = recompute
-        ctx.save_for_backward(x, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw, wl_b,
-                              wv_bf16, g1, be1, g2)
+        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw,
+                              wl_b, wv_bf16, g1, be1, g2)
+        ctx.hlo = hlo
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
         ctx.tail = bool(tail) and WGRAD_TAIL_FULL
         ctx.set_materialize_grads(False)
@@ -254,13 +288,18 @@ class LocalBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh2, dvpart):
         streams.wait_ready(dvpart)           # produced by the global-track backward on its aux stream
-        (x, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        cp, hlo = ctx.cp, ctx.hlo
+        x = s1                                  # shape / dtype / device template of the [B, L, C] activations
         B, L, KS, dil, T1, T2, NJ = ctx.meta
         dev = x.device
         stream = _lib.stream_ptr(dev)
         params = ctx.params
         dsts = [_grad_dst(p, p.shape) for p in params]
         (dwn, _), (dbn, _), (dww, _), (dbw, _), (dg1, _), (dbe1, _), (dwl, _), (dbl, _), (dg2, _), (dbe2, _) = dsts
+        if cp is not None:
+            # this shard's rows of the [L, C] affine gradients (the kernels accumulate into them)
+            dg1, dbe1, dg2, dbe2 = (cp.rows(t) for t in (dg1, dbe1, dg2, dbe2))
         dh2 = None if dh2 is None else dh2.to(torch.bfloat16).contiguous()
         BMV = 64                                # positions per forward vpart row
         TV = (L + BMV - 1) // BMV
@@ -278,6 +317,9 @@ class LocalBlockFn(torch.autograd.Function):
         if bwd4:
             TA *= 4                              # attn_bwd4: one partial per (tile, wave)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
+        if cp is not None:
+            # CP: the global track is replicated, so dvpart is already the gradient of the group-wide pool sum
+            pass
         if bwd4:
             _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
@@ -290,6 +332,8 @@ class LocalBlockFn(torch.autograd.Function):
             _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
                       stream)
+        if cp is not None:
+            cp.fix_sums(sums2)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
         dh1 = torch.empty_like(x)
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)
@@ -321,11 +365,15 @@ class LocalBlockFn(torch.autograd.Function):
         dx = torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
+        if cp is not None:
+            cp.fix_sums(sums1)
         # LN1 finalize (ds1) + gradient of the broadcast global->local vector
         ds1 = torch.empty_like(x)
         _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
                   TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, int(fused_deterministic()),
                   stream)
+        if cp is not None:
+            cp.all_reduce_(dgb)                 # gb is replicated: its gradient sums every shard's positions
         if streams.GLOBAL_ENABLED:
             # the previous block's global-track backward (next autograd node, aux stream) needs only
             # dgb: let it start here, beside the conv data gradient below
@@ -336,19 +384,25 @@ class LocalBlockFn(torch.autograd.Function):
             # data gradient, so its 18 MB weight-gradient bucket is ready ~0.2 ms earlier for the DP
             # all-reduce (ops/global_track.py InputLayerFn.backward)
             streams.fork(dev, "ann")
-        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
+        if cp is None:
+            conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
+        else:
+            # the transposed conv reads dpre = ds1 GELU' of the neighbours' edge rows too
+            conv_dgrad(cp.halo_rows(ds1), cp.halo_rows(pre_n), cp.halo_rows(pre_w), wtn, wtw, dx, dpn, dpw, B, L,
+                       KS, dil, stream, hlo, hlo)
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
-            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], ctx.tail),
-                           keep=[dpn, dpw, x], name="wgrad")
+            streams.launch(dev, lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], ctx.tail,
+                                               hlo, hlo),
+                           keep=[dpn, dpw, x_ext], name="wgrad")
         else:
-            _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
+            _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], False, hlo, hlo)
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None, None, None)
+        return (dx, dgb, *pgrads, None, None, None, None, None)
 
 
 class EmbedFn(torch.autograd.Function):
@@ -417,8 +471,10 @@ def conv_images(wn: torch.Tensor, ww: torch.Tensor):
     return imgs, [(0, wn.detach(), imgs[0], imgs[1], KS, 0), (0, ww.detach(), imgs[2], imgs[3], KS, 0)]
 
 
-def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``); ``tail``: it is the first block."""
+def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool = False,
+                cp=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``); ``tail``: it is the first block;
+    ``cp``: context-parallel shard (:class:`..parallel.cp_fused.CPShard`)."""
     att = blk.global_attention_layer
     wv = _wv_bf16(att)                                                       # [H*vd, C]
     nc = blk.local_narrow_conv_layer[0]
@@ -426,4 +482,4 @@ def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool 
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
                               blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed,
-                              tail)
+                              tail, cp)

@@ -22,7 +22,8 @@ owners), so ``sum_r loss_r`` is the single-device loss and summing parameter gra
 CP group gives its exact gradient: :func:`cp_pretrain_loss` weights the replicated GO term by
 1/P for that reason, and :func:`all_reduce_grads` does the sum.
 
-CP runs the PyTorch op path (any dtype/device); the fused HIP executor is single-shard.
+CP here runs the PyTorch op path (any dtype / device, paper semantics included); reference semantics on
+the fused HIP executor is :mod:`.cp_fused` (the same collectives around the CDNA4 kernels).
 Combine with data parallelism through :func:`make_cp_groups` (ranks ``[i*P, (i+1)*P)`` share
 one batch; strided ranks form the DP groups).
 """
