@@ -164,6 +164,7 @@ def main():
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
                           "impl": a.impl, "hip_graph": graphed},
                "world_size": n, "backend": info.backend if n > 1 else "single",
+               "rccl_env": getattr(info, "rccl_env", None),
                "device": _device_label(dev), "final_loss": round(final_loss, 5)}
         if dev.type != "cuda" and a.preset == "cfg1_cpu_smoke":
             # BASELINE cfg 1 is a CPU config: compare with the reference step measured on a CPU

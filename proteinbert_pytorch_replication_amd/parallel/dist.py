@@ -26,6 +26,7 @@ class DistInfo:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    rccl_env: Optional[dict] = None       # the RCCL settings rccl_node_defaults applied (None: none)
 
     @property
     def is_main(self) -> bool:
@@ -60,6 +61,8 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
     if info.world_size > 1:
         if backend == "auto":
             backend = "nccl" if use_gpu else "gloo"
+        if backend == "nccl":
+            info.rccl_env = rccl_node_defaults(info.world_size)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
@@ -73,6 +76,34 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
         info.backend = backend
     _INFO = info
     return info
+
+
+# RCCL defaults for one 8 x MI355X node.  The node's xGMI is a fully connected K8: 7 point-to-
+# point links of ~153 GB/s per GPU.  One ring all-reduce is bound by ONE link per direction (2 (7/8) 67 MB /
+# 153 GB/s = 0.77 ms for the 67 MB gradient payload); K8 decomposes into 3 edge-disjoint Hamiltonian
+# cycles + a perfect matching, i.e. up to 6 link-disjoint directed rings, so the all-reduce needs >= 6
+# channels, with a margin for RCCL's per-channel protocol overhead.  These are DEFAULTS: every variable the
+# launch environment already sets wins, and PBX_RCCL_DEFAULTS=0 applies none.
+RCCL_NODE_DEFAULTS = {
+    "NCCL_MIN_NCHANNELS": "16",        # >= 6 directed rings over the K8 links (RCCL may still use more)
+    "HSA_NO_SCRATCH_RECLAIM": "1",     # keep RCCL kernels' scratch resident (no reclaim stalls per call)
+    "TORCH_NCCL_ASYNC_ERROR_HANDLING": "1",   # a failed / hung collective aborts the job (watchdog)
+}
+
+
+def rccl_node_defaults(world_size: int) -> Optional[dict]:
+    """Apply :data:`RCCL_NODE_DEFAULTS` for a single-node multi-GPU job (one process per GPU); returns
+    what was set.  Multi-node jobs (LOCAL_WORLD_SIZE < WORLD_SIZE) keep RCCL's own topology tuning."""
+    if os.environ.get("PBX_RCCL_DEFAULTS", "1") == "0" or world_size < 2:
+        return None
+    if int(os.environ.get("LOCAL_WORLD_SIZE", world_size)) != world_size:
+        return None
+    applied = {}
+    for k, v in RCCL_NODE_DEFAULTS.items():
+        if k not in os.environ:
+            os.environ[k] = v
+            applied[k] = v
+    return applied
 
 
 def nccl_pg_options():

@@ -226,3 +226,21 @@ def test_bucketer_counts_each_parameter_once():
         assert ddp._pending == ddp.bucket_nparams and not any(ddp._ready)
     finally:
         dist.destroy_process_group()
+
+
+def test_rccl_node_defaults_respect_environment(monkeypatch):
+    """single-node RCCL defaults are applied only where the environment is silent, never on
+    multi-node jobs, and not at all with PBX_RCCL_DEFAULTS=0."""
+    from proteinbert_pytorch_replication_amd.parallel import dist as pdist
+    for k in pdist.RCCL_NODE_DEFAULTS:
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("NCCL_MIN_NCHANNELS", "32")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    applied = pdist.rccl_node_defaults(8)
+    assert os.environ["NCCL_MIN_NCHANNELS"] == "32" and "NCCL_MIN_NCHANNELS" not in applied
+    assert os.environ["HSA_NO_SCRATCH_RECLAIM"] == "1"
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert pdist.rccl_node_defaults(8) is None                 # two nodes
+    monkeypatch.setenv("PBX_RCCL_DEFAULTS", "0")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert pdist.rccl_node_defaults(8) is None
