@@ -76,3 +76,13 @@ PBX_EXPORT int pbx_pack_batch(const void* const* ptrs, const int* meta, int coun
   hipLaunchKernelGGL(pack_batch_kernel, dim3(gx, count), dim3(256), 0, st, pb);
   return pbx_launch_status();
 }
+
+// An empty one-wave kernel: the graph-capture ordering marker of ops/streams.py (a main-stream node
+// captured between a fork point and the aux-stream body, so the main chain stays the fork point's
+// first child and hipGraph's stream assignment keeps it on one queue).
+__global__ void __launch_bounds__(64) noop_kernel() {}
+
+PBX_EXPORT int pbx_noop(hipStream_t st) {
+  hipLaunchKernelGGL(noop_kernel, dim3(1), dim3(64), 0, st);
+  return pbx_launch_status();
+}

@@ -366,6 +366,7 @@ def glob_fused_ok(G: int, NGL: int) -> bool:
 
 
 _lib.register("pbx_pack_batch", [_P, _P, _I, _P])
+_lib.register("pbx_noop", [_P])
 
 
 def pack_batch(items) -> None:

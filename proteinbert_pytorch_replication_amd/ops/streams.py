@@ -93,6 +93,12 @@ _forked: Dict[Tuple[int, str], bool] = {}
 
 
 _events: Dict[Tuple[int, int], torch.cuda.Event] = {}
+# Under hipGraph capture a fork whose aux body starts at the main stream's current tail makes that tail
+# node have two children, and the graph executor continues a node's queue with its FIRST child in
+# capture order -- the aux body (e.g. the conv weight gradient) would take the main chain's queue and
+# the critical path would wait behind it.  PBX_GRAPH_MARKER=1 (default) captures an empty main-stream
+# kernel before the aux body so the main chain is the first child (tests/test_graph_step.py).
+GRAPH_MARKER = os.environ.get("PBX_GRAPH_MARKER", "1") != "0"
 # PBX_STREAM_FAST=0: per-call wait_stream events and the torch.cuda.stream context (A/B of the host cost)
 _FAST = os.environ.get("PBX_STREAM_FAST", "1") != "0"
 
@@ -138,6 +144,9 @@ def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
     aux = _aux(device, name)
     if not _forked.pop((idx, name), False):
         _wait(aux, main)
+        if GRAPH_MARKER and torch.cuda.is_current_stream_capturing():
+            from . import _lib
+            _lib.call("pbx_noop", main.cuda_stream)
     scope = _AuxScope(idx)
     scope.keep(*keep)
     _used.setdefault(idx, set()).add(name)
