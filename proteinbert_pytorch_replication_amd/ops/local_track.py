@@ -172,6 +172,11 @@ WGRAD_TAIL_FULL = os.environ.get("PBX_WGRAD_TAIL_FULL", "1") != "0"
 # the local-MLP dWl / dbl slab folds run on the weight-gradient stream (PBX_LN2_LATE_FOLD=0: on the main
 # stream right after the LN2 / MLP backward kernel)
 LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
+# the conv data gradient of blocks 1.. runs on its own aux stream ("dg"), so the previous block's
+# global-track backward -- next on the main stream, needed by that block's pool backward -- is dispatched
+# first and runs beside it on the CUs it takes (PBX_DGRAD_STREAM=0: data gradient on the main stream,
+# the global backward after it)
+DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "1") != "0"
 # the input layer's backward starts beside the first block's conv data gradient (PBX_INPUT_BWD_EARLY=0:
 # on the main stream after it)
 INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
@@ -287,7 +292,9 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, dvpart):
-        streams.wait_ready(dvpart)           # produced by the global-track backward on its aux stream
+        # dvpart: produced by the global-track backward on its aux stream (PBX_GLOBAL_STREAM=1); dh2: by
+        # the next block's conv data gradient on the "dg" stream
+        streams.wait_ready(dvpart, dh2)
         (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
         cp, hlo = ctx.cp, ctx.hlo
         x = s1                                  # shape / dtype / device template of the [B, L, C] activations
@@ -384,7 +391,15 @@ class LocalBlockFn(torch.autograd.Function):
             # data gradient, so its 18 MB weight-gradient bucket is ready ~0.2 ms earlier for the DP
             # all-reduce (ops/global_track.py InputLayerFn.backward)
             streams.fork(dev, "ann")
-        if cp is None:
+        dg_aux = (DGRAD_STREAM and cp is None and not ctx.tail and streams.ENABLED and not streams.GLOBAL_ENABLED
+                  and dev.type == "cuda")
+        if dg_aux:
+            streams.launch(dev, lambda: conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil,
+                                                   _lib.stream_ptr(dev)),
+                           keep=[ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw], name="dg")
+            streams.mark_ready(dev, "dg", [dx])
+            streams.chain(dev, "wgrad", "dg")   # the weight gradient reads dpre_n / dpre_w
+        elif cp is None:
             conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
         else:
             # the transposed conv reads dpre = ds1 GELU' of the neighbours' edge rows too

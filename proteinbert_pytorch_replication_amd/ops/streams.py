@@ -4,6 +4,9 @@ Two pieces of one block's backward do not feed the critical path directly:
 
 * ``wgrad``  - the conv weight gradient (``pbx_wgrad`` + slab reduction, ~1 ms of a 5 ms
   paper-config step): only the optimizer and the DP all-reduce read it;
+* ``dg``     - the conv data gradient of blocks 1.. (ops/local_track.py DGRAD_STREAM): the previous
+  block's global-track backward, next on the main stream, is dispatched beside it instead of after it;
+  the next local-block backward waits for its ``dx`` (:func:`wait_ready`);
 * ``global`` - the global-track backward of the previous block (~0.1 ms of small GEMMs and row
   LayerNorms per block): its outputs are consumed by the NEXT local-block backward, so it can run
   beside this block's conv data gradient instead of after it (opt-in, see GLOBAL_ENABLED).
@@ -179,6 +182,12 @@ def mark_ready(device: torch.device, name: str, tensors: Iterable[torch.Tensor])
     for t in tensors:
         if isinstance(t, torch.Tensor):
             _ready[t.data_ptr()] = (_idx(device), name)
+
+
+def chain(device: torch.device, dst: str, src: str) -> None:
+    """Aux stream ``dst`` waits for the work enqueued on aux stream ``src`` so far."""
+    _wait(_aux(device, dst), _aux(device, src))
+    _used.setdefault(_idx(device), set()).add(dst)
 
 
 def wait_for(device: torch.device, name: str) -> None:
