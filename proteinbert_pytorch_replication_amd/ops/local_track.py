@@ -172,11 +172,11 @@ WGRAD_TAIL_FULL = os.environ.get("PBX_WGRAD_TAIL_FULL", "1") != "0"
 # the local-MLP dWl / dbl slab folds run on the weight-gradient stream (PBX_LN2_LATE_FOLD=0: on the main
 # stream right after the LN2 / MLP backward kernel)
 LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
-# the conv data gradient of blocks 1.. runs on its own aux stream ("dg"), so the previous block's
-# global-track backward -- next on the main stream, needed by that block's pool backward -- is dispatched
-# first and runs beside it on the CUs it takes (PBX_DGRAD_STREAM=0: data gradient on the main stream,
-# the global backward after it)
-DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "1") != "0"
+# PBX_DGRAD_STREAM=1: the conv data gradient of blocks 1.. on its own aux stream ("dg") so the previous
+# block's global-track backward (next on the main stream) runs beside it.  Measured 1.9 % SLOWER
+# (profiles/r4_dgrad_stream_ab.txt): the one-launch global backward (8-wave workgroups) only finds CUs as
+# conv_dgrad4's 2-per-CU workgroups drain and stretches from 51 to ~210 us.  Off.
+DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "0") == "1"
 # the input layer's backward starts beside the first block's conv data gradient (PBX_INPUT_BWD_EARLY=0:
 # on the main stream after it)
 INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
