@@ -91,9 +91,10 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
-# conv forward: 1 (default) = persistent conv_fwd4 (csrc/conv4.hip: the epilogue of tile i-1 runs inside the
-# K loop of tile i); 0 = conv_fwd3 (csrc/conv2.hip, epilogue after each tile's MFMAs)
-CONV_FWD4 = int(os.environ.get("PBX_CONV_FWD4", "1"))
+# conv forward: 0 (default) = conv_fwd3 (csrc/conv2.hip, epilogue after each tile's MFMAs); 1 = persistent
+# conv_fwd4 (csrc/conv4.hip: the epilogue of tile i-1 runs inside the K loop of tile i).  Equal in
+# isolation (197.5 vs 198.9 us, profiles/r4_conv_ab.txt) but 3.3 % slower in the step (76.0k vs 78.7k seq/s)
+CONV_FWD4 = int(os.environ.get("PBX_CONV_FWD4", "0"))
 
 
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream, xlo: int = 0,

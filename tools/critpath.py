@@ -34,3 +34,7 @@ for r in rs:
     s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
     ov = [x['Kernel_Name'][:28] for x in aux if int(x['Start_Timestamp']) < e and int(x['End_Timestamp']) > s]
     print(f"  {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {r['Kernel_Name'][:45]:45s} | {', '.join(sorted(set(ov)))[:90]}")
+print("aux-queue kernels in order (queue, start us, duration us):")
+for r in sorted(aux, key=lambda x: int(x['Start_Timestamp'])):
+    s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
+    print(f"  q{r['Queue_Id']:>3s} {(s - t0) / 1e3:8.1f} {(e - s) / 1e3:7.1f}  {r['Kernel_Name'][:60]}")
