@@ -185,7 +185,11 @@ class BucketedAllReduce:
             self._tmp[b] = None
 
     def _launch_ready(self) -> None:
-        while self._next < len(self.buckets) and self._pending[self._next] <= 0:
+        # overlapped optimizer step: the LAST bucket stays for finish_and_step, so the group-wide
+        # non-finite flag's all-reduce is queued ahead of it and the update of buckets 0..n-2 runs
+        # beside the last (largest: embedding + input layer) all-reduce instead of after it
+        end = len(self.buckets) - (1 if self.track_nonfinite and len(self.buckets) > 1 else 0)
+        while self._next < end and self._pending[self._next] <= 0:
             self._launch(self._next)
             self._next += 1
 
@@ -238,7 +242,8 @@ class BucketedAllReduce:
         opt.step_range(0, split)              # beside the tail buckets' all-reduce
         for b in range(split_b, len(self.buckets)):
             self._land(b)
-        opt.step_range(split, self.arena.numel)
+        if split < self.arena.numel:
+            opt.step_range(split, self.arena.numel)
         self.track_nonfinite = False
         self._flag_work = None
         self.start_step()

@@ -91,10 +91,15 @@ def run(a):
             total = t0.elapsed_time(t1)
             print(f"step {total:.3f} ms, {len(ddp.buckets)} buckets of <= {a.bucket_mb:g} MB, loss {float(loss):.4f}")
             bwd_end = next(t0.elapsed_time(ev) for ev, n in marks if n < 0)
-            for k, (ev, n) in enumerate(x for x in marks if x[1] >= 0):
+            k = 0
+            for ev, n in (x for x in marks if x[1] >= 0):
                 t = t0.elapsed_time(ev)
+                if n <= 8:      # the 4-byte group-wide non-finite flag (MAX), queued ahead of the last bucket
+                    print(f"  non-finite flag (MAX all-reduce) enqueued at {t:7.3f} ms")
+                    continue
                 print(f"  bucket {k:2d}  {n / 2**20:6.2f} MB  gradients final at {t:7.3f} ms"
                       f"  ({'inside backward' if t < bwd_end - 1e-3 else 'after backward'})")
+                k += 1
             print(f"  backward (+ aux streams) ends at {bwd_end:.3f} ms; Adam ends at {total:.3f} ms")
             last_ar = t0.elapsed_time([ev for ev, n in marks if n >= 0][-1])
             for e_a, e_b, n in ranges:
