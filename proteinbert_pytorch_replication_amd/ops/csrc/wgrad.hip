@@ -292,3 +292,171 @@ PBX_EXPORT int pbx_wgrad2(const void* dy0, const void* dy1, const void* x, float
                           hipStream_t st) {
   return pbx_wgrad2x(dy0, dy1, x, slab, bslab, dw0, dw1, db0, db1, B, L, dil1, nconv, R, 0, 0, st);
 }
+
+// ------------------------------------------------------------------------------------------------
+// Weight gradient of the first block's convolutions, whose input is the token embedding
+// x[pos] = bf16(E[tok[pos]]) (reference modules.py:249-253,300 feeding :185-199): through the token
+// one-hot instead of the 128 input channels,
+//   dW[co][ci][k] = sum_pos dpre[pos][co] x[pos + s_k][ci] = sum_v bf16(E[v][ci]) S_k[v][co],
+//   S_k[v][co]    = sum_{src : tok[src] = v} dpre[src - s_k][co]      (s_k = (k - 4) d; zero padding)
+// S is a one-hot GEMM (M = 32 token rows, K = source positions, N = 128 channels: a quarter of the
+// 128-input-channel product's MFMA work, the embed_bwd pattern of ln.hip with 9 shifted B operands per
+// K-step), E^T S is 2 x 9 x 128 x 128 x V.  Same fp32-accumulated sums as wgrad2, in another order;
+// deterministic (per-workgroup slab, fixed-order fold).  Replaces the step's exposed tail (the first
+// block's wgrad2 runs after every other backward kernel).
+namespace {
+constexpr int TBM = 128;   // source positions per tile
+
+// Workgroup: 8 waves, wave w = (conv w >> 2, 32-channel tile w & 3), 9 tap accumulators each.
+// LDS buffer (double-buffered, DMA-staged): narrow dpre rows [TBM + 8][256 B] | wide dpre rows
+// [TBM + 8 d][256 B] (swz256) | the tile's tokens (int64, one 1-KiB DMA)
+__global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __restrict__ tok,
+                                                           const bf16_t* __restrict__ dy0,
+                                                           const bf16_t* __restrict__ dy1, float* __restrict__ slab,
+                                                           int B, int L, int dil1, int R, int V, int buf_bytes) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, h = lane >> 5;
+  const int q = tr_q(lane), tc = tr_c(lane);
+  const int cv = w >> 2, ct = w & 3;
+  const int d = cv ? dil1 : 1;
+  const int hal0 = KS / 2, hal1 = (KS / 2) * dil1;
+  const int rows0 = TBM + 2 * hal0, rows1 = TBM + 2 * hal1;
+  const int T = (L + TBM - 1) / TBM;
+  const long NT = (long)B * T;
+  const long t0 = NT * blockIdx.x / R, t1 = NT * (blockIdx.x + 1) / R;
+
+  auto stage = [&](long tile, unsigned char* buf) {
+    const int b = (int)(tile / T), t = (int)(tile - (tile / T) * T);
+    const int pos0 = t * TBM;
+    const size_t sbase = (size_t)b * L * CH;
+    const int n0 = rows0 / 4, n1 = rows1 / 4;
+    for (int i = w; i <= n0 + n1; i += 8) {
+      if (i == n0 + n1) {                      // tokens pos0 .. pos0 + 127: 2 per lane (L even)
+        const int p = pos0 + 2 * lane;
+        const void* src = p < L ? (const void*)(tok + (size_t)b * L + p) : (const void*)g_zero16;
+        glds16(src, buf + (rows0 + rows1) * 256);
+        continue;
+      }
+      const int c = i >= n0;
+      const int j = c ? i - n0 : i;
+      const int hal = c ? hal1 : hal0;
+      const bf16_t* dy = c ? dy1 : dy0;
+      const int row = j * 4 + (lane >> 4);
+      const int chunk16 = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+      const int pos = pos0 - hal + row;
+      const void* src = (pos >= 0 && pos < L) ? (const void*)(dy + sbase + (size_t)pos * CH + chunk16 * 8)
+                                              : (const void*)g_zero16;
+      glds16(src, buf + (c ? rows0 * 256 : 0) + j * 1024);
+    }
+  };
+
+  f32x16_t acc[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) acc[k] = zero16();
+  const int hal = cv ? hal1 : hal0;
+  const int colb = ct * 32 + tc;
+  if (t0 < t1) stage(t0, smem);
+  for (long tile = t0; tile < t1; ++tile) {
+    unsigned char* cur = smem + ((tile - t0) & 1) * buf_bytes;
+    unsigned char* nxt = smem + (((tile - t0) & 1) ^ 1) * buf_bytes;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of `cur` landed
+    __syncthreads();                                   // ... every wave's; `nxt` no longer read
+    if (tile + 1 < t1) stage(tile + 1, nxt);
+    const int pos0 = (int)(tile - (tile / T) * T) * TBM;
+    const unsigned char* base = cur + (cv ? rows0 * 256 : 0);
+    const long long* ts = reinterpret_cast<const long long*>(cur + (rows0 + rows1) * 256);
+#pragma unroll 2
+    for (int kb = 0; kb < TBM / 16; ++kb) {
+      // A[i = v][k = src]: lane's token row v = r, sources kb*16 + 8h + j
+      typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
+      u16x8 oh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int s = kb * 16 + 8 * h + j;
+        oh[j] = (pos0 + s < L && (int)ts[s] == r) ? (unsigned short)0x3F80 : (unsigned short)0;
+      }
+      const bf16x8 a = __builtin_bit_cast(bf16x8, oh);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        // B[k = src][col = co] = dpre[src - s_k][co]: tile row hal + (4 - k) d + kb*16 + 8h + j
+        const int rb = hal + (KS / 2 - k) * d + kb * 16 + 8 * h + q;
+        const bf16x8 fb = cat_tr(lds_tr(base, swz256e(rb, colb)), lds_tr(base, swz256e(rb + 4, colb)));
+        acc[k] = mfma32(a, fb, acc[k]);
+      }
+    }
+  }
+  // slab [R][2][KS][V][128]: D row = token v, column = channel
+#pragma unroll
+  for (int k = 0; k < KS; ++k)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int v = (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (v < V) slab[((((size_t)blockIdx.x * 2 + cv) * KS + k) * V + v) * CH + ct * 32 + r] = acc[k][i];
+    }
+}
+
+// dW_c[co][ci][k] += sum_v bf16(E[v][ci]) S[c][k][v][co] ; db_c[co] += sum_v S[c][4][v][co]
+// (the centre tap reads every position).  One workgroup per (conv, co), thread = ci.
+__global__ void __launch_bounds__(128) wgrad_tok_finish_kernel(const float* __restrict__ S, const float* __restrict__ E,
+                                                               float* __restrict__ dw0, float* __restrict__ dw1,
+                                                               float* __restrict__ db0, float* __restrict__ db1,
+                                                               int V) {
+  __shared__ float sv[KS * 32];
+  const int c = blockIdx.x / CH, co = blockIdx.x % CH, ci = threadIdx.x;
+  for (int i = threadIdx.x; i < KS * V; i += 128) {
+    const int k = i / V, v = i % V;
+    sv[k * 32 + v] = S[(((size_t)c * KS + k) * V + v) * CH + co];
+  }
+  __syncthreads();
+  float o[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) o[k] = 0.f;
+  for (int v = 0; v < V; ++v) {
+    const float e = bfround(E[v * CH + ci]);
+#pragma unroll
+    for (int k = 0; k < KS; ++k) o[k] = fmaf(e, sv[k * 32 + v], o[k]);
+  }
+  float* dw = (c ? dw1 : dw0) + ((size_t)co * CH + ci) * KS;
+#pragma unroll
+  for (int k = 0; k < KS; ++k) dw[k] += o[k];
+  if (ci == 0) {
+    float s = 0.f;
+    for (int v = 0; v < V; ++v) s += sv[(KS / 2) * 32 + v];
+    (c ? db1 : db0)[co] += s;
+  }
+}
+
+bool wgrad_tok_attr_set = false;
+}  // namespace
+
+extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st);
+
+// Rows of the per-workgroup slab pbx_wgrad_tok needs ([R][2][9][V][128] fp32).
+PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
+  const long NT = (long)B * ((L + TBM - 1) / TBM);
+  return (int)(NT < 128 ? NT : 128);
+}
+
+// Both convolutions of a block whose input is bf16(E[tok]) (KS = 9, L even, V <= 32): slab as
+// pbx_wgrad_tok_rows x 2 x 9 x V x 128 floats, S 2 x 9 x V x 128 floats (scratch); dW / db accumulated.
+PBX_EXPORT int pbx_wgrad_tok(const void* tok, const void* dy0, const void* dy1, const float* E, float* slab, float* S,
+                             float* dw0, float* dw1, float* db0, float* db1, int B, int L, int dil1, int V,
+                             hipStream_t st) {
+  if (V < 1 || V > 32 || dil1 < 1 || (L & 1) || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  const int buf = (2 * TBM + 8 + 8 * dil1) * 256 + 1024;
+  if (2 * buf > 163840) return (int)hipErrorInvalidValue;
+  if (!wgrad_tok_attr_set) {
+    (void)hipFuncSetAttribute((const void*)wgrad_tok_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    wgrad_tok_attr_set = true;
+  }
+  const int R = pbx_wgrad_tok_rows(B, L);
+  hipLaunchKernelGGL(wgrad_tok_kernel, dim3(R), dim3(512), 2 * buf, st, (const long long*)tok, (const bf16_t*)dy0,
+                     (const bf16_t*)dy1, slab, B, L, dil1, R, V, buf);
+  const int cols = 2 * KS * V * CH;
+  (void)hipMemsetAsync(S, 0, (size_t)cols * sizeof(float), st);
+  int rc = pbx_colsum_add(slab, R, cols, S, nullptr, st);
+  if (rc != 0) return rc;
+  hipLaunchKernelGGL(wgrad_tok_finish_kernel, dim3(2 * CH), dim3(128), 0, st, S, E, dw0, dw1, db0, db1, V);
+  return pbx_launch_status();
+}

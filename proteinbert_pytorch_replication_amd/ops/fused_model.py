@@ -100,7 +100,11 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:
-            h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0), cp=cp)
+            # the first block's input is the embedding: its conv weight gradient goes through the tokens
+            first = i == 0 and cp is None
+            h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0), cp=cp,
+                                   tok=tokens.contiguous() if first else None,
+                                   emb=model.local_embedding.weight if first else None)
             if cp is not None:
                 vpart = cp.pool_sum(vpart)      # [B, 1, NJ]: the group-wide sum over every shard's tiles
             wp = att.W_parameter

@@ -39,6 +39,7 @@ _lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad_tok", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
@@ -211,16 +212,46 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     return [slab, bslab]
 
 
+# the first block's conv weight gradient through the token one-hot (csrc/wgrad.hip wgrad_tok: its input is
+# the embedding bf16(E[tok]), so dW = E^T S with S a 32-row one-hot GEMM); PBX_WGRAD_TOK=0: wgrad2 over the
+# 128 embedding channels
+WGRAD_TOK = os.environ.get("PBX_WGRAD_TOK", "1") != "0"
+
+
+def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: int, KS: int) -> bool:
+    return (WGRAD_TOK and tok is not None and emb is not None and KS == 9 and L % 2 == 0
+            and emb.shape[0] <= 32 and emb.shape[1] == CH and tok.dtype == torch.int64 and tok.is_contiguous())
+
+
+def _wgrad_tok(dy0: torch.Tensor, dy1: torch.Tensor, tok: torch.Tensor, emb: torch.Tensor, dil: int, B: int, L: int,
+               outs):
+    """Both conv weight gradients of a block whose input is the embedding bf16(E[tok]); ``outs`` as
+    :func:`_wgrad`.  Returns the scratch tensors (kept alive while the launch may be running)."""
+    dev = dy0.device
+    V = emb.shape[0]
+    R = _lib.lib().pbx_wgrad_tok_rows(B, L)
+    slab = torch.empty((R, 2, 9, V, CH), dtype=torch.float32, device=dev)
+    S = torch.empty((2, 9, V, CH), dtype=torch.float32, device=dev)
+    e = emb.detach().float().contiguous()
+    (dw0, db0), (dw1, db1) = outs
+    _lib.call("pbx_wgrad_tok", tok.data_ptr(), dy0.data_ptr(), dy1.data_ptr(), e.data_ptr(), slab.data_ptr(),
+              S.data_ptr(), dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(), B, L, dil, V,
+              _lib.stream_ptr(dev))
+    return [slab, S, e]
+
+
 class LocalBlockFn(torch.autograd.Function):
     """Fused local track of one block (reference semantics)."""
 
     @staticmethod
     def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None,
-                tail: bool = False, cp=None):
+                tail: bool = False, cp=None, tok=None, emb=None):
         """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch);
         ``tail``: the first block (its backward ends the step: the conv weight gradient gets every CU);
         ``cp``: a :class:`..parallel.cp_fused.CPShard` -- ``x`` is this rank's slice of the sequence, the
-        conv reads the neighbours' halo rows and the (L, C) LayerNorm statistics are group-wide."""
+        conv reads the neighbours' halo rows and the (L, C) LayerNorm statistics are group-wide;
+        ``tok`` / ``emb``: ``x`` is the embedding bf16(emb[tok]) (the first block): the conv weight gradient
+        goes through the token one-hot (:func:`_wgrad_tok`)."""
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
         ctx.cp = cp
         if cp is not None:
@@ -285,6 +316,7 @@ class LocalBlockFn(torch.autograd.Function):
         ctx.save_for_backward(x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw,
                               wl_b, wv_bf16, g1, be1, g2)
         ctx.hlo = hlo
+        ctx.tok = (tok, emb) if cp is None and wgrad_tok_ok(tok, emb, L, KS) else None
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
         ctx.tail = bool(tail) and WGRAD_TAIL_FULL
         ctx.set_materialize_grads(False)
@@ -406,19 +438,25 @@ class LocalBlockFn(torch.autograd.Function):
             # the transposed conv reads dpre = ds1 GELU' of the neighbours' edge rows too
             conv_dgrad(cp.halo_rows(ds1), cp.halo_rows(pre_n), cp.halo_rows(pre_w), wtn, wtw, dx, dpn, dpw, B, L,
                        KS, dil, stream, hlo, hlo)
+        if ctx.tok is not None:
+            tok, emb = ctx.tok
+            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)])   # noqa: E731
+            keep = [dpn, dpw, tok]
+        else:
+            wg = lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)],   # noqa: E731
+                                ctx.tail and streams.ENABLED, hlo, hlo)
+            keep = [dpn, dpw, x_ext]
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
-            streams.launch(dev, lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], ctx.tail,
-                                               hlo, hlo),
-                           keep=[dpn, dpw, x_ext], name="wgrad")
+            streams.launch(dev, wg, keep=keep, name="wgrad")
         else:
-            _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)], False, hlo, hlo)
+            wg()
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None, None, None, None)
+        return (dx, dgb, *pgrads, None, None, None, None, None, None, None)
 
 
 class EmbedFn(torch.autograd.Function):
@@ -488,9 +526,10 @@ def conv_images(wn: torch.Tensor, ww: torch.Tensor):
 
 
 def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool = False,
-                cp=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                cp=None, tok=None, emb=None) -> Tuple[torch.Tensor, torch.Tensor]:
     """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``); ``tail``: it is the first block;
-    ``cp``: context-parallel shard (:class:`..parallel.cp_fused.CPShard`)."""
+    ``cp``: context-parallel shard (:class:`..parallel.cp_fused.CPShard`); ``tok`` / ``emb``: ``x`` is
+    the token embedding bf16(emb[tok])."""
     att = blk.global_attention_layer
     wv = _wv_bf16(att)                                                       # [H*vd, C]
     nc = blk.local_narrow_conv_layer[0]
@@ -498,4 +537,4 @@ def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool 
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
                               blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed,
-                              tail, cp)
+                              tail, cp, tok, emb)

@@ -123,6 +123,27 @@ def test_embedding_kernels():
     assert rel(E.grad, dref) < 1e-5
 
 
+@pytest.mark.parametrize("B,L,dil", [(3, 300, 5), (2, 512, 5), (1, 130, 2)])
+def test_wgrad_token_onehot_vs_fp32(B, L, dil):
+    """First-block conv weight gradient through the token one-hot (csrc/wgrad.hip wgrad_tok) vs the fp32
+    weight gradient of the 128-channel conv input bf16(E[tok]) (torch.nn.grad.conv1d_weight)."""
+    from proteinbert_pytorch_replication_amd.ops.local_track import _wgrad_tok
+    torch.manual_seed(B * L)
+    V = 26
+    E = torch.randn(V, 128, device="cuda")
+    tok = torch.randint(0, V, (B, L), device="cuda")
+    dpn = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
+    dpw = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
+    outs = [(torch.zeros(128, 128, 9, device="cuda"), torch.zeros(128, device="cuda")) for _ in range(2)]
+    _wgrad_tok(dpn, dpw, tok, E, dil, B, L, outs)
+    torch.cuda.synchronize()
+    x = E.to(torch.bfloat16).float()[tok].transpose(1, 2)                       # [B, 128, L]
+    for (dw, db), dp, d in ((outs[0], dpn, 1), (outs[1], dpw, dil)):
+        ref = torch.nn.grad.conv1d_weight(x, (128, 128, 9), dp.float().transpose(1, 2), padding=4 * d, dilation=d)
+        assert rel(dw, ref) < 1e-5, rel(dw, ref)
+        assert rel(db, dp.float().sum(dim=(0, 1))) < 1e-5
+
+
 @pytest.mark.parametrize("nblocks", [2, 3])
 def test_full_model_loss_and_grads_vs_torch(nblocks):
     from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
