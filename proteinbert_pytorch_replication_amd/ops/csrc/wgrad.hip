@@ -21,6 +21,7 @@
 // covers 2 x 128 contiguous bytes); wgrad2_reduce sums the chunks in fixed order (deterministic)
 // and adds into the torch layouts [co][ci][k] (the flat-arena .grad views).
 #include "mfma.h"
+#include <stdlib.h>
 
 using namespace pbx;
 typedef unsigned short bf16_t;
@@ -366,24 +367,37 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
     const int pos0 = (int)(tile - (tile / T) * T) * TBM;
     const unsigned char* base = cur + (cv ? rows0 * 256 : 0);
     const long long* ts = reinterpret_cast<const long long*>(cur + (rows0 + rows1) * 256);
-#pragma unroll 2
-    for (int kb = 0; kb < TBM / 16; ++kb) {
-      // A[i = v][k = src]: lane's token row v = r, sources kb*16 + 8h + j
+    // B[k = src][col = co] = dpre[src - s_k][co] of tap k: tile row hal + (4 - k) d + kb*16 + 8h + j
+    auto read_b = [&](int kb, bf16x8 (&fb)[KS]) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) {
+        const int rb = hal + (KS / 2 - k) * d + kb * 16 + 8 * h + q;
+        fb[k] = cat_tr(lds_tr(base, swz256e(rb, colb)), lds_tr(base, swz256e(rb + 4, colb)));
+      }
+    };
+    // A[i = v][k = src]: lane's token row v = r, sources kb*16 + 8h + j (positions >= L: no token)
+    auto onehot = [&](int kb) {
+      const uint4* tp = reinterpret_cast<const uint4*>(ts + kb * 16 + 8 * h);
+      const uint4 t0 = tp[0], t1 = tp[1], t2 = tp[2], t3 = tp[3];
+      const unsigned tv[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
       typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
       u16x8 oh;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int s = kb * 16 + 8 * h + j;
-        oh[j] = (pos0 + s < L && (int)ts[s] == r) ? (unsigned short)0x3F80 : (unsigned short)0;
-      }
-      const bf16x8 a = __builtin_bit_cast(bf16x8, oh);
+      for (int j = 0; j < 8; ++j)
+        oh[j] = (pos0 + kb * 16 + 8 * h + j < L && tv[j] == (unsigned)r) ? (unsigned short)0x3F80 : (unsigned short)0;
+      return __builtin_bit_cast(bf16x8, oh);
+    };
+    // every LDS read of a K-step is issued before its 9 MFMAs (one exposed LDS latency per step, which
+    // the SIMD's other wave covers; a second fragment set for a one-step-ahead prefetch spills)
+#pragma unroll 1
+    for (int kb = 0; kb < TBM / 16; ++kb) {
+      bf16x8 fb[KS];
+      read_b(kb, fb);
+      const bf16x8 a = onehot(kb);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        // B[k = src][col = co] = dpre[src - s_k][co]: tile row hal + (4 - k) d + kb*16 + 8h + j
-        const int rb = hal + (KS / 2 - k) * d + kb * 16 + 8 * h + q;
-        const bf16x8 fb = cat_tr(lds_tr(base, swz256e(rb, colb)), lds_tr(base, swz256e(rb + 4, colb)));
-        acc[k] = mfma32(a, fb, acc[k]);
-      }
+      for (int k = 0; k < KS; ++k) acc[k] = mfma32(a, fb[k], acc[k]);
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // slab [R][2][KS][V][128]: D row = token v, column = channel
@@ -434,8 +448,9 @@ extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
 
 // Rows of the per-workgroup slab pbx_wgrad_tok needs ([R][2][9][V][128] fp32).
 PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
+  static const int cap = getenv("PBX_WGRAD_TOK_R") ? atoi(getenv("PBX_WGRAD_TOK_R")) : 128;   // sweep knob
   const long NT = (long)B * ((L + TBM - 1) / TBM);
-  return (int)(NT < 128 ? NT : 128);
+  return (int)(NT < cap ? NT : cap);
 }
 
 // Both convolutions of a block whose input is bf16(E[tok]) (KS = 9, L even, V <= 32): slab as
