@@ -28,7 +28,7 @@ typedef unsigned short bf16_t;
 namespace {
 typedef __attribute__((ext_vector_type(4))) float f4_t;
 constexpr int RB = 16;       // rows per workgroup
-constexpr int PF = 4;        // B-fragment prefetch depth (k-steps in flight)
+constexpr int pbx_glob_pf = 4;   // B-fragment prefetch depth (k-steps in flight)
 
 __device__ __forceinline__ f4_t mfma16(const bf16x8& a, const bf16x8& b, const f4_t& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -43,7 +43,7 @@ __device__ __forceinline__ int atile_e(int row, int col, int W) { return atile(r
 // [tile][kstep][lane] of bf16x8 (KK / 32 k-steps per tile, a multiple of PF).  Step s uses ring slot
 // s % PF while the loads of step s + PF - 1 are in flight: the loop is unrolled by the ring size so
 // no register rotates (which would make the compiler wait for the newest load every step).
-template <int NT>
+template <int NT, int PF = (NT > 4 ? 2 : pbx_glob_pf)>   // 8 tiles a wave (4-wave backward): a 2-deep ring
 __device__ __forceinline__ void gemm_rows(f4_t* acc, const unsigned char* at, int KK, const bf16x8* __restrict__ frag,
                                           int tile0, int lane) {
   const int S = KK / 32;
@@ -544,9 +544,16 @@ extern "C" int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, f
 // the eight gradient destinations in a fixed order
 PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, float* slab, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1 || K > 512) return (int)hipErrorInvalidValue;
-  // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves)
-  if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, slab, st);
-  else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, slab, st);
+  // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves; PBX_GLOB_BWD_WAVES=4: a
+  // 4-wave form with the workgroup shape of conv_dgrad4, so the two share CUs when they run side by side)
+  static const int bw = getenv("PBX_GLOB_BWD_WAVES") ? atoi(getenv("PBX_GLOB_BWD_WAVES")) : 8;
+  if (bw == 4) {
+    if (G == 512) (NGL ? launch_bwd<8, 4, 128> : launch_bwd<8, 4, 0>)(B, p, K, slab, st);
+    else (NGL ? launch_bwd<4, 4, 128> : launch_bwd<4, 4, 0>)(B, p, K, slab, st);
+  } else {
+    if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, slab, st);
+    else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, slab, st);
+  }
   int rc = pbx_launch_status();
   if (rc != 0 || slab == nullptr) return rc;
   const int rows = (B + RB - 1) / RB, ld = 6 * G + NGL + K;

@@ -363,7 +363,9 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
     unsigned char* nxt = smem + (((tile - t0) & 1) ^ 1) * buf_bytes;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of `cur` landed
     __syncthreads();                                   // ... every wave's; `nxt` no longer read
+#ifndef PBX_TOK_NOSTAGE   // ablation builds only (tools/ubench/build_flags.sh)
     if (tile + 1 < t1) stage(tile + 1, nxt);
+#endif
     const int pos0 = (int)(tile - (tile / T) * T) * TBM;
     const unsigned char* base = cur + (cv ? rows0 * 256 : 0);
     const long long* ts = reinterpret_cast<const long long*>(cur + (rows0 + rows1) * 256);
@@ -448,7 +450,7 @@ extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
 
 // Rows of the per-workgroup slab pbx_wgrad_tok needs ([R][2][9][V][128] fp32).
 PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
-  static const int cap = getenv("PBX_WGRAD_TOK_R") ? atoi(getenv("PBX_WGRAD_TOK_R")) : 128;   // sweep knob
+  static const int cap = getenv("PBX_WGRAD_TOK_R") ? atoi(getenv("PBX_WGRAD_TOK_R")) : 256;   // sweep knob (128: +50 % time)
   const long NT = (long)B * ((L + TBM - 1) / TBM);
   return (int)(NT < cap ? NT : cap);
 }
