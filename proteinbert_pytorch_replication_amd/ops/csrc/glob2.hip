@@ -542,12 +542,20 @@ extern "C" int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, f
 //    db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl, dwp   (29 pointers)
 // slab (nullable, deterministic mode): [ceil(B / 16)][6 G + NGL + K] fp32 column-sum partials, folded into
 // the eight gradient destinations in a fixed order
+static int g_bwd_waves = -1;
+// waves per workgroup of pbx_glob_bwd: 8 (default) or 4 (tests select both)
+PBX_EXPORT int pbx_glob_set_bwd_waves(int w) {
+  if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
+  g_bwd_waves = w;
+  return 0;
+}
+
 PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, float* slab, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1 || K > 512) return (int)hipErrorInvalidValue;
   // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves; PBX_GLOB_BWD_WAVES=4: a
   // 4-wave form with the workgroup shape of conv_dgrad4, so the two share CUs when they run side by side)
-  static const int bw = getenv("PBX_GLOB_BWD_WAVES") ? atoi(getenv("PBX_GLOB_BWD_WAVES")) : 8;
-  if (bw == 4) {
+  if (g_bwd_waves < 0) g_bwd_waves = getenv("PBX_GLOB_BWD_WAVES") ? atoi(getenv("PBX_GLOB_BWD_WAVES")) : 8;
+  if (g_bwd_waves == 4) {
     if (G == 512) (NGL ? launch_bwd<8, 4, 128> : launch_bwd<8, 4, 0>)(B, p, K, slab, st);
     else (NGL ? launch_bwd<4, 4, 128> : launch_bwd<4, 4, 0>)(B, p, K, slab, st);
   } else {

@@ -3,6 +3,8 @@ one-launch form (csrc/glob2.hip) -- against a plain PyTorch fp32 evaluation of t
 (reference modules.py:175-199,219-229, reference semantics): forward outputs, the input / attention-
 partial gradients and every parameter gradient.  The kernels use bf16 GEMM operands (activations and
 weight mirrors), so the tolerances are bf16-level relative errors."""
+import os
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -50,12 +52,22 @@ def _run(fn_apply, params, g0, vp0, dg2, dgb, NGL):
     return [g2.detach(), gb.detach()], [g.grad, vp.grad] + [None if p is None else p.grad.clone() for p in params]
 
 
-@pytest.mark.parametrize("fwd3,bwd3", [(True, False), (True, True), (False, False)])   # default first
+@pytest.mark.parametrize("fwd3,bwd3,bwaves", [(True, False, 8), (True, True, 8), (False, False, 8), (True, False, 4)])
 @pytest.mark.parametrize("B,G,NGL,TV", [(512, 512, 128, 8), (256, 512, 128, 8), (20, 512, 128, 2),
                                         (37, 256, 0, 4), (16, 256, 128, 1)])
-def test_fused_global_block_vs_fp32(B, G, NGL, TV, fwd3, bwd3, monkeypatch):
+def test_fused_global_block_vs_fp32(B, G, NGL, TV, fwd3, bwd3, bwaves, monkeypatch):
+    """bwaves: workgroup size of the one-launch backward (csrc/glob2.hip, 8 waves default / 4-wave form)."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
     monkeypatch.setattr(global_track, "GLOB3", fwd3)
     monkeypatch.setattr(global_track, "GLOB3_BWD", bwd3)
+    assert _lib.lib().pbx_glob_set_bwd_waves(bwaves) == 0
+    try:
+        _check_fused_global_block(B, G, NGL, TV)
+    finally:
+        _lib.lib().pbx_glob_set_bwd_waves(int(os.environ.get("PBX_GLOB_BWD_WAVES", "8")))
+
+
+def _check_fused_global_block(B, G, NGL, TV):
     dev = torch.device("cuda")
     K = 64
     params = _params(G, NGL, K, dev)
