@@ -96,7 +96,8 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         if paper:
             # per-position LayerNorm local track, then attention over positions (split-L HIP core);
             # its [B, G] output enters the global track unscaled (W_parameter unused, as in the oracle)
-            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i])
+            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i], tok=tokens.contiguous() if i == 0 else None,
+                               emb=model.local_embedding.weight if i == 0 else None)
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:

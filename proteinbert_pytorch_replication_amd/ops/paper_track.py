@@ -28,7 +28,8 @@ from ..train.arena import notify_grads_ready
 from .gemm import gemm as _gemm
 from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
                            addmm_into)
-from .local_track import CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad
+from .local_track import (CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad,
+                          _wgrad_tok, wgrad_tok_ok)
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
@@ -49,6 +50,9 @@ FUSED_BWD_WAVES = int(os.environ.get("PBX_PF_BWD_WAVES", "8"))   # backward: 32 
 # weight gradients of the K/V projections and of the local head (K = B*L reductions): the in-tree
 # split-K MFMA GEMM (default) or chunked library bmm (PBX_PAPER_WGRAD=bmm, A/B)
 PAPER_WGRAD_GEMM = os.environ.get("PBX_PAPER_WGRAD", "gemm") != "bmm"
+# the attention projections' weight gradients on the weight-gradient stream (PBX_PAPER_ATT_WGRAD_AUX=0: on
+# the main stream, inline)
+ATT_WGRAD_AUX = os.environ.get("PBX_PAPER_ATT_WGRAD_AUX", "1") != "0"
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
@@ -76,7 +80,8 @@ class PaperBlockFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, gb, g, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv, mask, dil: int, packed=None):
+    def forward(ctx, x, gb, g, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv, mask, dil: int, packed=None,
+                tok=None, emb=None):
         from .paper_attention import KEY_DIM, VALUE_DIM, _nsplit
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv)
         B, L, C = x.shape
@@ -133,6 +138,8 @@ class PaperBlockFn(torch.autograd.Function):
                       o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
             wsave = wcat
         ctx.fused = fused
+        # the first block: x = bf16(emb[tok]), the conv weight gradient goes through the token one-hot
+        ctx.tok = (tok, emb) if wgrad_tok_ok(tok, emb, L, KS) else None
         ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
                               wq_cat)
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
@@ -177,21 +184,32 @@ class PaperBlockFn(torch.autograd.Function):
                           stream)
                 dh2_att = [mm32(dpre, wsave.t()).to(BF16), None]                          # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
-            if PAPER_WGRAD_GEMM:
-                # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
-                dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
-                _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)                   # [C, N] fp32
-            else:
-                nc = _split_k_chunks(R)
-                dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
-                                  out_dtype=F32).sum(dim=0)                               # [C, N] fp32
-            dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
-            dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
             dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K).to(BF16)   # [B, H*K]
-            G = g_bf.shape[1]
-            dwq = mm32(g_bf.t(), dqpre)                                                    # [G, H*K], K = B
-            dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
             dg = mm32(dqpre, wq_cat.t())                                                   # [B, G]
+
+            def att_wgrad(dpre=dpre, h2=h2, dqpre=dqpre, g_bf=g_bf):
+                # attention projection weight gradients: dWk | dWv = h2^T dpre (K = B*L), dWq = g^T dqpre
+                if PAPER_WGRAD_GEMM:
+                    # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
+                    dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
+                    _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)               # [C, N] fp32
+                else:
+                    nc = _split_k_chunks(R)
+                    dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
+                                      out_dtype=F32).sum(dim=0)                           # [C, N] fp32
+                dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
+                dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
+                G = g_bf.shape[1]
+                dwq = mm32(g_bf.t(), dqpre)                                                # [G, H*K], K = B
+                dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
+                return [dwcat, dwq]
+
+            if ATT_WGRAD_AUX and streams.ENABLED and dev.type == "cuda" and all(d for _, d in dsts[10:]):
+                # only the optimizer and the DP all-reduce read them: beside the critical path, on the
+                # weight-gradient stream (the split-K GEMM over B*L rows was ~60 us per block on it)
+                streams.launch(dev, att_wgrad, keep=[dpre, h2, dqpre, g_bf], name="wgrad")
+            else:
+                att_wgrad()
         ds1 = torch.empty_like(x)
         T = (L + TR - 1) // TR
         dgbp = torch.empty((B, T, CH), dtype=F32, device=dev)
@@ -205,27 +223,32 @@ class PaperBlockFn(torch.autograd.Function):
             streams.fork(dev, "global")
         dx, dpn, dpw = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
         conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
-        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
-            streams.launch(dev, lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)]),
-                           keep=[dpn, dpw, x], name="wgrad")
+        if ctx.tok is not None:
+            tok, emb = ctx.tok
+            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)])   # noqa: E731
         else:
-            _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])
+            wg = lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])      # noqa: E731
+        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
+            streams.launch(dev, wg, keep=[dpn, dpw, x], name="wgrad")
+        else:
+            wg()
         direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else gr for (gr, d) in dsts]
-        return (dx, dgb, dg, *pgrads, None, None, None)
+        return (dx, dgb, dg, *pgrads, None, None, None, None, None)
 
 
-def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None):
-    """``(h2, o)`` of one paper-semantics block's local track + attention (fused HIP path)."""
+def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None, tok=None, emb=None):
+    """``(h2, o)`` of one paper-semantics block's local track + attention (fused HIP path); ``tok`` /
+    ``emb``: ``x`` is the token embedding bf16(emb[tok]) (the first block)."""
     nc = blk.local_narrow_conv_layer[0]
     wc = blk.local_wide_conv_layer[0]
     att = blk.global_attention_layer
     return PaperBlockFn.apply(x, gb, g, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
                               blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
-                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed)
+                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed, tok, emb)
 
 
 def paper_local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> torch.Tensor:
