@@ -131,9 +131,15 @@ def main():
             return pretrain_loss_torch(pl, pg, Y, W, return_parts=return_parts)
         step.loss = faithful_loss
     gen = SyntheticUniRefGO(L, mcfg.num_annotations, B, dev, seed=a.seed + 1000 * info.rank)
+    batches = gen.next_batch
+    if dev.type == "cuda" and os.environ.get("PBX_PREFETCH", "1") != "0":
+        # the next step's synthetic batch is generated on a side stream beside this step
+        # (train.step.PrefetchedBatches; PBX_PREFETCH=0: at the head of each step)
+        from proteinbert_pytorch_replication_amd.train.step import PrefetchedBatches
+        batches = PrefetchedBatches(gen.next_batch, dev)
 
     def one():
-        X, Y, W = gen.next_batch()
+        X, Y, W = batches()
         return step(X, Y, W)
 
     use_graph = a.graph == "on" or (a.graph == "auto" and dev.type == "cuda" and a.impl == "hip" and

@@ -99,6 +99,46 @@ class PretrainStep:
         return loss.detach()
 
 
+class PrefetchedBatches:
+    """Device-side batch producer run one step ahead on its own HIP stream.
+
+    ``batch_fn()`` enqueues the generation of a batch (synthetic data + corruption kernels, or an H2D
+    copy) on the current stream.  Here batch i + 1 is enqueued on a side stream when batch i is handed
+    out, so its small, latency-bound kernels run beside the training step instead of at the head of
+    the next one; the consumer stream waits on an event recorded after the batch (the reference's
+    loader hands the step a ready batch the same way, ``utils.py:282-289``).  Every batch is still
+    produced inside the consumer's loop; the extra one is only ever the next step's."""
+
+    def __init__(self, batch_fn, device: torch.device):
+        self.batch_fn = batch_fn
+        self.device = device
+        self.stream = torch.cuda.Stream(device=device)
+        self._next = None
+
+    def _make(self):
+        if self._next is None:
+            # once: the producer's device state (RNG / step counters) was created on the consumer stream
+            self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.stream):
+            batch = self.batch_fn()
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return batch, ev
+
+    def __call__(self):
+        if self._next is None:
+            self._next = self._make()
+        batch, ev = self._next
+        main = torch.cuda.current_stream(self.device)
+        main.wait_event(ev)
+        for part in batch:
+            for t in (part.values() if isinstance(part, dict) else (part,)):
+                if isinstance(t, torch.Tensor):
+                    t.record_stream(main)       # allocated on the side stream, consumed on this one
+        self._next = self._make()
+        return batch
+
+
 class GraphedStep:
     """The whole training step captured once as a hipGraph and replayed.
 

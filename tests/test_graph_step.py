@@ -66,3 +66,16 @@ def test_aux_stream_backward_matches_inline():
     assert torch.isfinite(grads[0]).all()
     scale = float(grads[0].abs().max())
     assert float((grads[0] - grads[1]).abs().max()) <= 1e-3 * scale
+
+
+def test_prefetched_batches_match_direct():
+    """bench.py's side-stream batch producer hands out the same batches, in order, as direct calls."""
+    from proteinbert_pytorch_replication_amd.train.step import PrefetchedBatches
+    g1 = SyntheticUniRefGO(128, 512, 8, "cuda", seed=5)
+    g2 = SyntheticUniRefGO(128, 512, 8, "cuda", seed=5)
+    pf = PrefetchedBatches(g2.next_batch, torch.device("cuda"))
+    for _ in range(4):
+        a, b = g1.next_batch(), pf()
+        for da, db in zip(a, b):
+            for k in da:
+                assert torch.equal(da[k], db[k]), k
