@@ -69,13 +69,17 @@ def test_local_block_forward(L, B, frozen):
 
 
 # pool backward: attn_bwd4 (weight-stationary, csrc/pool_bwd.hip) / attn_bwd2 (stored GELU' fragments, Wv in
-# LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup
-@pytest.mark.parametrize("recompute,wide,bwd4,tpw", [(0, 1, 1, 0), (0, 1, 1, 3), (0, 1, 0, 0), (1, 1, 0, 0),
-                                                     (1, 0, 0, 0)])
+# LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup;
+# conv: 3 = conv_fwd3 + conv_dgrad4 (default), 4 = persistent conv_fwd4 + conv_dgrad4, 2 = conv_fwd3 + conv_dgrad3
+@pytest.mark.parametrize("recompute,wide,bwd4,tpw,conv", [(0, 1, 1, 0, 3), (0, 1, 1, 3, 3), (0, 1, 0, 0, 3),
+                                                          (1, 1, 0, 0, 3), (1, 0, 0, 0, 3), (0, 1, 1, 0, 4),
+                                                          (0, 1, 1, 0, 2)])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
-def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, monkeypatch):
+def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
+    monkeypatch.setattr(local_track, "CONV_FWD4", int(conv == 4))
+    monkeypatch.setattr(local_track, "CONV_DGRAD4", int(conv != 2))
     monkeypatch.setattr(local_track, "POOL_RECOMPUTE", recompute)
     monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
     monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
@@ -107,6 +111,59 @@ def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, monkeypatch):
     print(f"L={L} B={B}: " + " ".join(f"{n}={e:.2e}" for n, e in errs.items()))
     for n, e in errs.items():
         assert e < 3e-2, f"{n}: rel err {e:.3e}"
+
+
+@pytest.mark.parametrize("B,L,P", [(2, 256, 2), (3, 300, 3)])
+def test_cp_halo_conv_kernels_match_whole_sequence(B, L, P):
+    """The context-parallel conv launchers (pbx_conv_fwd4x / pbx_conv_dgrad4x / pbx_wgrad2x: neighbour
+    rows in place, csrc/conv4.hip, csrc/wgrad.hip) on P shards with 20-row halos reproduce the whole-
+    sequence kernels (parallel/cp_fused.py's exchange, done here by slicing)."""
+    from proteinbert_pytorch_replication_amd.ops import local_track as lt
+    torch.manual_seed(L + P)
+    dev = torch.device("cuda")
+    H, dil, C = 20, 5, 128
+    Ls = L // P
+    x = torch.randn(B, L, C, device=dev).to(torch.bfloat16)
+    wn, ww = (torch.randn(C, C, 9, device=dev) * 0.05 for _ in range(2))
+    bn, bw = torch.randn(C, device=dev) * 0.1, torch.randn(C, device=dev) * 0.1
+    gb = torch.randn(B, C, device=dev)
+    wpn, wtn = lt.pack_conv(wn)
+    wpw, wtw = lt.pack_conv(ww)
+    st = lt._lib.stream_ptr(dev)
+    T1 = (L + lt.BM1 - 1) // lt.BM1
+
+    def ext(t, r):       # shard r of [B, L, C] with H neighbour rows each side (zeros past the ends)
+        z = torch.zeros(B, H, C, dtype=t.dtype, device=dev)
+        tp = torch.cat([z, t, z], dim=1)
+        return tp[:, r * Ls:r * Ls + Ls + 2 * H].contiguous()
+
+    pre_n, pre_w, s1 = (torch.empty_like(x) for _ in range(3))
+    stats = torch.empty(B, T1, 2, device=dev)
+    lt.conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, 9, dil, st)
+    ds1 = torch.randn(B, L, C, device=dev).to(torch.bfloat16)
+    dx, dpn, dpw = (torch.empty_like(x) for _ in range(3))
+    lt.conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, 9, dil, st)
+    outs = [(torch.zeros(C, C, 9, device=dev), torch.zeros(C, device=dev)) for _ in range(2)]
+    lt._wgrad(dpn, dpw, x, 9, dil, 2, B, L, outs)
+    outs_s = [(torch.zeros(C, C, 9, device=dev), torch.zeros(C, device=dev)) for _ in range(2)]
+    keep = []
+    for r in range(P):
+        sl = slice(r * Ls, (r + 1) * Ls)
+        xe = ext(x, r)
+        pn_s, pw_s, s1_s = (torch.empty(B, Ls, C, dtype=torch.bfloat16, device=dev) for _ in range(3))
+        st_s = torch.empty(B, (Ls + lt.BM1 - 1) // lt.BM1, 2, device=dev)
+        lt.conv_fwd(xe, wpn, wpw, bn, bw, gb, pn_s, pw_s, s1_s, st_s, B, Ls, 9, dil, st, H, H)
+        dx_s, dpn_s, dpw_s = (torch.empty(B, Ls, C, dtype=torch.bfloat16, device=dev) for _ in range(3))
+        lt.conv_dgrad(ext(ds1, r), ext(pre_n, r), ext(pre_w, r), wtn, wtw, dx_s, dpn_s, dpw_s, B, Ls, 9, dil, st,
+                      H, H)
+        keep += lt._wgrad(dpn_s, dpw_s, xe, 9, dil, 2, B, Ls, outs_s, False, H, H)
+        torch.cuda.synchronize()
+        for name, a, b_ in (("pre_n", pn_s, pre_n[:, sl]), ("pre_w", pw_s, pre_w[:, sl]), ("s1", s1_s, s1[:, sl]),
+                            ("dx", dx_s, dx[:, sl]), ("dpn", dpn_s, dpn[:, sl]), ("dpw", dpw_s, dpw[:, sl])):
+            assert rel(a, b_) < 1e-2, (name, r, rel(a, b_))
+    torch.cuda.synchronize()
+    for (dw, db), (dws, dbs) in zip(outs, outs_s):
+        assert rel(dws, dw) < 1e-4 and rel(dbs, db) < 1e-4, (rel(dws, dw), rel(dbs, db))
 
 
 def test_embedding_kernels():
