@@ -1515,11 +1515,13 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   int BM1, const float* g1, const float* be1, const void* wl, float* consts,
                                   void* dh1, float* sums1, float* dg2, float* db2, float* dg1, float* db1, float* dwl,
                                   float* dbl, float* dgb_zero, int B, int L, float eps, float* dwl_slab, int slab_rows,
-                                  int det, int fold, hipStream_t st) {
+                                  int det, int fold, int consts_ready, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
-  hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
-                     consts, dgb_zero, B, L, eps);
+  // consts_ready: the pool backward (pbx_attn_bwd4c) already wrote consts and zeroed dgb_zero
+  if (!consts_ready)
+    hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
+                       consts, dgb_zero, B, L, eps);
   int gx, nsplit;
   ln2_bwd_grid(B, L, det, gx, nsplit);
   const int lds = 32768 + 2 * 32 * 256 + 32 * YS * 4;

@@ -49,12 +49,17 @@ struct EpiOps {            // one lane's epilogue operands of one tile: 4 groups
   float4 g[4];
 };
 
-template <int NJT>
+// CONSTS (a workgroup owns a whole sample, tpw >= ceil(L / 32)): the workgroup also writes the sample's
+// LayerNorm-2 / LayerNorm-1 backward constants consts[b] = (mean2, rstd2, m1, m2, mean1, rstd1, 0, 0) --
+// what ln2_consts_kernel (ln.hip) derives from the per-tile partials in a launch of its own -- and zeroes
+// row b of the [B, 128] accumulator the LN1 finalize adds into.  m1 / m2 sum the waves' per-tile partials
+// in a fixed order (deterministic).
+template <int NJT, bool CONSTS>
 __global__ void __launch_bounds__(256, 2) attn_bwd4_kernel(
     const bf16x8* __restrict__ gfrag, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
     const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dv,
     const bf16x8* __restrict__ wvt, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int L, int tpw,
-    float eps) {
+    float eps, const float* __restrict__ st1, int T1, int BM1, float* __restrict__ consts, float* __restrict__ zero128) {
   constexpr int NJ = NJT * 32;
   constexpr int NF = 2 * NJT;                 // 16-deep k-steps (1-KiB fragments) per tile
   constexpr int FPW = NF / 4;                 // fragments each wave DMAs per tile
@@ -131,6 +136,7 @@ __global__ void __launch_bounds__(256, 2) attn_bwd4_kernel(
   }
   float mean, rstd;
   wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
+  float wsa = 0.f, wsc = 0.f;                 // CONSTS: this wave's partial sums over the sample's tiles
 
   auto step = [&](int t, int buf) {
     // this wave's DMA of tile t has landed: after it the wave issued only tile t-1's epilogue loads
@@ -184,6 +190,10 @@ __global__ void __launch_bounds__(256, 2) attn_bwd4_kernel(
     }
     sa = wave_reduce_sum(sa);
     sc = wave_reduce_sum(sc);
+    if constexpr (CONSTS) {
+      wsa += sa;
+      wsc += sc;
+    }
     __builtin_amdgcn_sched_barrier(0);
     const int vo = okb ? (pos * CH + w * 32 + 4 * h) * 2 : 0x7ffffff0;
 #pragma unroll
@@ -192,6 +202,30 @@ __global__ void __launch_bounds__(256, 2) attn_bwd4_kernel(
     __builtin_amdgcn_raw_buffer_store_b64(sv2, sumr, lane == 0 ? ((t * 4 + w) * 8) : 0x7ffffff0, 0, 0);
   };
   for (int t = t0; t < t1; ++t) step(t, (t - t0) & 1);
+  if constexpr (CONSTS) {
+    // every DMA was consumed by its tile; the buffers are free once all waves are past their last tile
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    float* red = reinterpret_cast<float*>(smem);
+    if (lane == 0) {
+      red[2 * w] = wsa;
+      red[2 * w + 1] = wsc;
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float inv = 1.0f / (float)(L * CH);
+      const float m1 = (red[0] + red[2] + red[4] + red[6]) * inv;
+      const float m2 = (red[1] + red[3] + red[5] + red[7]) * inv;
+      float mean1, rstd1;
+      wave_ln_stats(st1 + (size_t)b * T1 * 2, T1, BM1, L, CH, eps, mean1, rstd1);
+      if (lane == 0) {
+        float4* c = reinterpret_cast<float4*>(consts + (size_t)b * 8);
+        c[0] = make_float4(mean, rstd, m1, m2);
+        c[1] = make_float4(mean1, rstd1, 0.f, 0.f);
+      }
+    } else if (w == 1) {
+      *reinterpret_cast<float2*>(zero128 + (size_t)b * CH + 2 * lane) = make_float2(0.f, 0.f);
+    }
+  }
 }
 // Wv [NJ][128] bf16 -> Wv^T A-operand fragments [ct = c / 32][i = NJ / 16][lane][8]:
 // element jj of lane (r, h) = Wv[16 i + 8 (jj >> 2) + 4 h + (jj & 3)][32 ct + r]
@@ -217,20 +251,24 @@ PBX_EXPORT int pbx_pack_wvt_frag(const void* wv, void* out, int NJ, hipStream_t 
 
 static bool pool4_attrs_set = false;
 
-// B samples; gfrag as written by pbx_ln_attn_fwd2; dv [B][NJ] fp32 (one gradient row per sample);
-// wvt: pbx_pack_wvt_frag image of Wv; sums2 [B][4 ceil(L/32)][2]; tpw <= 0: tiles per workgroup chosen here.
-PBX_EXPORT int pbx_attn_bwd4(const void* gfrag, const void* s2, const float* st2, const float* g2,
-                             const void* dh2_in, const float* dv, const void* wvt, void* dh2, float* sums2,
-                             int B, int L, int NJ, float eps, int tpw, hipStream_t st) {
+static int attn_bwd4_launch(const void* gfrag, const void* s2, const float* st2, const float* g2, const void* dh2_in,
+                            const float* dv, const void* wvt, void* dh2, float* sums2, int B, int L, int NJ, float eps,
+                            int tpw, const float* st1, int T1, int BM1, float* consts, float* zero128, hipStream_t st) {
   if ((NJ != 256 && NJ != 512) || B < 1 || L < 1) return (int)hipErrorInvalidValue;
-  const auto kern = NJ == 512 ? attn_bwd4_kernel<16> : attn_bwd4_kernel<8>;
+  const bool fuse = consts != nullptr;
+  const auto kern = NJ == 512 ? (fuse ? attn_bwd4_kernel<16, true> : attn_bwd4_kernel<16, false>)
+                              : (fuse ? attn_bwd4_kernel<8, true> : attn_bwd4_kernel<8, false>);
   if (!pool4_attrs_set) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    (void)hipFuncSetAttribute((const void*)attn_bwd4_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     pool4_attrs_set = true;
   }
   const int TW = (L + 31) / 32;
-  if (tpw <= 0) {
+  if (fuse) {
+    tpw = TW;                                 // one workgroup per sample
+  } else if (tpw <= 0) {
     // >= ~4 workgroups per CU-pair slot over the grid, whole samples when B alone fills the chip
     int dev = 0, ncu = 256;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -243,6 +281,28 @@ PBX_EXPORT int pbx_attn_bwd4(const void* gfrag, const void* s2, const float* st2
   const int nsplit = (TW + tpw - 1) / tpw;
   const int lds = 2 * (NJ / 16) * 1024;
   hipLaunchKernelGGL(kern, dim3(nsplit, B), dim3(256), lds, st, (const bf16x8*)gfrag, (const bf16_t*)s2, st2, g2,
-                     (const bf16_t*)dh2_in, dv, (const bf16x8*)wvt, (bf16_t*)dh2, sums2, L, tpw, eps);
+                     (const bf16_t*)dh2_in, dv, (const bf16x8*)wvt, (bf16_t*)dh2, sums2, L, tpw, eps, st1, T1, BM1,
+                     consts, zero128);
   return pbx_launch_status();
+}
+
+// B samples; gfrag as written by pbx_ln_attn_fwd2; dv [B][NJ] fp32 (one gradient row per sample);
+// wvt: pbx_pack_wvt_frag image of Wv; sums2 [B][4 ceil(L/32)][2]; tpw <= 0: tiles per workgroup chosen here.
+PBX_EXPORT int pbx_attn_bwd4(const void* gfrag, const void* s2, const float* st2, const float* g2,
+                             const void* dh2_in, const float* dv, const void* wvt, void* dh2, float* sums2,
+                             int B, int L, int NJ, float eps, int tpw, hipStream_t st) {
+  return attn_bwd4_launch(gfrag, s2, st2, g2, dh2_in, dv, wvt, dh2, sums2, B, L, NJ, eps, tpw, nullptr, 0, 0, nullptr,
+                          nullptr, st);
+}
+
+// pbx_attn_bwd4 with one workgroup per sample that also writes consts [B][8] (the ln2_consts_kernel output:
+// pbx_ln2_linear_bwd then runs with consts_ready = 1) and zeroes zero128 [B][128]; st1 [B][T1][2]: the
+// LayerNorm-1 (mean, M2) tile partials (tile BM1).
+PBX_EXPORT int pbx_attn_bwd4c(const void* gfrag, const void* s2, const float* st2, const float* g2,
+                              const void* dh2_in, const float* dv, const void* wvt, void* dh2, float* sums2,
+                              int B, int L, int NJ, float eps, const float* st1, int T1, int BM1, float* consts,
+                              float* zero128, hipStream_t st) {
+  if (consts == nullptr || zero128 == nullptr || st1 == nullptr) return (int)hipErrorInvalidValue;
+  return attn_bwd4_launch(gfrag, s2, st2, g2, dh2_in, dv, wvt, dh2, sums2, B, L, NJ, eps, 0, st1, T1, BM1, consts,
+                          zero128, st);
 }

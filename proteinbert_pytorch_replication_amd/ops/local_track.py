@@ -46,9 +46,10 @@ _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _
 _lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
+_lib.register("pbx_attn_bwd4c", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _I, _I, _P, _P, _P])
 _lib.register("pbx_pack_wvt_frag", [_P, _P, _I, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
-                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _P])
+                                     _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
@@ -75,6 +76,9 @@ POOL_RECOMPUTE = int(os.environ.get("PBX_POOL_RECOMPUTE", "0"))
 # CU); 0 = attn_bwd2 (whole Wv in 128 KB of LDS, dv applied per streamed fragment on the VALU)
 POOL_BWD4 = int(os.environ.get("PBX_POOL_BWD4", "1"))
 POOL_BWD4_TPW = int(os.environ.get("PBX_POOL_BWD4_TPW", "0"))   # tiles per workgroup (0: launcher's choice)
+# 1: attn_bwd4 runs one workgroup per sample and also writes the LayerNorm-2 / -1 backward constants (one
+# launch less per block: pbx_attn_bwd4c); 0: the launcher's tile split + ln2_consts_kernel
+POOL_CONSTS_FUSED = int(os.environ.get("PBX_POOL_CONSTS_FUSED", "1"))
 # attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
 POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
 
@@ -357,10 +361,15 @@ class LocalBlockFn(torch.autograd.Function):
         if bwd4:
             TA *= 4                              # attn_bwd4: one partial per (tile, wave)
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        if cp is not None:
-            # CP: the global track is replicated, so dvpart is already the gradient of the group-wide pool sum
-            pass
-        if bwd4:
+        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
+        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
+        # CP rewrites the LN2 partials group-wide between the pool backward and the constants: separate launch
+        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None))
+        if consts_ready:
+            _lib.call("pbx_attn_bwd4c", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
+                      LN_EPS, st1.data_ptr(), T1, BM1, consts.data_ptr(), dgb.data_ptr(), stream)
+        elif bwd4:
             _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
                       LN_EPS, POOL_BWD4_TPW, stream)
@@ -378,8 +387,6 @@ class LocalBlockFn(torch.autograd.Function):
         dh1 = torch.empty_like(x)
         TS1 = (L + 1) // 2                      # LN1 partials per (sample, position pair)
         sums1 = torch.empty((B, TS1, 2), dtype=torch.float32, device=dev)
-        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
-        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts kernel
         det = int(fused_deterministic())
         # the local-MLP weight / bias gradient partials are folded on the weight-gradient stream (only the
         # optimizer and the DP all-reduce read them): a slab of this call's own, the shared one is reused
@@ -395,7 +402,7 @@ class LocalBlockFn(torch.autograd.Function):
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, *slab_args, det, int(not late_fold), stream)
+                  dgb.data_ptr(), B, L, LN_EPS, *slab_args, det, int(not late_fold), consts_ready, stream)
         if late_fold:
             def fold(slab=fslab, rows=rows, dwl=dwl, dbl=dbl):
                 st = _lib.stream_ptr(dev)

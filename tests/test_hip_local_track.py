@@ -71,7 +71,8 @@ def test_local_block_forward(L, B, frozen):
 # pool backward: attn_bwd4 (weight-stationary, csrc/pool_bwd.hip) / attn_bwd2 (stored GELU' fragments, Wv in
 # LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup;
 # conv: 3 = conv_fwd3 + conv_dgrad4 (default), 4 = persistent conv_fwd4 + conv_dgrad4, 2 = conv_fwd3 + conv_dgrad3
-@pytest.mark.parametrize("recompute,wide,bwd4,tpw,conv", [(0, 1, 1, 0, 3), (0, 1, 1, 3, 3), (0, 1, 0, 0, 3),
+@pytest.mark.parametrize("recompute,wide,bwd4,tpw,conv", [(0, 1, 1, 0, 3), (0, 1, 1, 3, 3), (0, 1, 1, 16, 3),
+                                                          (0, 1, 0, 0, 3),
                                                           (1, 1, 0, 0, 3), (1, 0, 0, 0, 3), (0, 1, 1, 0, 4),
                                                           (0, 1, 1, 0, 2)])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
@@ -84,6 +85,9 @@ def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatc
     monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
     monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
     monkeypatch.setattr(local_track, "POOL_BWD4_TPW", tpw)
+    # tpw = 0: one workgroup per sample writing the LN constants too (pbx_attn_bwd4c, default); tpw > 0: the
+    # tile-split pbx_attn_bwd4 + ln2_consts_kernel
+    monkeypatch.setattr(local_track, "POOL_CONSTS_FUSED", int(tpw == 0))
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
