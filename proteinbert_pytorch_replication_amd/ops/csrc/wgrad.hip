@@ -394,8 +394,17 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
 #pragma unroll 1
     for (int kb = 0; kb < TBM / 16; ++kb) {
       bf16x8 fb[KS];
+#ifdef PBX_TOK_NOLDS      // ablation builds only (tools/ubench/build_flags.sh): B fragments without LDS reads
+#pragma unroll
+      for (int k = 0; k < KS; ++k) fb[k] = __builtin_bit_cast(bf16x8, make_uint4(kb + k, lane, 0u, 0u));
+#else
       read_b(kb, fb);
+#endif
+#ifdef PBX_TOK_NOONEHOT   // ablation builds only: a constant A operand
+      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(0x3F80u * (unsigned)(r == kb), 0u, 0u, 0u));
+#else
       const bf16x8 a = onehot(kb);
+#endif
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = mfma32(a, fb[k], acc[k]);
