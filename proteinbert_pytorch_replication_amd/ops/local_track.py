@@ -19,7 +19,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import Dict, Optional, Tuple
+from typing import List, Dict, Optional, Tuple
 
 import torch
 
@@ -183,6 +183,19 @@ LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
 # (profiles/r4_dgrad_stream_ab.txt): the one-launch global backward (8-wave workgroups) only finds CUs as
 # conv_dgrad4's 2-per-CU workgroups drain and stretches from 51 to ~210 us.  Off.
 DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "0") == "1"
+# PBX_WGRAD_DEFER=1: a block's conv weight gradient (aux stream) is launched after the NEXT block's pool
+# backward instead of right after its own data gradient, so it overlaps the LN2 / MLP backward, the LN1
+# finalize and the data gradient rather than the memory-bound pool backward (experiment, off by default)
+WGRAD_DEFER = os.environ.get("PBX_WGRAD_DEFER", "0") == "1"
+_DEFERRED: List = []
+
+
+def flush_deferred() -> None:
+    while _DEFERRED:
+        _DEFERRED.pop(0)()
+
+
+streams.pre_join_hooks.append(flush_deferred)
 # the input layer's backward starts beside the first block's conv data gradient (PBX_INPUT_BWD_EARLY=0:
 # on the main stream after it)
 INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
@@ -381,6 +394,7 @@ class LocalBlockFn(torch.autograd.Function):
             _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
                       stream)
+        flush_deferred()                         # the previous (deeper) block's deferred weight gradient
         if cp is not None:
             cp.fix_sums(sums2)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
@@ -453,13 +467,22 @@ class LocalBlockFn(torch.autograd.Function):
             wg = lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)],   # noqa: E731
                                 ctx.tail and streams.ENABLED, hlo, hlo)
             keep = [dpn, dpw, x_ext]
+        direct = [p for p, (_, d) in zip(params, dsts) if d]
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
-            streams.launch(dev, wg, keep=keep, name="wgrad")
+            if WGRAD_DEFER and not ctx.tail and cp is None and dev.type == "cuda":
+                conv_params = list(params[:4])
+
+                def deferred(wg=wg, keep=keep, conv_params=conv_params):
+                    streams.launch(dev, wg, keep=keep, name="wgrad")
+                    notify_grads_ready(conv_params)     # DP buckets see them once their kernel is enqueued
+                _DEFERRED.append(deferred)
+                direct = [p for p in direct if not any(p is c for c in conv_params)]
+            else:
+                streams.launch(dev, wg, keep=keep, name="wgrad")
         else:
             wg()
-        direct = [p for p, (_, d) in zip(params, dsts) if d]
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]

@@ -209,9 +209,15 @@ def wait_ready(*tensors) -> None:
                     _wait(cur, _streams[key])
 
 
+# callables run at the start of join(): launches that a backward deferred (ops/local_track.py WGRAD_DEFER)
+pre_join_hooks: List = []
+
+
 def join() -> None:
     """Main stream(s) wait for every aux stream; release the tensors kept for them."""
     _callback_queued["v"] = False
+    for hook in pre_join_hooks:
+        hook()
     for idx, keep in list(_pending.items()):
         if not keep and not _used.get(idx):
             continue
