@@ -11,10 +11,11 @@ from proteinbert_pytorch_replication_amd.train.step import PretrainStep
 from proteinbert_pytorch_replication_amd.utils import determinism
 
 
-def _run(device, backend, steps=3, L=64, A=96, G=64, C=32, B=6, blocks=2):
+def _run(device, backend, steps=3, L=64, A=96, G=64, C=32, B=6, blocks=2, semantics="reference"):
     torch.manual_seed(0)
     m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=C, global_dim=G,
-                    key_dim=64 if C == 128 else 16, num_heads=4, num_blocks=blocks, device=device, backend=backend)
+                    key_dim=64 if C == 128 else 16, num_heads=4, num_blocks=blocks, device=device, backend=backend,
+                    semantics=semantics)
     opt = FusedAdam(m.parameters(), lr=1e-3)
     step = PretrainStep(m, opt)
     gen = SyntheticUniRefGO(L, A, B, device, seed=7)
@@ -114,3 +115,20 @@ def test_backend_routing_without_fixed_order_kernels():
     finally:
         determinism.disable()
         torch.use_deterministic_algorithms(prev)
+
+
+def test_deterministic_paper_semantics_bitwise_cpu():
+    """Paper semantics in deterministic mode: routed to the PyTorch path (its HIP kernels reduce with float
+    atomics), and two runs from the same seed agree bitwise."""
+    prev = _enable_and_restore()
+    try:
+        dev = torch.device("cpu")
+        be = determinism.backend_for("hip", dict(semantics="paper", global_dim=64, local_dim=32))
+        assert be == "torch"
+        l1, p1 = _run(dev, be, semantics="paper")
+        l2, p2 = _run(dev, be, semantics="paper")
+    finally:
+        torch.use_deterministic_algorithms(prev)
+        determinism._STATE["on"] = False
+    assert l1 == l2
+    assert torch.equal(p1, p2)
