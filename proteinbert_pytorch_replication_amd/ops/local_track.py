@@ -79,6 +79,7 @@ POOL_BWD4_TPW = int(os.environ.get("PBX_POOL_BWD4_TPW", "0"))   # tiles per work
 # 1: attn_bwd4 runs one workgroup per sample and also writes the LayerNorm-2 / -1 backward constants (one
 # launch less per block: pbx_attn_bwd4c); 0: the launcher's tile split + ln2_consts_kernel
 POOL_CONSTS_FUSED = int(os.environ.get("PBX_POOL_CONSTS_FUSED", "1"))
+POOL_CONSTS_MIN_B: Optional[int] = None     # smallest batch for that form (None: two workgroups per CU)
 # attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
 POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
 
@@ -376,8 +377,11 @@ class LocalBlockFn(torch.autograd.Function):
         sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
         consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
         dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
-        # CP rewrites the LN2 partials group-wide between the pool backward and the constants: separate launch
-        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None))
+        # one workgroup per sample only when the batch alone fills two workgroups per CU (long sequences at
+        # small B keep the tile split); CP rewrites the LN2 partials group-wide between the pool backward and
+        # the constants: separate launch
+        min_b = POOL_CONSTS_MIN_B if POOL_CONSTS_MIN_B is not None else 2 * _num_cus(dev)
+        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None and dev.type == "cuda" and B >= min_b))
         if consts_ready:
             _lib.call("pbx_attn_bwd4c", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
                       dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,

@@ -85,9 +85,10 @@ def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatc
     monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
     monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
     monkeypatch.setattr(local_track, "POOL_BWD4_TPW", tpw)
-    # tpw = 0: one workgroup per sample writing the LN constants too (pbx_attn_bwd4c, default); tpw > 0: the
-    # tile-split pbx_attn_bwd4 + ln2_consts_kernel
+    # tpw = 0: one workgroup per sample writing the LN constants too (pbx_attn_bwd4c, the default when the
+    # batch fills the chip; forced here for every B); tpw > 0: the tile-split pbx_attn_bwd4 + ln2_consts_kernel
     monkeypatch.setattr(local_track, "POOL_CONSTS_FUSED", int(tpw == 0))
+    monkeypatch.setattr(local_track, "POOL_CONSTS_MIN_B", 0)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
