@@ -367,11 +367,12 @@ __global__ void __launch_bounds__(512) lhead_grad_kernel(const float* __restrict
 // P (G - T) into the table and the bf16 dz rows for the dWo GEMM, (6) dbo partial and dh = dZ Wo (MFMA,
 // staged through LDS for 256-B row stores).  h is read once (512-B runs per sample), Z never leaves
 // the CU.
-constexpr int PP = 2;
-constexpr int BMAXF = 512;
+// PP = 1 (513 <= B <= 1024): a workgroup owns ONE position; the table holds PP * B <= 1024 rows either way.
+constexpr int ROWSF = 1024;       // table rows = PP * max B
 constexpr int ZS = VP + 1;        // fp32 row stride of the table (column walks hit distinct banks)
-constexpr int FUSED_LDS = PP * BMAXF * ZS * 4 + VP * 256 + VP * 4 + 8 * 64 * 8 + 64 * 8 + 64 * 4 + 8 * 4;
+constexpr int FUSED_LDS = ROWSF * ZS * 4 + VP * 256 + VP * 4 + 8 * 64 * 8 + 64 * 8 + 64 * 4 + 8 * 4;
 
+template <int PP>
 __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restrict__ h, const float* __restrict__ wo,
                                                           const float* __restrict__ bo,
                                                           const long long* __restrict__ y,
@@ -380,12 +381,13 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
                                                           float* __restrict__ loss_part, int B, int L, int V,
                                                           float inv_bl) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NPAIR = PP * 32, PARTS = 512 / NPAIR;   // (position, v) columns; sample slices per column
   float* zt = reinterpret_cast<float*>(smem);                              // [PP * B][ZS]
-  unsigned char* wos = smem + PP * BMAXF * ZS * 4;                         // [32][128] bf16
+  unsigned char* wos = smem + ROWSF * ZS * 4;                              // [32][128] bf16
   float* bo_s = reinterpret_cast<float*>(wos + VP * 256);                  // [32]
-  float2* red = reinterpret_cast<float2*>(bo_s + VP);                      // [8][64]
-  float2* ms = red + 8 * 64;                                               // [64] (M, 1/S) per (p, v)
-  float* tt = reinterpret_cast<float*>(ms + 64);                           // [64] T per (p, v)
+  float2* red = reinterpret_cast<float2*>(bo_s + VP);                      // [PARTS][NPAIR]
+  float2* ms = red + 8 * 64;                                               // [NPAIR] (M, 1/S) per (p, v)
+  float* tt = reinterpret_cast<float*>(ms + 64);                           // [NPAIR] T per (p, v)
   float* lred = tt + 64;                                                   // [8]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r = lane & 31, hh = lane >> 5;
@@ -419,32 +421,32 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
     }
   }
   __syncthreads();
-  const int pair = tid & 63, part = tid >> 6;       // column (p, v) and sample slice of the reductions
+  const int pair = tid % NPAIR, part = tid / NPAIR;  // column (p, v) and sample slice of the reductions
   const int pp = pair >> 5, pv = pair & 31;
   // (2) (max, sum exp) over the samples of every (p, v)
   {
     float m = -3.0e38f, se = 0.f;
-    for (int s = part; s < B; s += 8) {
+    for (int s = part; s < B; s += PARTS) {
       const float z = zt[(pp * B + s) * ZS + pv];
       const float mn = fmaxf(m, z);
       se = se * __expf(m - mn) + __expf(z - mn);
       m = mn;
     }
-    red[part * 64 + pair] = make_float2(m, se);
+    red[part * NPAIR + pair] = make_float2(m, se);
   }
   __syncthreads();
-  if (tid < 64) {
+  if (tid < NPAIR) {
     float mm = red[tid].x;
 #pragma unroll
-    for (int k = 1; k < 8; ++k) mm = fmaxf(mm, red[k * 64 + tid].x);
+    for (int k = 1; k < PARTS; ++k) mm = fmaxf(mm, red[k * NPAIR + tid].x);
     float ss = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) ss += red[k * 64 + tid].y * __expf(red[k * 64 + tid].x - mm);
+    for (int k = 0; k < PARTS; ++k) ss += red[k * NPAIR + tid].y * __expf(red[k * NPAIR + tid].x - mm);
     ms[tid] = make_float2(mm, ss > 0.f ? 1.0f / ss : 0.f);
   }
   __syncthreads();
   // (3) per row: P (registers), CE term, G P into the table
-  constexpr int RPT = PP * BMAXF / 512;             // rows per thread
+  constexpr int RPT = ROWSF / 512;                  // rows per thread
   float P[RPT][VP], rse[RPT], coef[RPT];
   int yv[RPT];
   float lsum = 0.f;
@@ -460,7 +462,7 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
     float e[VP], se = 0.f, py = 0.f;
 #pragma unroll
     for (int v = 0; v < VP; ++v) {
-      const float2 mv = ms[(p & 1) * 32 + v];
+      const float2 mv = ms[p * 32 + v];
       const float z = row < NR ? zt[row * ZS + v] : 0.f;
       P[k][v] = ok && v < V ? __expf(z - mv.x) * mv.y : 0.f;
       e[v] = ok && v < V ? __expf(P[k][v]) : 0.f;
@@ -478,14 +480,14 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
   // (4) T = sum_b G P for every (p, v)
   {
     float a = 0.f;
-    for (int s = part; s < B; s += 8) a += zt[(pp * B + s) * ZS + pv];
-    red[part * 64 + pair] = make_float2(a, 0.f);
+    for (int s = part; s < B; s += PARTS) a += zt[(pp * B + s) * ZS + pv];
+    red[part * NPAIR + pair] = make_float2(a, 0.f);
   }
   __syncthreads();
-  if (tid < 64) {
+  if (tid < NPAIR) {
     float a = 0.f;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) a += red[k * 64 + tid].x;
+    for (int k = 0; k < PARTS; ++k) a += red[k * NPAIR + tid].x;
     tt[tid] = a;
   }
   __syncthreads();
@@ -500,7 +502,7 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
 #pragma unroll
     for (int v = 0; v < VP; ++v) {
       const float G = coef[k] * (__expf(P[k][v]) * rse[k] - (v == yv[k] ? 1.f : 0.f));
-      d[v] = ok && v < V ? P[k][v] * (G - tt[(p & 1) * 32 + v]) : 0.f;
+      d[v] = ok && v < V ? P[k][v] * (G - tt[p * 32 + v]) : 0.f;
       zt[row * ZS + v] = d[v];
     }
     if (ok) {
@@ -526,7 +528,7 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
     reinterpret_cast<float*>(red)[sl * 32 + v] = a;
   }
   // (6b) dh = dZ Wo: A fragments (bf16 of the fp32 table) of this wave's row tiles first
-  constexpr int TPW = PP * BMAXF / 32 / 8;          // row tiles per wave
+  constexpr int TPW = ROWSF / 32 / 8;               // row tiles per wave
   bf16x8 fa[TPW][2];
 #pragma unroll
   for (int i = 0; i < TPW; ++i) {
@@ -622,18 +624,25 @@ PBX_EXPORT int pbx_local_head3(const void* h, const float* wo, const float* bo, 
   return pbx_launch_status();
 }
 
-// One-launch head (B <= 512): dbo_part [ceil(L / 2)][V], loss_part [ceil(L / 2)] (each already / (B L))
+// Positions per workgroup of pbx_local_head_fused: 2 for B <= 512, 1 for B <= 1024 (0: unsupported).
+PBX_EXPORT int pbx_local_head_fused_pp(int B) { return B <= 512 ? 2 : B <= 1024 ? 1 : 0; }
+
+// One-launch head (B <= 1024): dbo_part [ceil(L / pp)][V], loss_part [ceil(L / pp)] (each already / (B L)),
+// pp = pbx_local_head_fused_pp(B)
 PBX_EXPORT int pbx_local_head_fused(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
                                     void* dh, void* dz, float* dbo_part, float* loss_part, int B, int L, int V,
                                     hipStream_t st) {
-  if (V > VP || V < 1 || B < 1 || B > BMAXF || L < 1) return (int)hipErrorInvalidValue;
+  const int pp = pbx_local_head_fused_pp(B);
+  if (V > VP || V < 1 || B < 1 || pp == 0 || L < 1) return (int)hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)lhead_fused_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FUSED_LDS);
+    (void)hipFuncSetAttribute((const void*)lhead_fused_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, FUSED_LDS);
+    (void)hipFuncSetAttribute((const void*)lhead_fused_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, FUSED_LDS);
     attr = true;
   }
   const float inv_bl = 1.0f / ((float)B * (float)L);
-  hipLaunchKernelGGL(lhead_fused_kernel, dim3((L + PP - 1) / PP), dim3(512), FUSED_LDS, st, (const bf16_t*)h, wo, bo,
-                     (const long long*)y, wl, (bf16_t*)dh, (bf16_t*)dz, dbo_part, loss_part, B, L, V, inv_bl);
+  hipLaunchKernelGGL(pp == 2 ? lhead_fused_kernel<2> : lhead_fused_kernel<1>, dim3((L + pp - 1) / pp), dim3(512),
+                     FUSED_LDS, st, (const bf16_t*)h, wo, bo, (const long long*)y, wl, (bf16_t*)dh, (bf16_t*)dz,
+                     dbo_part, loss_part, B, L, V, inv_bl);
   return pbx_launch_status();
 }

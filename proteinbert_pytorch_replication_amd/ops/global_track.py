@@ -49,9 +49,11 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     st = _s(dev)
     B, L, C = h.shape
     V = wo.shape[0]
-    if LHEAD_FUSED and B <= 512:
-        # one launch: a workgroup per 2 positions x all samples (the batch reductions stay on chip)
-        nt = (L + 1) // 2
+    if LHEAD_FUSED and B <= 1024:
+        # one launch: a workgroup per 2 positions (B <= 512) or 1 (B <= 1024) x all samples (the batch
+        # reductions stay on chip)
+        pp = _lib.lib().pbx_local_head_fused_pp(B)
+        nt = (L + pp - 1) // pp
         dh = torch.empty_like(h)
         dz = torch.empty((B * L, 32), dtype=BF16, device=dev)
         dbo_part = torch.empty((nt, V), dtype=F32, device=dev)

@@ -1,5 +1,5 @@
 """GPU: the fused pretraining heads + loss (HeadsLossFn: the one-launch local head of csrc/lhead.hip
-for B <= 512 and its five-pass form,
+for B <= 1024 (two positions per workgroup up to B = 512, one above) and its five-pass form,
 the GO head fused into the MFMA GEMM of csrc/gemm.hip) match the PyTorch fp32 reference
 (models/proteinbert.py heads_torch + train/losses.py) -- loss, dh, dg and every head parameter
 gradient (Wo, bo, Wa, ba), at the real 8943-wide GO head and at batch / length extents that leave
@@ -14,7 +14,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("B,L,A", [(6, 24, 96), (100, 24, 96), (512, 24, 96), (640, 24, 96), (6, 1100, 96),
-                                   (40, 2000, 96), (512, 64, 8943), (300, 37, 8943), (17, 512, 8943)])
+                                   (40, 2000, 96), (512, 64, 8943), (300, 37, 8943), (17, 512, 8943),
+                                   (1024, 21, 96), (1030, 9, 96)])
 @pytest.mark.parametrize("lhead_fused", [True, False])
 def test_heads_loss_matches_torch(B, L, A, lhead_fused, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import global_track
