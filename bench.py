@@ -173,6 +173,8 @@ def main():
                "world_size": n, "backend": info.backend if n > 1 else "single",
                "rccl_env": getattr(info, "rccl_env", None),
                "device": _device_label(dev), "final_loss": round(final_loss, 5)}
+        if dev.type == "cuda":
+            out["peak_mem_gib"] = round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)
         if dev.type != "cuda" and a.preset == "cfg1_cpu_smoke":
             # BASELINE cfg 1 is a CPU config: compare with the reference step measured on a CPU
             out["vs_baseline"] = round(value / REFERENCE_CFG1_CPU_SEQ_PER_S, 2)

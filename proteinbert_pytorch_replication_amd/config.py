@@ -125,10 +125,12 @@ PRESETS: Dict[str, RunConfig] = {
         train=TrainConfig(batch_size=4)),
     # Per-GPU batches are sized for throughput on a 288 GB MI355X (~17 MiB of bf16 activations per
     # L=512 sequence): at 256 sequences many fused kernels still run only 1-2 work items per wave
-    # (latency-bound), 512 fills the chip (measured 53k -> 61k seq/s; 1024: 63k).
+    # (latency-bound); 512 fills the chip, and 1024 amortises the step's fixed part (weight-gradient
+    # reductions, the optimizer, launch tails; ~0.9 ms of a 6.3 ms B=512 step).  Round-4 same-box
+    # sweep: B=512 81.3k, 1024 87.1-87.5k, 1536 88.9k, 2048 90.0k seq/s (profiles/r4_batch_sweep.txt).
     "cfg2_paper_l512": RunConfig(
         name="cfg2_paper_l512", model=_paper_model(512),
-        train=TrainConfig(batch_size=512)),
+        train=TrainConfig(batch_size=1024)),
     "cfg3_paper_l1024_dp8": RunConfig(
         name="cfg3_paper_l1024_dp8", model=_paper_model(1024),
         train=TrainConfig(batch_size=256)),
