@@ -1272,9 +1272,15 @@ __global__ void __launch_bounds__(256) embed_fwd_kernel(const long long* __restr
 // dE: accumulated with one atomic per (token, channel) and workgroup, or (slab != nullptr, the
 // deterministic mode) this workgroup's [V][128] partial goes to slab row blockIdx.x (folded in a fixed
 // order by the caller)
+// DPRE (the first block's fold, pbx_embed_dpre): dout is that block's dS1 (the residual part of the
+// embedding gradient) and the staging pass also writes the conv pre-activation gradients
+// dpre_c = dS1 * GELU'(pre_c) of both convolutions (the products conv_dgrad4 would stage, bitwise)
+template <bool DPRE>
 __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restrict__ tok,
                                                         const bf16_t* __restrict__ dout, float* __restrict__ dE,
-                                                        long rows, int V, float* __restrict__ slab) {
+                                                        long rows, int V, float* __restrict__ slab,
+                                                        const bf16_t* __restrict__ gdn, const bf16_t* __restrict__ gdw,
+                                                        bf16_t* __restrict__ dpn, bf16_t* __restrict__ dpw) {
   __shared__ __attribute__((aligned(16))) unsigned char ds[256 * 256];
   __shared__ int ts[256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1286,14 +1292,49 @@ __global__ void __launch_bounds__(256) embed_bwd_kernel(const long long* __restr
   for (long t0 = r0; t0 < r1; t0 += 256) {
     const int n = (int)min((long)256, r1 - t0);
     __syncthreads();
-    stage_chunks(
-        256 * 16,
-        [&](int idx) {
-          const int row = idx >> 4;
-          return row < n ? *reinterpret_cast<const uint4*>(dout + (t0 + row) * CH + (idx & 15) * 8)
-                         : make_uint4(0u, 0u, 0u, 0u);
-        },
-        [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(ds + swz256(idx >> 4, idx & 15)) = v; });
+    if constexpr (DPRE) {
+      // 4 chunks x (dS1, GELU'_n, GELU'_w) in flight per thread
+      for (int base = tid; base < 256 * 16; base += 4 * 256) {
+        uint4 gq[4], nq[4], wq[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = base + i * 256, row = idx >> 4;
+          const size_t off = (size_t)(t0 + min(row, n - 1)) * CH + (idx & 15) * 8;
+          gq[i] = *reinterpret_cast<const uint4*>(dout + off);
+          nq[i] = *reinterpret_cast<const uint4*>(gdn + off);
+          wq[i] = *reinterpret_cast<const uint4*>(gdw + off);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int idx = base + i * 256, row = idx >> 4;
+          const bool ok = row < n;
+          *reinterpret_cast<uint4*>(ds + swz256(row, idx & 15)) = ok ? gq[i] : make_uint4(0u, 0u, 0u, 0u);
+          if (ok) {
+            float g[8], pn[8], pw[8], on[8], ow[8];
+            unpack8(gq[i], g);
+            unpack8(nq[i], pn);
+            unpack8(wq[i], pw);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              on[e] = pn[e] * g[e];
+              ow[e] = pw[e] * g[e];
+            }
+            const size_t off = (size_t)(t0 + row) * CH + (idx & 15) * 8;
+            *reinterpret_cast<uint4*>(dpn + off) = packq8(on);
+            *reinterpret_cast<uint4*>(dpw + off) = packq8(ow);
+          }
+        }
+      }
+    } else {
+      stage_chunks(
+          256 * 16,
+          [&](int idx) {
+            const int row = idx >> 4;
+            return row < n ? *reinterpret_cast<const uint4*>(dout + (t0 + row) * CH + (idx & 15) * 8)
+                           : make_uint4(0u, 0u, 0u, 0u);
+          },
+          [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(ds + swz256(idx >> 4, idx & 15)) = v; });
+    }
     ts[tid] = tid < n ? (int)tok[t0 + tid] : -1;
     __syncthreads();
     const int colb = w * 32 + tc;
@@ -1582,8 +1623,28 @@ PBX_EXPORT int pbx_embed_bwd(const void* tok, const void* dout, float* dE, long 
                              hipStream_t st) {
   if (V > 32) return (int)hipErrorInvalidValue;
   const int g = pbx_embed_bwd_groups(rows);
-  hipLaunchKernelGGL(embed_bwd_kernel, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
-                     (const bf16_t*)dout, dE, rows, V, slab);
+  hipLaunchKernelGGL(embed_bwd_kernel<false>, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
+                     (const bf16_t*)dout, dE, rows, V, slab, nullptr, nullptr, nullptr, nullptr);
+  if (slab != nullptr) {
+    const int rc = pbx_launch_status();
+    if (rc != 0) return rc;
+    return pbx_colsum_add(slab, g, V * CH, dE, nullptr, st);
+  }
+  return pbx_launch_status();
+}
+
+// The first block's backward without its conv data gradient (reference modules.py:249-253,300: the
+// block input is the embedding, so dE = sum_{tok} dx, dx = dS1 + conv^T(dpre); the conv^T part is
+// E-space and added by pbx_wgrad_tok from its one-hot sums): dE += sum_{rows : tok = v} dS1[row] and
+// dpre_n / dpre_w = dS1 * GELU'(pre) for the weight gradient, one pass over dS1.  Same slab contract
+// as pbx_embed_bwd.
+PBX_EXPORT int pbx_embed_dpre(const void* tok, const void* ds1, const void* gdn, const void* gdw, void* dpn, void* dpw,
+                              float* dE, long rows, int V, float* slab, hipStream_t st) {
+  if (V > 32 || rows < 1) return (int)hipErrorInvalidValue;
+  const int g = pbx_embed_bwd_groups(rows);
+  hipLaunchKernelGGL(embed_bwd_kernel<true>, dim3((unsigned)g), dim3(256), 0, st, (const long long*)tok,
+                     (const bf16_t*)ds1, dE, rows, V, slab, (const bf16_t*)gdn, (const bf16_t*)gdw, (bf16_t*)dpn,
+                     (bf16_t*)dpw);
   if (slab != nullptr) {
     const int rc = pbx_launch_status();
     if (rc != 0) return rc;

@@ -423,10 +423,15 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
 
 // dW_c[co][ci][k] += sum_v bf16(E[v][ci]) S[c][k][v][co] ; db_c[co] += sum_v S[c][4][v][co]
 // (the centre tap reads every position).  One workgroup per (conv, co), thread = ci.
+// W0 / W1 / dEslab (the embedding gradient's conv part, pbx_embed_dpre): this workgroup's share of
+//   dE[v][ci] = sum_c sum_co sum_k bf16(W_c[co][ci][k]) S[c][k][v][co]
+// (the transposed convolution of dpre summed over the source positions with token v) goes to slab row
+// blockIdx.x, folded in a fixed order by the caller.
 __global__ void __launch_bounds__(128) wgrad_tok_finish_kernel(const float* __restrict__ S, const float* __restrict__ E,
                                                                float* __restrict__ dw0, float* __restrict__ dw1,
                                                                float* __restrict__ db0, float* __restrict__ db1,
-                                                               int V) {
+                                                               int V, const float* __restrict__ W0,
+                                                               const float* __restrict__ W1, float* __restrict__ dEslab) {
   __shared__ float sv[KS * 32];
   const int c = blockIdx.x / CH, co = blockIdx.x % CH, ci = threadIdx.x;
   for (int i = threadIdx.x; i < KS * V; i += 128) {
@@ -450,6 +455,18 @@ __global__ void __launch_bounds__(128) wgrad_tok_finish_kernel(const float* __re
     for (int v = 0; v < V; ++v) s += sv[(KS / 2) * 32 + v];
     (c ? db1 : db0)[co] += s;
   }
+  if (dEslab != nullptr) {
+    const float* wr = (c ? W1 : W0) + ((size_t)co * CH + ci) * KS;
+    float wk[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) wk[k] = bfround(wr[k]);
+    for (int v = 0; v < V; ++v) {
+      float a = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) a = fmaf(wk[k], sv[k * 32 + v], a);
+      dEslab[((size_t)blockIdx.x * V + v) * CH + ci] = a;
+    }
+  }
 }
 
 bool wgrad_tok_attr_set = false;
@@ -466,10 +483,14 @@ PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
 
 // Both convolutions of a block whose input is bf16(E[tok]) (KS = 9, L even, V <= 32): slab as
 // pbx_wgrad_tok_rows x 2 x 9 x V x 128 floats, S 2 x 9 x V x 128 floats (scratch); dW / db accumulated.
+// W0 / W1 / dE / dEslab (all null, or all set): also dE += the conv part of the embedding gradient (see
+// the finish kernel; W_c: the fp32 conv weights [128][128][9]; dEslab: 2 x 128 x V x 128 floats scratch).
 PBX_EXPORT int pbx_wgrad_tok(const void* tok, const void* dy0, const void* dy1, const float* E, float* slab, float* S,
                              float* dw0, float* dw1, float* db0, float* db1, int B, int L, int dil1, int V,
-                             hipStream_t st) {
+                             const float* W0, const float* W1, float* dE, float* dEslab, hipStream_t st) {
   if (V < 1 || V > 32 || dil1 < 1 || (L & 1) || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  if ((dE == nullptr) != (W0 == nullptr) || (dE == nullptr) != (W1 == nullptr) || (dE == nullptr) != (dEslab == nullptr))
+    return (int)hipErrorInvalidValue;
   const int buf = (2 * TBM + 8 + 8 * dil1) * 256 + 1024;
   if (2 * buf > 163840) return (int)hipErrorInvalidValue;
   if (!wgrad_tok_attr_set) {
@@ -483,6 +504,10 @@ PBX_EXPORT int pbx_wgrad_tok(const void* tok, const void* dy0, const void* dy1, 
   (void)hipMemsetAsync(S, 0, (size_t)cols * sizeof(float), st);
   int rc = pbx_colsum_add(slab, R, cols, S, nullptr, st);
   if (rc != 0) return rc;
-  hipLaunchKernelGGL(wgrad_tok_finish_kernel, dim3(2 * CH), dim3(128), 0, st, S, E, dw0, dw1, db0, db1, V);
-  return pbx_launch_status();
+  hipLaunchKernelGGL(wgrad_tok_finish_kernel, dim3(2 * CH), dim3(128), 0, st, S, E, dw0, dw1, db0, db1, V, W0, W1,
+                     dEslab);
+  if (dE == nullptr) return pbx_launch_status();
+  rc = pbx_launch_status();
+  if (rc != 0) return rc;
+  return pbx_colsum_add(dEslab, 2 * CH, V * CH, dE, nullptr, st);
 }

@@ -17,7 +17,8 @@ import torch
 import torch.nn.functional as F
 
 from .global_track import FusedGlobalBlockFn, GlobalBlockFn, HeadsLossFn, InputLayerFn, glob_fused_ok, pack_batch
-from .local_track import CH, EmbedFn, conv_images, local_block
+from . import local_track as _lt
+from .local_track import CH, EmbedFn, conv_images, embed_tokens, local_block, wgrad_tok_ok
 from .paper_track import PaperHeadsLossFn, paper_block, unit_attention_weight
 
 
@@ -66,8 +67,13 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     gl0 = blocks[0].global_to_local_linear_layer[0]
     # g0 and block 0's global->local vector; every GlobalBlockFn then produces the next block's gb
     g, g_bf, gb = InputLayerFn.apply(annotations, lin.weight, lin.bias, gl0.weight, gl0.bias)
-    h = EmbedFn.apply(tokens, model.local_embedding.weight)                      # [B,L,128] bf16
     paper = model.semantics == "paper"
+    emb_w = model.local_embedding.weight
+    tok_c = tokens.contiguous()
+    # the first block folds its conv data gradient into the embedding gradient (local_track.EMBED_FOLD)
+    fold = (_lt.EMBED_FOLD and cp is None and tokens.device.type == "cuda" and len(blocks) > 0
+            and wgrad_tok_ok(tok_c, emb_w, tokens.shape[1], blocks[0].local_narrow_conv_layer[0].weight.shape[2]))
+    h = embed_tokens(tok_c, emb_w) if fold else EmbedFn.apply(tokens, emb_w)    # [B,L,128] bf16
     mask = (tokens != 0).contiguous() if paper else None
     # every weight image the fused kernels read this step, built by one launch
     items, conv_imgs, glob_imgs = [], [], []
@@ -96,16 +102,16 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         if paper:
             # per-position LayerNorm local track, then attention over positions (split-L HIP core);
             # its [B, G] output enters the global track unscaled (W_parameter unused, as in the oracle)
-            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i], tok=tokens.contiguous() if i == 0 else None,
-                               emb=model.local_embedding.weight if i == 0 else None)
+            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i], tok=tok_c if i == 0 else None,
+                               emb=emb_w if i == 0 else None, emb_grad=fold and i == 0)
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:
             # the first block's input is the embedding: its conv weight gradient goes through the tokens
             first = i == 0 and cp is None
             h, vpart = local_block(h, gb, blk, conv_imgs[i], tail=(i == 0), cp=cp,
-                                   tok=tokens.contiguous() if first else None,
-                                   emb=model.local_embedding.weight if first else None)
+                                   tok=tok_c if first else None, emb=emb_w if first else None,
+                                   emb_grad=fold and i == 0)
             if cp is not None:
                 vpart = cp.pool_sum(vpart)      # [B, 1, NJ]: the group-wide sum over every shard's tiles
             wp = att.W_parameter

@@ -39,7 +39,7 @@ _lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I
 _lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
-_lib.register("pbx_wgrad_tok", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_wgrad_tok", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
@@ -55,6 +55,7 @@ _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
+_lib.register("pbx_embed_dpre", [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P, _P])
 _lib.register("pbx_embed_bwd_groups", [_L])
 
 CH = 128          # kernels are specialised for local_dim = 128
@@ -234,6 +235,11 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
 # the embedding bf16(E[tok]), so dW = E^T S with S a 32-row one-hot GEMM); PBX_WGRAD_TOK=0: wgrad2 over the
 # 128 embedding channels
 WGRAD_TOK = os.environ.get("PBX_WGRAD_TOK", "1") != "0"
+# ... and its conv data gradient is folded away: the block input is the embedding, so only
+# dE = sum_{tok} (dS1 + conv^T dpre) is needed -- the dS1 part in one pass that also writes dpre
+# (pbx_embed_dpre), the conv^T part as bf16(W)-weighted sums of the weight gradient's one-hot S
+# (pbx_wgrad_tok).  PBX_EMBED_FOLD=0: conv data gradient + embedding backward as for any block.
+EMBED_FOLD = os.environ.get("PBX_EMBED_FOLD", "1") != "0"
 
 
 def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: int, KS: int) -> bool:
@@ -242,9 +248,11 @@ def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: in
 
 
 def _wgrad_tok(dy0: torch.Tensor, dy1: torch.Tensor, tok: torch.Tensor, emb: torch.Tensor, dil: int, B: int, L: int,
-               outs):
+               outs, demb=None):
     """Both conv weight gradients of a block whose input is the embedding bf16(E[tok]); ``outs`` as
-    :func:`_wgrad`.  Returns the scratch tensors (kept alive while the launch may be running)."""
+    :func:`_wgrad`.  ``demb``: (W_narrow, W_wide, dE) -- also add the convolutions' part of the embedding
+    gradient into dE (the block's data gradient is folded away, :data:`EMBED_FOLD`).  Returns the scratch
+    tensors (kept alive while the launch may be running)."""
     dev = dy0.device
     V = emb.shape[0]
     R = _lib.lib().pbx_wgrad_tok_rows(B, L)
@@ -252,10 +260,31 @@ def _wgrad_tok(dy0: torch.Tensor, dy1: torch.Tensor, tok: torch.Tensor, emb: tor
     S = torch.empty((2, 9, V, CH), dtype=torch.float32, device=dev)
     e = emb.detach().float().contiguous()
     (dw0, db0), (dw1, db1) = outs
+    w0 = w1 = dE = dEslab = None
+    if demb is not None:
+        w0, w1 = (w.detach().float().contiguous() for w in demb[:2])
+        dE = demb[2]
+        dEslab = torch.empty((2 * CH, V, CH), dtype=torch.float32, device=dev)
     _lib.call("pbx_wgrad_tok", tok.data_ptr(), dy0.data_ptr(), dy1.data_ptr(), e.data_ptr(), slab.data_ptr(),
               S.data_ptr(), dw0.data_ptr(), dw1.data_ptr(), db0.data_ptr(), db1.data_ptr(), B, L, dil, V,
-              _lib.stream_ptr(dev))
-    return [slab, S, e]
+              _p(w0), _p(w1), _p(dE), _p(dEslab), _lib.stream_ptr(dev))
+    return [slab, S, e, w0, w1, dEslab]
+
+
+def embed_fold_bwd(tok, emb, ds1, gdn, gdw, dpn, dpw, wn, ww, stream):
+    """First block with its conv data gradient folded away (:data:`EMBED_FOLD`): dE += sum_tok dS1 and
+    dpn / dpw = dS1 GELU'(pre) in one pass over dS1 (``pbx_embed_dpre``).  Returns ``((wn, ww, dE),
+    direct)``: the ``demb`` argument of :func:`_wgrad_tok` (which adds the convolutions' part of dE) and
+    whether dE is the arena gradient itself."""
+    B, L = tok.shape
+    dE, direct = _grad_dst(emb, emb.shape)
+    slab = None
+    if fused_deterministic():
+        slab = torch.empty((_lib.lib().pbx_embed_bwd_groups(B * L), emb.shape[0], CH), dtype=torch.float32,
+                           device=ds1.device)
+    _lib.call("pbx_embed_dpre", tok.data_ptr(), ds1.data_ptr(), gdn.data_ptr(), gdw.data_ptr(), dpn.data_ptr(),
+              dpw.data_ptr(), dE.data_ptr(), B * L, emb.shape[0], _p(slab), stream)
+    return (wn, ww, dE), direct
 
 
 class LocalBlockFn(torch.autograd.Function):
@@ -263,13 +292,14 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gb, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, wv_bf16, dil: int, packed=None,
-                tail: bool = False, cp=None, tok=None, emb=None):
+                tail: bool = False, cp=None, tok=None, emb=None, emb_grad: bool = False):
         """``packed``: (wpn, wtn, wpw, wtw) weight images already built for this step (pack_batch);
         ``tail``: the first block (its backward ends the step: the conv weight gradient gets every CU);
         ``cp``: a :class:`..parallel.cp_fused.CPShard` -- ``x`` is this rank's slice of the sequence, the
         conv reads the neighbours' halo rows and the (L, C) LayerNorm statistics are group-wide;
         ``tok`` / ``emb``: ``x`` is the embedding bf16(emb[tok]) (the first block): the conv weight gradient
-        goes through the token one-hot (:func:`_wgrad_tok`)."""
+        goes through the token one-hot (:func:`_wgrad_tok`); ``emb_grad``: ``x`` carries no autograd
+        history and the backward returns ``emb``'s gradient instead of ``x``'s (:data:`EMBED_FOLD`)."""
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2)
         ctx.cp = cp
         if cp is not None:
@@ -335,6 +365,9 @@ class LocalBlockFn(torch.autograd.Function):
                               wl_b, wv_bf16, g1, be1, g2)
         ctx.hlo = hlo
         ctx.tok = (tok, emb) if cp is None and wgrad_tok_ok(tok, emb, L, KS) else None
+        ctx.emb_grad = bool(emb_grad)
+        if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
+            raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
         ctx.tail = bool(tail) and WGRAD_TAIL_FULL
         ctx.set_materialize_grads(False)
@@ -427,7 +460,7 @@ class LocalBlockFn(torch.autograd.Function):
                 _lib.call("pbx_colsum_add", slab.data_ptr(), rows, CH * CH, dwl.data_ptr(), None, st)
                 _lib.call("pbx_colsum_add", slab[rows * CH * CH:].data_ptr(), rows, CH, dbl.data_ptr(), None, st)
             streams.launch(dev, fold, keep=[fslab], name="wgrad")
-        dx = torch.empty_like(x)
+        dx = None if ctx.emb_grad else torch.empty_like(x)
         dpn = torch.empty_like(x)
         dpw = torch.empty_like(x)
         if cp is not None:
@@ -451,7 +484,12 @@ class LocalBlockFn(torch.autograd.Function):
             streams.fork(dev, "ann")
         dg_aux = (DGRAD_STREAM and cp is None and not ctx.tail and streams.ENABLED and not streams.GLOBAL_ENABLED
                   and dev.type == "cuda")
-        if dg_aux:
+        demb = None
+        if ctx.emb_grad:
+            # first block, folded: no conv data gradient (the conv part of dE comes with the weight gradient)
+            demb, dE_direct = embed_fold_bwd(*ctx.tok, ds1, pre_n, pre_w, dpn, dpw, params[0], params[2], stream)
+            dE = demb[2]
+        elif dg_aux:
             streams.launch(dev, lambda: conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil,
                                                    _lib.stream_ptr(dev)),
                            keep=[ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw], name="dg")
@@ -465,14 +503,16 @@ class LocalBlockFn(torch.autograd.Function):
                        KS, dil, stream, hlo, hlo)
         if ctx.tok is not None:
             tok, emb = ctx.tok
-            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)])   # noqa: E731
-            keep = [dpn, dpw, tok]
+            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)], demb)   # noqa: E731
+            keep = [dpn, dpw, tok] + ([demb[2]] if demb is not None else [])
         else:
             wg = lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)],   # noqa: E731
                                 ctx.tail and streams.ENABLED, hlo, hlo)
             keep = [dpn, dpw, x_ext]
         direct = [p for p, (_, d) in zip(params, dsts) if d]
-        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
+        if demb is not None and dE_direct:
+            direct.append(ctx.tok[1])
+        if all(dsts[i][1] for i in (0, 1, 2, 3)) and (demb is None or dE_direct) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
             if WGRAD_DEFER and not ctx.tail and cp is None and dev.type == "cuda":
@@ -490,7 +530,19 @@ class LocalBlockFn(torch.autograd.Function):
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else g for (g, d) in dsts]
-        return (dx, dgb, *pgrads, None, None, None, None, None, None, None)
+        gemb = dE if demb is not None and not dE_direct else None
+        return (dx, dgb, *pgrads, None, None, None, None, None, None, gemb, None)
+
+
+def embed_tokens(tokens: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """bf16(weight[tokens]) without autograd history (the folded first block returns the weight's
+    gradient itself, :data:`EMBED_FOLD`)."""
+    B, L = tokens.shape
+    tok = tokens.contiguous()
+    out = torch.empty((B, L, weight.shape[1]), dtype=torch.bfloat16, device=tokens.device)
+    _lib.call("pbx_embed_fwd", tok.data_ptr(), weight.detach().contiguous().data_ptr(), out.data_ptr(), B * L,
+              _lib.stream_ptr(tokens.device))
+    return out
 
 
 class EmbedFn(torch.autograd.Function):
@@ -560,10 +612,11 @@ def conv_images(wn: torch.Tensor, ww: torch.Tensor):
 
 
 def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool = False,
-                cp=None, tok=None, emb=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                cp=None, tok=None, emb=None, emb_grad: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
     """Run the fused local track of ``blk`` (a ``ProteinBERTBlock``); ``tail``: it is the first block;
     ``cp``: context-parallel shard (:class:`..parallel.cp_fused.CPShard`); ``tok`` / ``emb``: ``x`` is
-    the token embedding bf16(emb[tok])."""
+    the token embedding bf16(emb[tok]); ``emb_grad``: the backward returns ``emb``'s gradient (``x``
+    from :func:`embed_tokens`, no autograd history)."""
     att = blk.global_attention_layer
     wv = _wv_bf16(att)                                                       # [H*vd, C]
     nc = blk.local_narrow_conv_layer[0]
@@ -571,4 +624,4 @@ def local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None, tail: bool 
     return LocalBlockFn.apply(x, gb, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight, blk.local_linear_layer[0].bias,
                               blk.local_norm_2.weight, blk.local_norm_2.bias, wv, blk.wide_conv_dilation, packed,
-                              tail, cp, tok, emb)
+                              tail, cp, tok, emb, emb_grad)

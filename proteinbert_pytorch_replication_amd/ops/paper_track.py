@@ -29,7 +29,7 @@ from .gemm import gemm as _gemm
 from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
                            addmm_into)
 from .local_track import (CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad,
-                          _wgrad_tok, wgrad_tok_ok)
+                          _wgrad_tok, embed_fold_bwd, wgrad_tok_ok)
 
 _P, _I, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_float
 _lib.register("pbx_pc_ln_linear_fwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
@@ -81,7 +81,7 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gb, g, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv, mask, dil: int, packed=None,
-                tok=None, emb=None):
+                tok=None, emb=None, emb_grad: bool = False):
         from .paper_attention import KEY_DIM, VALUE_DIM, _nsplit
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv)
         B, L, C = x.shape
@@ -140,6 +140,11 @@ class PaperBlockFn(torch.autograd.Function):
         ctx.fused = fused
         # the first block: x = bf16(emb[tok]), the conv weight gradient goes through the token one-hot
         ctx.tok = (tok, emb) if wgrad_tok_ok(tok, emb, L, KS) else None
+        # emb_grad: x has no autograd history; the backward folds the conv data gradient into emb's
+        # gradient (local_track.EMBED_FOLD)
+        ctx.emb_grad = bool(emb_grad)
+        if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
+            raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
         ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
                               wq_cat)
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
@@ -221,34 +226,44 @@ class PaperBlockFn(torch.autograd.Function):
         dgb = dgbp.sum(dim=1)
         if streams.GLOBAL_ENABLED:
             streams.fork(dev, "global")
-        dx, dpn, dpw = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
-        conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
+        dpn, dpw = torch.empty_like(x), torch.empty_like(x)
+        demb, dE_direct, dx = None, True, None
+        if ctx.emb_grad:
+            demb, dE_direct = embed_fold_bwd(*ctx.tok, ds1, pre_n, pre_w, dpn, dpw, wn, ww, stream)
+        else:
+            dx = torch.empty_like(x)
+            conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
         if ctx.tok is not None:
             tok, emb = ctx.tok
-            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)])   # noqa: E731
+            wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)], demb)   # noqa: E731
         else:
             wg = lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])      # noqa: E731
-        if all(dsts[i][1] for i in (0, 1, 2, 3)) and streams.ENABLED:
-            streams.launch(dev, wg, keep=[dpn, dpw, x], name="wgrad")
+        if all(dsts[i][1] for i in (0, 1, 2, 3)) and dE_direct and streams.ENABLED:
+            streams.launch(dev, wg, keep=[dpn, dpw, x] + ([demb[2]] if demb is not None else []), name="wgrad")
         else:
             wg()
         direct = [p for p, (_, d) in zip(params, dsts) if d]
+        if demb is not None and dE_direct:
+            direct.append(ctx.tok[1])
         if direct:
             notify_grads_ready(direct)
         pgrads = [None if d else gr for (gr, d) in dsts]
-        return (dx, dgb, dg, *pgrads, None, None, None, None, None)
+        gemb = demb[2] if demb is not None and not dE_direct else None
+        return (dx, dgb, dg, *pgrads, None, None, None, None, gemb, None)
 
 
-def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None, tok=None, emb=None):
+def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None, tok=None, emb=None,
+                emb_grad: bool = False):
     """``(h2, o)`` of one paper-semantics block's local track + attention (fused HIP path); ``tok`` /
-    ``emb``: ``x`` is the token embedding bf16(emb[tok]) (the first block)."""
+    ``emb``: ``x`` is the token embedding bf16(emb[tok]) (the first block); ``emb_grad``: the backward
+    returns ``emb``'s gradient (``x`` without autograd history, local_track.EMBED_FOLD)."""
     nc = blk.local_narrow_conv_layer[0]
     wc = blk.local_wide_conv_layer[0]
     att = blk.global_attention_layer
     return PaperBlockFn.apply(x, gb, g, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
                               blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
-                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed, tok, emb)
+                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed, tok, emb, emb_grad)
 
 
 def paper_local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> torch.Tensor:

@@ -197,13 +197,21 @@ def test_wgrad_token_onehot_vs_fp32(B, L, dil):
     dpn = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     dpw = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     outs = [(torch.zeros(128, 128, 9, device="cuda"), torch.zeros(128, device="cuda")) for _ in range(2)]
-    _wgrad_tok(dpn, dpw, tok, E, dil, B, L, outs)
+    Wn, Ww = torch.randn(128, 128, 9, device="cuda") * 0.05, torch.randn(128, 128, 9, device="cuda") * 0.05
+    dE = torch.zeros(V, 128, device="cuda")
+    _wgrad_tok(dpn, dpw, tok, E, dil, B, L, outs, demb=(Wn, Ww, dE))
     torch.cuda.synchronize()
     x = E.to(torch.bfloat16).float()[tok].transpose(1, 2)                       # [B, 128, L]
-    for (dw, db), dp, d in ((outs[0], dpn, 1), (outs[1], dpw, dil)):
+    dx = torch.zeros(B, 128, L, device="cuda")
+    for (dw, db), dp, d, Wc in ((outs[0], dpn, 1, Wn), (outs[1], dpw, dil, Ww)):
         ref = torch.nn.grad.conv1d_weight(x, (128, 128, 9), dp.float().transpose(1, 2), padding=4 * d, dilation=d)
         assert rel(dw, ref) < 1e-5, rel(dw, ref)
         assert rel(db, dp.float().sum(dim=(0, 1))) < 1e-5
+        dx += torch.nn.grad.conv1d_input(x.shape, Wc.to(torch.bfloat16).float(), dp.float().transpose(1, 2),
+                                         padding=4 * d, dilation=d)
+    # the embedding gradient's conv part (first-block fold): sum over positions with token v of conv^T dpre
+    dE_ref = torch.zeros(V, 128, device="cuda").index_add_(0, tok.reshape(-1), dx.transpose(1, 2).reshape(-1, 128))
+    assert rel(dE, dE_ref) < 1e-5, rel(dE, dE_ref)
 
 
 @pytest.mark.parametrize("nblocks", [2, 3])
@@ -265,3 +273,44 @@ def test_arena_direct_grads_match_autograd_path():
         err = (direct[n] - ref[n]).norm().item()
         print(f"{n:60s} |g|={ref[n].norm().item():.3e} err={err:.3e}")
         assert err < 3e-2 * ref[n].norm().item() + 1e-4 * scale, f"{n}: err {err:.3e} |g| {ref[n].norm().item():.3e}"
+
+
+@pytest.mark.parametrize("arena,det,semantics", [(True, False, "reference"), (False, False, "reference"),
+                                                 (True, True, "reference"), (True, False, "paper")])
+def test_embed_fold_matches_data_gradient_path(arena, det, semantics, monkeypatch):
+    """First block with its conv data gradient folded into the embedding gradient (local_track.EMBED_FOLD:
+    pbx_embed_dpre + the E-space conv term of pbx_wgrad_tok) vs conv_dgrad4 + embedding backward: same
+    gradients (the fold sums fp32 dS1 + bf16(W)-weighted one-hot sums instead of a bf16-rounded dx)."""
+    from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
+    from proteinbert_pytorch_replication_amd.ops import local_track
+    from proteinbert_pytorch_replication_amd.utils import determinism
+    from proteinbert_pytorch_replication_amd.train.optim import FusedAdam
+    from proteinbert_pytorch_replication_amd.train.step import PretrainStep
+    L, A = 256, 512
+    X, Y, W = SyntheticUniRefGO(L, A, 6, "cuda", seed=9).next_batch()
+    grads = []
+    monkeypatch.setitem(determinism._STATE, "on", det)       # the fused kernels' fixed-order forms only
+    for fold in (False, True):
+        monkeypatch.setattr(local_track, "EMBED_FOLD", fold)
+        torch.manual_seed(0)
+        m = ProteinBERT(sequences_length=L, num_annotations=A, local_dim=128, global_dim=512, key_dim=64,
+                        num_heads=4, num_blocks=2, device="cuda", backend="hip", semantics=semantics)
+        step = PretrainStep(m, FusedAdam(m.parameters(), lr=1e-3)) if arena else None
+        if arena:
+            step.optimizer.zero_grad()
+            step.loss(X, Y, W).backward()
+        else:
+            from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss
+            fused_pretrain_loss(m, X, Y, W).backward()
+        from proteinbert_pytorch_replication_amd.ops import streams
+        streams.join()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().float().clone() for n, p in m.named_parameters() if p.grad is not None})
+    g0, g1 = grads
+    assert set(g0) == set(g1)
+    for n in g0:
+        err = (g0[n] - g1[n]).norm().item()
+        ref = g0[n].norm().item()
+        print(f"{n:60s} |g|={ref:.3e} err={err:.3e}")
+        tol = 2e-2 if n == "local_embedding.weight" else 1e-3
+        assert err <= tol * ref + 1e-6, (n, err, ref)
