@@ -55,6 +55,8 @@ _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
+_lib.register("pbx_conv_dgrad4f", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
+                                    _F, _P])
 _lib.register("pbx_embed_dpre", [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P, _P])
 _lib.register("pbx_embed_bwd_groups", [_L])
 
@@ -185,6 +187,10 @@ LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
 # (profiles/r4_dgrad_stream_ab.txt): the one-launch global backward (8-wave workgroups) only finds CUs as
 # conv_dgrad4's 2-per-CU workgroups drain and stretches from 51 to ~210 us.  Off.
 DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "0") == "1"
+# the LN1 backward finalize fused into the conv data gradient (csrc/conv4.hip conv_dgrad4<FIN>): dS1 is
+# computed in the staging pass and never stored (PBX_DGRAD_FIN=0: ln1_finalize + conv_dgrad4); not in the
+# deterministic mode (its dgb column sums are float atomics per tile) nor under context parallelism
+DGRAD_FIN = os.environ.get("PBX_DGRAD_FIN", "1") != "0"
 # PBX_WGRAD_DEFER=1: a block's conv weight gradient (aux stream) is launched after the NEXT block's pool
 # backward instead of right after its own data gradient, so it overlaps the LN2 / MLP backward, the LN1
 # finalize and the data gradient rather than the memory-bound pool backward (experiment, off by default)
@@ -465,27 +471,40 @@ class LocalBlockFn(torch.autograd.Function):
         dpw = torch.empty_like(x)
         if cp is not None:
             cp.fix_sums(sums1)
-        # LN1 finalize (ds1) + gradient of the broadcast global->local vector
-        ds1 = torch.empty_like(x)
-        _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
-                  TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, int(fused_deterministic()),
-                  stream)
-        if cp is not None:
-            cp.all_reduce_(dgb)                 # gb is replicated: its gradient sums every shard's positions
-        if streams.GLOBAL_ENABLED:
-            # the previous block's global-track backward (next autograd node, aux stream) needs only
-            # dgb: let it start here, beside the conv data gradient below
-            streams.fork(dev, "global")
-        if ctx.tail and INPUT_BWD_EARLY and streams.ENABLED and dev.type == "cuda":
-            # first block: the input layer's backward (the last autograd node but one) needs only dgb and
-            # the global-track gradient, both final here -- it runs on the "ann" stream beside this conv
-            # data gradient, so its 18 MB weight-gradient bucket is ready ~0.2 ms earlier for the DP
-            # all-reduce (ops/global_track.py InputLayerFn.backward)
-            streams.fork(dev, "ann")
         dg_aux = (DGRAD_STREAM and cp is None and not ctx.tail and streams.ENABLED and not streams.GLOBAL_ENABLED
                   and dev.type == "cuda")
+        # the LN1 finalize fused into the conv data gradient (DGRAD_FIN; its dgb is final only after it)
+        fin = (DGRAD_FIN and cp is None and not ctx.emb_grad and not dg_aux and CONV_DGRAD4 and KS == 9
+               and dev.type == "cuda" and not fused_deterministic())
+
+        def dgb_ready():
+            if streams.GLOBAL_ENABLED:
+                # the previous block's global-track backward (next autograd node, aux stream) needs only
+                # dgb: let it start here, beside the conv data gradient below
+                streams.fork(dev, "global")
+            if ctx.tail and INPUT_BWD_EARLY and streams.ENABLED and dev.type == "cuda":
+                # first block: the input layer's backward (the last autograd node but one) needs only dgb
+                # and the global-track gradient, both final here -- it runs on the "ann" stream beside this
+                # conv data gradient, so its 18 MB weight-gradient bucket is ready ~0.2 ms earlier for the
+                # DP all-reduce (ops/global_track.py InputLayerFn.backward)
+                streams.fork(dev, "ann")
+
+        if not fin:
+            # LN1 finalize (ds1) + gradient of the broadcast global->local vector
+            ds1 = torch.empty_like(x)
+            _lib.call("pbx_ln1_finalize", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+                      TS1, g1.data_ptr(), ds1.data_ptr(), dgb.data_ptr(), B, L, LN_EPS, int(fused_deterministic()),
+                      stream)
+            if cp is not None:
+                cp.all_reduce_(dgb)             # gb is replicated: its gradient sums every shard's positions
+            dgb_ready()
         demb = None
-        if ctx.emb_grad:
+        if fin:
+            _lib.call("pbx_conv_dgrad4f", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+                      TS1, g1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
+                      dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), dgb.data_ptr(), B, L, KS, dil, LN_EPS, stream)
+            dgb_ready()
+        elif ctx.emb_grad:
             # first block, folded: no conv data gradient (the conv part of dE comes with the weight gradient)
             demb, dE_direct = embed_fold_bwd(*ctx.tok, ds1, pre_n, pre_w, dpn, dpw, params[0], params[2], stream)
             dE = demb[2]

@@ -70,17 +70,19 @@ def test_local_block_forward(L, B, frozen):
 
 # pool backward: attn_bwd4 (weight-stationary, csrc/pool_bwd.hip) / attn_bwd2 (stored GELU' fragments, Wv in
 # LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup;
-# conv: 3 = conv_fwd3 + conv_dgrad4 (default), 4 = persistent conv_fwd4 + conv_dgrad4, 2 = conv_fwd3 + conv_dgrad3
+# conv: 3 = conv_fwd3 + conv_dgrad4 with the LN1 finalize fused in (default), 5 = the same with a separate
+# ln1_finalize, 4 = persistent conv_fwd4 + conv_dgrad4, 2 = conv_fwd3 + conv_dgrad3
 @pytest.mark.parametrize("recompute,wide,bwd4,tpw,conv", [(0, 1, 1, 0, 3), (0, 1, 1, 3, 3), (0, 1, 1, 16, 3),
                                                           (0, 1, 0, 0, 3),
                                                           (1, 1, 0, 0, 3), (1, 0, 0, 0, 3), (0, 1, 1, 0, 4),
-                                                          (0, 1, 1, 0, 2)])
+                                                          (0, 1, 1, 0, 2), (0, 1, 1, 0, 5)])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
 def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     monkeypatch.setattr(local_track, "CONV_FWD4", int(conv == 4))
     monkeypatch.setattr(local_track, "CONV_DGRAD4", int(conv != 2))
+    monkeypatch.setattr(local_track, "DGRAD_FIN", conv != 5)
     monkeypatch.setattr(local_track, "POOL_RECOMPUTE", recompute)
     monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
     monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
@@ -314,3 +316,31 @@ def test_embed_fold_matches_data_gradient_path(arena, det, semantics, monkeypatc
         print(f"{n:60s} |g|={ref:.3e} err={err:.3e}")
         tol = 2e-2 if n == "local_embedding.weight" else 1e-3
         assert err <= tol * ref + 1e-6, (n, err, ref)
+
+
+@pytest.mark.parametrize("L,B", [(512, 4), (300, 3), (64, 5)])
+def test_dgrad_fin_matches_separate_finalize(L, B, monkeypatch):
+    """conv_dgrad4 with the LN1 backward finalize fused in (local_track.DGRAD_FIN) vs ln1_finalize +
+    conv_dgrad4: the same dS1 formula and bf16 rounding, so the block's gradients agree to float-atomic
+    order (dgb column sums)."""
+    from proteinbert_pytorch_replication_amd.ops import local_track
+    from proteinbert_pytorch_replication_amd.ops.local_track import local_block
+    m, blk = make_block(L, seed=3)
+    torch.manual_seed(L + B)
+    x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
+    gb0 = torch.randn(B, 128, device="cuda") * 0.5
+    dh = torch.randn(B, L, 128, device="cuda")
+    dv = torch.randn(B, 512, device="cuda") * 1e-2
+    params = [blk.local_narrow_conv_layer[0].weight, blk.local_wide_conv_layer[0].weight, blk.local_norm_1.weight,
+              blk.local_norm_1.bias, blk.local_linear_layer[0].weight]
+    out = []
+    for fin in (False, True):
+        monkeypatch.setattr(local_track, "DGRAD_FIN", fin)
+        x = x0.clone().requires_grad_(True)
+        gb = gb0.clone().requires_grad_(True)
+        h2, vpart = local_block(x, gb, blk)
+        loss = (h2.float() * dh).sum() + (vpart.sum(1) * dv).sum()
+        out.append(torch.autograd.grad(loss, [x, gb] + params))
+    torch.cuda.synchronize()
+    for n, a, b in zip(["x", "gb", "wn", "ww", "g1", "be1", "wl"], *out):
+        assert rel(b, a) < 2e-3, f"{n}: {rel(b, a):.3e}"
