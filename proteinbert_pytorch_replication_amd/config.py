@@ -123,8 +123,8 @@ PRESETS: Dict[str, RunConfig] = {
                           num_heads=4, num_blocks=2),
         kernel=KernelConfig(backend="torch", dtype="fp32"),
         train=TrainConfig(batch_size=4)),
-    # Per-GPU batches are sized for throughput on a 288 GB MI355X (~17 MiB of bf16 activations per
-    # L=512 sequence): at 256 sequences many fused kernels still run only 1-2 work items per wave
+    # Per-GPU batches are sized for throughput on a 288 GB MI355X (~9 MiB of activations per L=512
+    # sequence, 9.0 GiB peak at 1024): at 256 sequences many fused kernels still run only 1-2 work items per wave
     # (latency-bound); 512 fills the chip, and 1024 amortises the step's fixed part (weight-gradient
     # reductions, the optimizer, launch tails; ~0.9 ms of a 6.3 ms B=512 step).  Round-4 same-box
     # sweep: B=512 81.3k, 1024 87.1-87.5k, 1536 88.9k, 2048 90.0k seq/s (profiles/r4_batch_sweep.txt).
