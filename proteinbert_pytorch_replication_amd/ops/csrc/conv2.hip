@@ -58,7 +58,8 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
     bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
-    float* __restrict__ stats, int L, int KS, int dil) {
+    float* __restrict__ stats, int L, int KS, int dil, const long long* __restrict__ tok,
+    const bf16_t* __restrict__ emb) {
   constexpr int TBM = BM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
@@ -87,12 +88,16 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   fr[1] = fw[256 + lane];
   fr[2] = fw[512 + lane];
   if (tid < 3 * CH) bsm[tid] = tid < CH ? bn[tid] : tid < 2 * CH ? bw[tid - CH] : gb[(size_t)b * CH + tid - 2 * CH];
+  // tok != nullptr (the first block, pbx_conv_fwd3t): the input rows are the embedding rows emb[tok]
+  // (bf16 [V][128]), gathered here -- the [B, L, 128] embedding output is never materialised
+  const long long* toks = tok != nullptr ? tok + (size_t)b * L : nullptr;
   stage_chunks(
       XR * 16,
       [&](int idx) {
         const int pos = pos0 - halo + (idx >> 4);
-        return (pos >= 0 && pos < L) ? *reinterpret_cast<const uint4*>(xsmp + (size_t)pos * CH + (idx & 15) * 8)
-                                     : make_uint4(0u, 0u, 0u, 0u);
+        if (pos < 0 || pos >= L) return make_uint4(0u, 0u, 0u, 0u);
+        const bf16_t* row = toks != nullptr ? emb + (size_t)toks[pos] * CH : xsmp + (size_t)pos * CH;
+        return *reinterpret_cast<const uint4*>(row + (idx & 15) * 8);
       },
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
   __syncthreads();
@@ -495,9 +500,9 @@ static void set_conv3_attrs() {
 // fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels; gb [B][128] fp32.
 // pre_n / pre_w: GELU'(pre-activation) of the narrow / wide conv as bf16 (what conv_dgrad3 multiplies the
 // incoming gradient by), or both null (inference: no backward reads them).
-PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
-                             int dil, hipStream_t st) {
+static int conv_fwd3_launch(const void* x, const long long* tok, const void* emb, const void* fwn, const void* fww,
+                            const float* bn, const float* bw, const float* gb, void* pre_n, void* pre_w, void* s1,
+                            float* stats, int B, int L, int KS, int dil, hipStream_t st) {
   set_conv3_attrs();
   const int lds = fwd3_lds(KS, dil, BM);
   if (lds > 163840 || dil < 1 || KS < 2 || gb == nullptr) return (int)hipErrorInvalidValue;
@@ -505,8 +510,24 @@ PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, co
   if ((pre_n == nullptr) != (pre_w == nullptr)) return (int)hipErrorInvalidValue;
   const auto kern = pre_n != nullptr ? conv_fwd3_kernel<true> : conv_fwd3_kernel<false>;
   hipLaunchKernelGGL(kern, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
-                     (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil);
+                     (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil,
+                     tok, (const bf16_t*)emb);
   return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
+                             int dil, hipStream_t st) {
+  return conv_fwd3_launch(x, nullptr, nullptr, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st);
+}
+
+// The first block (reference modules.py:249-253,300 feeding :185-212): x = emb[tok] gathered in the
+// staging pass (tok [B][L] int64 < V, emb [V][128] bf16); otherwise pbx_conv_fwd3.
+PBX_EXPORT int pbx_conv_fwd3t(const long long* tok, const void* emb, const void* fwn, const void* fww, const float* bn,
+                              const float* bw, const float* gb, void* pre_n, void* pre_w, void* s1, float* stats,
+                              int B, int L, int KS, int dil, hipStream_t st) {
+  if (tok == nullptr || emb == nullptr) return (int)hipErrorInvalidValue;
+  return conv_fwd3_launch(nullptr, tok, emb, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st);
 }
 
 PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* pre_w, const void* ftn,

@@ -73,7 +73,12 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     # the first block folds its conv data gradient into the embedding gradient (local_track.EMBED_FOLD)
     fold = (_lt.EMBED_FOLD and cp is None and tokens.device.type == "cuda" and len(blocks) > 0
             and wgrad_tok_ok(tok_c, emb_w, tokens.shape[1], blocks[0].local_narrow_conv_layer[0].weight.shape[2]))
-    h = embed_tokens(tok_c, emb_w) if fold else EmbedFn.apply(tokens, emb_w)    # [B,L,128] bf16
+    # [B,L,128] bf16; reference semantics folded: no embedding tensor at all, the first conv gathers
+    # emb[tok] in its staging pass (pbx_conv_fwd3t)
+    if fold and not paper and _lt.EMBED_GATHER:
+        h = None
+    else:
+        h = embed_tokens(tok_c, emb_w) if fold else EmbedFn.apply(tokens, emb_w)
     mask = (tokens != 0).contiguous() if paper else None
     # every weight image the fused kernels read this step, built by one launch
     items, conv_imgs, glob_imgs = [], [], []

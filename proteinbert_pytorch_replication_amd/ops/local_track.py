@@ -55,6 +55,7 @@ _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
+_lib.register("pbx_conv_fwd3t", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4f", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                     _F, _P])
 _lib.register("pbx_embed_dpre", [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P, _P])
@@ -246,6 +247,9 @@ WGRAD_TOK = os.environ.get("PBX_WGRAD_TOK", "1") != "0"
 # (pbx_embed_dpre), the conv^T part as bf16(W)-weighted sums of the weight gradient's one-hot S
 # (pbx_wgrad_tok).  PBX_EMBED_FOLD=0: conv data gradient + embedding backward as for any block.
 EMBED_FOLD = os.environ.get("PBX_EMBED_FOLD", "1") != "0"
+# ... and (reference semantics) its conv gathers emb[tok] in the staging pass: the [B, L, 128] embedding
+# output is never written (PBX_EMBED_GATHER=0: embed_fwd + conv_fwd3)
+EMBED_GATHER = os.environ.get("PBX_EMBED_GATHER", "1") != "0"
 
 
 def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: int, KS: int) -> bool:
@@ -311,13 +315,21 @@ class LocalBlockFn(torch.autograd.Function):
         if cp is not None:
             # this shard's rows of the [L, C] LayerNorm affine (contiguous row slices of the parameters)
             g1, be1, g2, be2 = (cp.rows(t) for t in (g1, be1, g2, be2))
-        B, L, C = x.shape
-        assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
+        if x is None:
+            # the first block, folded (emb_grad): the conv gathers emb[tok] itself (pbx_conv_fwd3t)
+            if not (emb_grad and tok is not None and emb is not None and cp is None):
+                raise ValueError("x may be None only for the folded first block (emb_grad with tok / emb)")
+            B, L = tok.shape
+            xt = torch.empty((B, L, CH), dtype=torch.bfloat16, device=tok.device)   # shape template only
+        else:
+            B, L, C = x.shape
+            assert C == CH and x.dtype == torch.bfloat16 and x.is_contiguous()
+            xt = x
         NJ = wv_bf16.shape[0]
         if not attn_pool_supported(NJ):
             raise NotImplementedError(f"HIP attention pool: H * value_dim = {NJ} (kernels built for 256 / 512)")
         KS = wn.shape[2]
-        dev = x.device
+        dev = xt.device
         stream = _lib.stream_ptr(dev)
         T1 = (L + BM1 - 1) // BM1
         T2 = (L + PB - 1) // PB
@@ -330,27 +342,33 @@ class LocalBlockFn(torch.autograd.Function):
         # inference / frozen-encoder forwards keep no backward state: the conv pre-activations, the MLP
         # pre-activation and the pool's GELU' fragments are not written at all
         need_bwd = any(ctx.needs_input_grad)
-        pre_n = torch.empty_like(x) if need_bwd else None
-        pre_w = torch.empty_like(x) if need_bwd else None
-        s1 = torch.empty_like(x)
+        pre_n = torch.empty_like(xt) if need_bwd else None
+        pre_w = torch.empty_like(xt) if need_bwd else None
+        s1 = torch.empty_like(xt)
         st1 = torch.empty((B, T1, 2), dtype=torch.float32, device=dev)
         gb = gb.detach().float().contiguous()
-        if cp is None:
+        if x is None:
+            x_ext, hlo = None, 0
+            emb_b = emb.detach().to(torch.bfloat16).contiguous()
+            _lib.call("pbx_conv_fwd3t", tok.data_ptr(), emb_b.data_ptr(), wpn.data_ptr(), wpw.data_ptr(),
+                      bn.data_ptr(), bw.data_ptr(), gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(),
+                      st1.data_ptr(), B, L, KS, dil, stream)
+        elif cp is None:
             x_ext, hlo = x, 0
             conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream)
         else:
             x_ext, hlo = cp.halo_rows(x), cp.halo
             conv_fwd(x_ext, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream, hlo, hlo)
             cp.fix_stats(st1, BM1)
-        pre_l = torch.empty_like(x) if need_bwd else None
-        s2 = torch.empty_like(x)
+        pre_l = torch.empty_like(xt) if need_bwd else None
+        s2 = torch.empty_like(xt)
         st2 = torch.empty((B, T2, 2), dtype=torch.float32, device=dev)
         _lib.call("pbx_ln_linear_fwd", s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(), be1.data_ptr(),
                   wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS, stream)
         if cp is not None:
             cp.fix_stats(st2, PB)
         TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
-        h2 = torch.empty_like(x)
+        h2 = torch.empty_like(xt)
         vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
         recompute = need_bwd and POOL_RECOMPUTE and POOL_PRENORM
         if need_bwd:
@@ -372,7 +390,7 @@ class LocalBlockFn(torch.autograd.Function):
         ctx.hlo = hlo
         ctx.tok = (tok, emb) if cp is None and wgrad_tok_ok(tok, emb, L, KS) else None
         ctx.emb_grad = bool(emb_grad)
-        if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
+        if ctx.emb_grad and (ctx.tok is None or (x is not None and x.requires_grad)):
             raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
         ctx.meta = (B, L, KS, dil, T1, T2, NJ)
         ctx.tail = bool(tail) and WGRAD_TAIL_FULL

@@ -344,3 +344,36 @@ def test_dgrad_fin_matches_separate_finalize(L, B, monkeypatch):
     torch.cuda.synchronize()
     for n, a, b in zip(["x", "gb", "wn", "ww", "g1", "be1", "wl"], *out):
         assert rel(b, a) < 2e-3, f"{n}: {rel(b, a):.3e}"
+
+
+@pytest.mark.parametrize("B,L", [(3, 512), (2, 300)])
+def test_conv_fwd_token_gather_matches_embedding_input(B, L):
+    """The first block's conv with the embedding gathered in its staging pass (pbx_conv_fwd3t) writes the
+    same s1 / GELU' / LayerNorm partials, bitwise, as conv_fwd3 over the materialised bf16(E[tok])."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
+    from proteinbert_pytorch_replication_amd.ops.local_track import BM1, conv_fwd, pack_conv
+    torch.manual_seed(B * L)
+    dev = "cuda"
+    E = torch.randn(26, 128, device=dev)
+    tok = torch.randint(0, 26, (B, L), device=dev)
+    wn, ww = torch.randn(128, 128, 9, device=dev) * 0.05, torch.randn(128, 128, 9, device=dev) * 0.05
+    bn, bw, gb = torch.randn(128, device=dev), torch.randn(128, device=dev), torch.randn(B, 128, device=dev)
+    (wpn, _), (wpw, _) = pack_conv(wn), pack_conv(ww)
+    T1 = (L + BM1 - 1) // BM1
+    outs = []
+    for gather in (False, True):
+        o = [torch.empty(B, L, 128, dtype=torch.bfloat16, device=dev) for _ in range(3)]
+        st1 = torch.empty(B, T1, 2, device=dev)
+        st = _lib.stream_ptr(torch.device(dev))
+        if gather:
+            eb = E.to(torch.bfloat16).contiguous()
+            _lib.call("pbx_conv_fwd3t", tok.data_ptr(), eb.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(),
+                      bw.data_ptr(), gb.data_ptr(), o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), st1.data_ptr(),
+                      B, L, 9, 5, st)
+        else:
+            x = E.to(torch.bfloat16)[tok].contiguous()
+            conv_fwd(x, wpn, wpw, bn, bw, gb, o[0], o[1], o[2], st1, B, L, 9, 5, st)
+        outs.append(o + [st1])
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
