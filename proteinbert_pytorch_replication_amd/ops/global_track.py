@@ -624,6 +624,10 @@ class GlobalBlockFn(torch.autograd.Function):
         return (dg, None, dvpart, *gr.finish())
 
 
+# the GO head's forward on the "head" aux stream beside the local head (PBX_HEAD_AUX=0: in sequence)
+HEAD_AUX = os.environ.get("PBX_HEAD_AUX", "1") != "0"
+
+
 class HeadsLossFn(torch.autograd.Function):
     """Both pretraining heads + the reference loss (``utils.py:293-294``), reference semantics.
 
@@ -641,8 +645,22 @@ class HeadsLossFn(torch.autograd.Function):
         V = wo.shape[0]
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
-        dh, dzl, dbo_part = local_head_forward(h, wo, bo, y_l, w_l, loss[0:1])
-        dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
+        if HEAD_AUX and streams.ENABLED and dev.type == "cuda":
+            # the GO head (GEMM + VALU-heavy BCE epilogue) on its own stream beside the memory-bound
+            # local head; the loss sum waits for both
+            res = []
+
+            def go():
+                res.append(go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:]))
+                return list(res[0])
+
+            streams.launch(dev, go, keep=[g2_bf, wa, ba, y_g, w_g, loss], name="head")
+            dh, dzl, dbo_part = local_head_forward(h, wo, bo, y_l, w_l, loss[0:1])
+            streams.wait_for(dev, "head")
+            dz, dba, gx = res[0]
+        else:
+            dh, dzl, dbo_part = local_head_forward(h, wo, bo, y_l, w_l, loss[0:1])
+            dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
         ctx.save_for_backward(dh, dzl, dbo_part, h, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)
         ctx.V = V
