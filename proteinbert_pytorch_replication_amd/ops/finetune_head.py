@@ -1,11 +1,10 @@
 """Per-residue fine-tuning head on MI355X (BASELINE cfg 5).
 
 ``logits = h Wᵀ + b`` over ``[B*L, 128]`` bf16 encoder rows and K <= 16 classes.  The head weight
-stays an fp32 parameter and the logits keep fp32 accuracy: W is split into two bf16 terms
-``W = W_hi + W_lo`` (``W_lo = bf16(W - W_hi)``, together exact to ~2^-17 relative) and the bf16
-encoder output (exact in fp32) meets both in two bf16 GEMMs accumulating in fp32 -- the same
-result as the fp32 ``F.linear`` on an upcast copy to ~1e-6 relative, at 2 x 22 us instead of 75 us
-at B*L = 262,144.  The weight gradient, a 262,144-long reduction that hipBLASLt ran at 230-410 us,
+stays an fp32 parameter and the logits keep fp32 accuracy: one streaming kernel (``csrc/finetune.hip``
+``token_head_fwd``, a thread per residue, W broadcast from LDS) runs fp32 FMAs over the exact bf16
+rows -- the fp32 ``F.linear`` result on an upcast copy, memory-bound on the 67 MB row read at
+B*L = 262,144 (round 3-4 used two library bf16 GEMMs on a hi / lo weight split, 2 x 25 us).  The weight gradient, a 262,144-long reduction that hipBLASLt ran at 230-410 us,
 is the streaming kernel in ``csrc/finetune.hip`` (fp32 accumulation, deterministic slab reduction);
 the input gradient (unfrozen encoders only) is fp32.
 """
@@ -20,6 +19,7 @@ from . import global_track  # noqa: F401  (registers pbx_colsum_add)
 
 _P, _I, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_long
 _lib.register("pbx_token_head_wgrad", [_P, _P, _P, _L, _I, _I, _P])
+_lib.register("pbx_token_head_fwd", [_P, _P, _P, _P, _L, _I, _P])
 
 
 def supported(h: torch.Tensor, n_classes: int) -> bool:
@@ -31,10 +31,12 @@ class TokenHeadFn(torch.autograd.Function):
     def forward(ctx, h, weight, bias):
         B, L, C = h.shape
         h2 = h.contiguous().view(B * L, C)
-        w_hi = weight.detach().to(torch.bfloat16)
-        w_lo = (weight.detach() - w_hi.float()).to(torch.bfloat16)
-        logits = torch.addmm(bias.float(), h2, w_hi.t(), out_dtype=torch.float32)
-        torch.addmm(logits, h2, w_lo.t(), out_dtype=torch.float32, out=logits)
+        K = weight.shape[0]
+        # one streaming pass: fp32 FMAs over the exact bf16 rows and fp32 weights (csrc/finetune.hip)
+        logits = torch.empty((B * L, K), dtype=torch.float32, device=h.device)
+        _lib.call("pbx_token_head_fwd", h2.data_ptr(), weight.detach().float().contiguous().data_ptr(),
+                  bias.detach().float().contiguous().data_ptr(), logits.data_ptr(), B * L, K,
+                  _lib.stream_ptr(h.device))
         ctx.save_for_backward(h2, weight)
         ctx.shape = (B, L)
         return logits.view(B, L, -1)
