@@ -277,9 +277,10 @@ def test_arena_direct_grads_match_autograd_path():
         assert err < 3e-2 * ref[n].norm().item() + 1e-4 * scale, f"{n}: err {err:.3e} |g| {ref[n].norm().item():.3e}"
 
 
-@pytest.mark.parametrize("arena,det,semantics", [(True, False, "reference"), (False, False, "reference"),
-                                                 (True, True, "reference"), (True, False, "paper")])
-def test_embed_fold_matches_data_gradient_path(arena, det, semantics, monkeypatch):
+@pytest.mark.parametrize("arena,det,semantics,L", [(True, False, "reference", 256), (False, False, "reference", 256),
+                                                   (True, True, "reference", 256), (True, False, "paper", 256),
+                                                   (True, False, "reference", 202)])
+def test_embed_fold_matches_data_gradient_path(arena, det, semantics, L, monkeypatch):
     """First block with its conv data gradient folded into the embedding gradient (local_track.EMBED_FOLD:
     pbx_embed_dpre + the E-space conv term of pbx_wgrad_tok) vs conv_dgrad4 + embedding backward: same
     gradients (the fold sums fp32 dS1 + bf16(W)-weighted one-hot sums instead of a bf16-rounded dx)."""
@@ -288,7 +289,7 @@ def test_embed_fold_matches_data_gradient_path(arena, det, semantics, monkeypatc
     from proteinbert_pytorch_replication_amd.utils import determinism
     from proteinbert_pytorch_replication_amd.train.optim import FusedAdam
     from proteinbert_pytorch_replication_amd.train.step import PretrainStep
-    L, A = 256, 512
+    A = 512                                      # L = 202: 1212 rows, not a multiple of the 256-row tiles
     X, Y, W = SyntheticUniRefGO(L, A, 6, "cuda", seed=9).next_batch()
     grads = []
     monkeypatch.setitem(determinism._STATE, "on", det)       # the fused kernels' fixed-order forms only
