@@ -6,7 +6,7 @@ import sys
 
 res = collections.defaultdict(lambda: collections.defaultdict(list))
 for d in sys.argv[1:]:
-    fs = glob.glob(f"gpurun_out/{d}/runc/*_counter_collection.csv")
+    fs = glob.glob(f"gpurun_out/{d}/**/*counter_collection.csv", recursive=True)
     if not fs:
         print("missing", d)
         continue
