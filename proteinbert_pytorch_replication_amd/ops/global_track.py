@@ -422,7 +422,7 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         g1_bf, g2_bf = e(B, G, dt=BF16), e(B, G, dt=BF16)
         pregl, gb = (e(B, NGL), e(B, NGL)) if NGL else (None, torch.zeros((B, 0), dtype=F32, device=dev))
         vp, TVk = vpart.contiguous(), TV
-        if TV >= 16:
+        if TV > 16:
             # long sequences: the attention-pool tile partials are summed by the whole chip first (the
             # fused kernel has only B / 16 workgroups; at L = 4096 each would stream 64 tile rows)
             vp, TVk = vp.sum(dim=1, keepdim=True), 1

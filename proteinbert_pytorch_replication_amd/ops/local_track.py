@@ -48,6 +48,8 @@ _lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, 
 _lib.register("pbx_attn_bwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
 _lib.register("pbx_attn_bwd4c", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _I, _I, _P, _P, _P])
 _lib.register("pbx_pack_wvt_frag", [_P, _P, _I, _P])
+_lib.register("pbx_pool_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
+_lib.register("pbx_pool_bwd", [_P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
@@ -86,6 +88,9 @@ POOL_CONSTS_FUSED = int(os.environ.get("PBX_POOL_CONSTS_FUSED", "1"))
 POOL_CONSTS_MIN_B: Optional[int] = None     # smallest batch for that form (None: two workgroups per CU)
 # attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
 POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
+# 1 (default): recompute-form pool (csrc/pool.hip: LN2 apply fused into the pool forward, GELU' recomputed in
+# the backward, no GELU' tensor); 0: the stored-GELU' kernels above
+POOL_V5 = int(os.environ.get("PBX_POOL_V5", "1"))
 
 
 def attn_pool_supported(NJ: int) -> bool:
@@ -367,26 +372,34 @@ class LocalBlockFn(torch.autograd.Function):
                   wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS, stream)
         if cp is not None:
             cp.fix_stats(st2, PB)
-        TV = (L + 63) // 64                     # one vpart row per 64-position wave tile
         h2 = torch.empty_like(xt)
-        vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
-        recompute = need_bwd and POOL_RECOMPUTE and POOL_PRENORM
-        if need_bwd:
-            # recompute: GELU column sums only, the backward re-derives GELU' from h2 (attn_bwd3); else GELU'
-            # of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
-            gfrag = None if recompute else torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
-            _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), _p(gfrag), B, L, NJ, LN_EPS,
-                      POOL_PRENORM, stream)
+        if POOL_V5:
+            # LN2 apply + attention pool in one launch (csrc/pool.hip); the backward recomputes GELU' from h2
+            TV = (L + 31) // 32                 # one vpart row per 32-position tile
+            vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
+            _lib.call("pbx_pool_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(), wv_bf16.data_ptr(),
+                      h2.data_ptr(), vpart.data_ptr(), B, L, NJ, LN_EPS, stream)
+            recompute, gfrag = True, None
         else:
-            # forward-only pool (GELU only, 8 independent waves per workgroup)
-            gfrag = None
-            _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                      wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
+            TV = (L + 63) // 64                 # one vpart row per 64-position wave tile
+            vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
+            recompute = need_bwd and POOL_RECOMPUTE and POOL_PRENORM
+            if need_bwd:
+                # recompute: GELU column sums only, the backward re-derives GELU' from h2 (attn_bwd3); else GELU'
+                # of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
+                gfrag = None if recompute else torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
+                _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
+                          wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), _p(gfrag), B, L, NJ, LN_EPS,
+                          POOL_PRENORM, stream)
+            else:
+                # forward-only pool (GELU only, 8 independent waves per workgroup)
+                gfrag = None
+                _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
+                          wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
         # the pool backward's operand: the GELU' fragments, or the block output rows h2 it recomputes them from
         ctx.recompute = recompute
         ctx.save_for_backward(x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw,
-                              wl_b, wv_bf16, g1, be1, g2)
+                              wl_b, wv_bf16, g1, be1, g2, be2)
         ctx.hlo = hlo
         ctx.tok = (tok, emb) if cp is None and wgrad_tok_ok(tok, emb, L, KS) else None
         ctx.emb_grad = bool(emb_grad)
@@ -403,7 +416,8 @@ class LocalBlockFn(torch.autograd.Function):
         # dvpart: produced by the global-track backward on its aux stream (PBX_GLOBAL_STREAM=1); dh2: by
         # the next block's conv data gradient on the "dg" stream
         streams.wait_ready(dvpart, dh2)
-        (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2) = ctx.saved_tensors
+        (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2,
+         be2) = ctx.saved_tensors
         cp, hlo = ctx.cp, ctx.hlo
         x = s1                                  # shape / dtype / device template of the [B, L, C] activations
         B, L, KS, dil, T1, T2, NJ = ctx.meta
@@ -416,45 +430,26 @@ class LocalBlockFn(torch.autograd.Function):
             # this shard's rows of the [L, C] affine gradients (the kernels accumulate into them)
             dg1, dbe1, dg2, dbe2 = (cp.rows(t) for t in (dg1, dbe1, dg2, dbe2))
         dh2 = None if dh2 is None else dh2.to(torch.bfloat16).contiguous()
-        BMV = 64                                # positions per forward vpart row
-        TV = (L + BMV - 1) // BMV
-        if dvpart is None:
-            dvpart = torch.zeros((B, TV, NJ), dtype=torch.float32, device=dev)
-        if dvpart.dim() == 3 and dvpart.stride(1) == 0:
-            # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
-            dvpart = dvpart[:, 0, :].float().contiguous()
-            BMV = (L + 31) // 32 * 32
-        dvpart = dvpart.float().contiguous()
-        # attention pool + LN2 partials
-        TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
-        dh2t = torch.empty_like(x)
-        bwd4 = POOL_BWD4 and not ctx.recompute and dvpart.dim() == 2
-        if bwd4:
-            TA *= 4                              # attn_bwd4: one partial per (tile, wave)
-        sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
-        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
-        # one workgroup per sample only when the batch alone fills two workgroups per CU (long sequences at
-        # small B keep the tile split); CP rewrites the LN2 partials group-wide between the pool backward and
-        # the constants: separate launch
-        min_b = POOL_CONSTS_MIN_B if POOL_CONSTS_MIN_B is not None else 2 * _num_cus(dev)
-        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None and dev.type == "cuda" and B >= min_b))
-        if consts_ready:
-            _lib.call("pbx_attn_bwd4c", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
-                      LN_EPS, st1.data_ptr(), T1, BM1, consts.data_ptr(), dgb.data_ptr(), stream)
-        elif bwd4:
-            _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
-                      LN_EPS, POOL_BWD4_TPW, stream)
-        elif ctx.recompute:
-            _lib.call("pbx_attn_bwd3", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                      POOL_BWD3_WIDE, stream)
+        if POOL_V5:
+            # pool backward (csrc/pool.hip): GELU' recomputed from h2 (= gfrag here), LN2 partials per 32-position
+            # tile; the LN2 / LN1 constants come from ln2_consts_kernel inside pbx_ln2_linear_bwd
+            TA = (L + 31) // 32
+            if dvpart is None:
+                dv, dv_tiles = torch.zeros((B, NJ), dtype=torch.float32, device=dev), 1
+            elif dvpart.dim() == 3 and (dvpart.shape[1] == 1 or dvpart.stride(1) == 0):
+                dv, dv_tiles = dvpart[:, 0, :].float().contiguous(), 1     # one gradient row per sample
+            else:
+                dv, dv_tiles = dvpart.float().contiguous(), TA
+            dh2t = torch.empty_like(x)
+            sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
+            consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
+            dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
+            consts_ready = 0
+            _lib.call("pbx_pool_bwd", gfrag.data_ptr(), g2.data_ptr(), be2.data_ptr(), _p(dh2), dv.data_ptr(), dv_tiles,
+                      wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, stream)
         else:
-            _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                      stream)
+            TA, dh2t, sums2, consts, dgb, consts_ready = LocalBlockFn._pool_bwd_v4(
+                ctx, gfrag, s2, st2, g2, dh2, dvpart, wv_bf16, st1, cp, B, L, T1, NJ, dev, stream)
         flush_deferred()                         # the previous (deeper) block's deferred weight gradient
         if cp is not None:
             cp.fix_sums(sums2)
@@ -569,6 +564,49 @@ class LocalBlockFn(torch.autograd.Function):
         pgrads = [None if d else g for (g, d) in dsts]
         gemb = dE if demb is not None and not dE_direct else None
         return (dx, dgb, *pgrads, None, None, None, None, None, None, gemb, None)
+
+    @staticmethod
+    def _pool_bwd_v4(ctx, gfrag, s2, st2, g2, dh2, dvpart, wv_bf16, st1, cp, B, L, T1, NJ, dev, stream):
+        BMV = 64                                # positions per forward vpart row
+        TV = (L + BMV - 1) // BMV
+        if dvpart is None:
+            dvpart = torch.zeros((B, TV, NJ), dtype=torch.float32, device=dev)
+        if dvpart.dim() == 3 and dvpart.stride(1) == 0:
+            # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
+            dvpart = dvpart[:, 0, :].float().contiguous()
+            BMV = (L + 31) // 32 * 32
+        dvpart = dvpart.float().contiguous()
+        # attention pool + LN2 partials
+        TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
+        dh2t = torch.empty_like(s2)
+        bwd4 = POOL_BWD4 and not ctx.recompute and dvpart.dim() == 2
+        if bwd4:
+            TA *= 4                              # attn_bwd4: one partial per (tile, wave)
+        sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
+        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
+        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
+        # one workgroup per sample only when the batch alone fills two workgroups per CU (long sequences at
+        # small B keep the tile split); CP rewrites the LN2 partials group-wide between the pool backward and
+        # the constants: separate launch
+        min_b = POOL_CONSTS_MIN_B if POOL_CONSTS_MIN_B is not None else 2 * _num_cus(dev)
+        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None and dev.type == "cuda" and B >= min_b))
+        if consts_ready:
+            _lib.call("pbx_attn_bwd4c", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
+                      LN_EPS, st1.data_ptr(), T1, BM1, consts.data_ptr(), dgb.data_ptr(), stream)
+        elif bwd4:
+            _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
+                      LN_EPS, POOL_BWD4_TPW, stream)
+        elif ctx.recompute:
+            _lib.call("pbx_attn_bwd3", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
+                      POOL_BWD3_WIDE, stream)
+        else:
+            _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
+                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
+                      stream)
+        return TA, dh2t, sums2, consts, dgb, consts_ready
 
 
 def embed_tokens(tokens: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
