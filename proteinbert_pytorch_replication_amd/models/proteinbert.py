@@ -325,12 +325,17 @@ class ProteinBERT(nn.Module):
 
     # ------------------------------------------------------------------------
     def resolved_backend(self, device: torch.device) -> str:
-        if self.backend == "auto":
+        # deterministic mode routes configurations without fixed-order HIP kernels (paper semantics,
+        # general global-track shapes) to the PyTorch path, judged on this model's own config (so a
+        # checkpoint loaded with another preset's flags is routed by what it is)
+        from ..utils import determinism
+        backend = determinism.backend_for(self.backend, self.config)
+        if backend == "auto":
             if device.type != "cuda":
                 return "torch"
             from ..ops.fused_model import hip_supported
             return "hip" if hip_supported(self)[0] else "torch"
-        return self.backend
+        return backend
 
     def attention_heads_state(self) -> Dict[str, Dict[str, torch.Tensor]]:
         return {str(i): b.global_attention_layer.heads_state() for i, b in enumerate(self.proteinBERT_blocks)}

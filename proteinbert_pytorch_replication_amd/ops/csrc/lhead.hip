@@ -453,7 +453,8 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
 #pragma unroll
   for (int k = 0; k < RPT; ++k) {
     const int row = tid + 512 * k;
-    const int p = row / B, s = row - (row / B) * B;
+    // rows past NR (small B) give p = row / B up to 1023 / B: clamp the ms[] index into the PP positions
+    const int p = min(row / B, PP - 1), s = row - (row / B) * B;
     const bool ok = row < NR && l0 + p < L;
     const size_t gi = (size_t)s * L + min(l0 + p, L - 1);
     yv[k] = ok ? (int)y[gi] : -1;

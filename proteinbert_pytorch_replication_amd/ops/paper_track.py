@@ -26,6 +26,17 @@ import torch
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
 from .gemm import gemm as _gemm
+
+
+def mm_x3(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """fp32 a [M, K] x b [K, N] at ~fp32 accuracy on the bf16 MFMA GEMM: a = ah + al, b = bh + bl (bf16
+    hi / lo parts), a b ~ ah bh + ah bl + al bh as ONE GEMM over the concatenated K (relative error
+    ~2^-16 instead of bf16's 2^-8).  For the small [B, G] x [G, H*K] query products of paper semantics."""
+    ah = a.to(BF16)
+    al = (a - ah.float()).to(BF16)
+    bh = b.to(BF16)
+    bl = (b - bh.float()).to(BF16)
+    return mm32(torch.cat([ah, ah, al], dim=1).contiguous(), torch.cat([bh, bl, bh], dim=0).contiguous())
 from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
                            addmm_into)
 from .local_track import (CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad,
@@ -111,10 +122,11 @@ class PaperBlockFn(torch.autograd.Function):
                   bl.data_ptr(), g2.data_ptr(), be2.data_ptr(), h2.data_ptr(), stats.data_ptr(), B, L, LN_EPS, stream)
         # attention: q from the global track, K/V projection as one library GEMM, split-L core
         gf = g.detach().float()
-        # q = tanh(g Wq): [B, G] x [G, H*K] on the in-tree MFMA GEMM (bf16 operands, fp32 out)
-        wq_cat = Wq.detach().permute(1, 0, 2).reshape(gf.shape[1], -1).to(BF16).contiguous()   # [G, H*K]
+        # q = tanh(g Wq): [B, G] x [G, H*K] at ~fp32 accuracy (three bf16 MFMA terms in one in-tree GEMM:
+        # the query feeds the softmax over L, so the bf16 rounding of g and Wq is kept out of it)
+        wq_cat = Wq.detach().permute(1, 0, 2).reshape(gf.shape[1], -1).float().contiguous()   # [G, H*K] fp32
         g_bf = gf.to(BF16)
-        q = torch.tanh(mm32(g_bf, wq_cat)).view(B, H, K)                                 # [B, H, K]
+        q = torch.tanh(mm_x3(gf, wq_cat)).view(B, H, K)                                  # [B, H, K]
         qs = (q * (1.0 / math.sqrt(K))).contiguous()
         o = torch.empty(B, H * VD, device=dev, dtype=F32)
         lse = torch.empty(B * H, device=dev, dtype=F32)
@@ -138,6 +150,7 @@ class PaperBlockFn(torch.autograd.Function):
                       o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
             wsave = wcat
         ctx.fused = fused
+        ctx.g32 = gf                          # fp32 (detached) g for the dWq product
         # the first block: x = bf16(emb[tok]), the conv weight gradient goes through the token one-hot
         ctx.tok = (tok, emb) if wgrad_tok_ok(tok, emb, L, KS) else None
         # emb_grad: x has no autograd history; the backward folds the conv data gradient into emb's
@@ -189,10 +202,11 @@ class PaperBlockFn(torch.autograd.Function):
                           stream)
                 dh2_att = [mm32(dpre, wsave.t()).to(BF16), None]                          # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
-            dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K).to(BF16)   # [B, H*K]
-            dg = mm32(dqpre, wq_cat.t())                                                   # [B, G]
+            dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K)        # [B, H*K] fp32
+            dg = mm_x3(dqpre, wq_cat.t())                                                  # [B, G]
+            gf32 = ctx.g32
 
-            def att_wgrad(dpre=dpre, h2=h2, dqpre=dqpre, g_bf=g_bf):
+            def att_wgrad(dpre=dpre, h2=h2, dqpre=dqpre, g_bf=g_bf, gf32=gf32):
                 # attention projection weight gradients: dWk | dWv = h2^T dpre (K = B*L), dWq = g^T dqpre
                 if PAPER_WGRAD_GEMM:
                     # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
@@ -205,14 +219,14 @@ class PaperBlockFn(torch.autograd.Function):
                 dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
                 dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
                 G = g_bf.shape[1]
-                dwq = mm32(g_bf.t(), dqpre)                                                # [G, H*K], K = B
+                dwq = mm_x3(gf32.t(), dqpre)                                               # [G, H*K], K = B
                 dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
                 return [dwcat, dwq]
 
             if ATT_WGRAD_AUX and streams.ENABLED and dev.type == "cuda" and all(d for _, d in dsts[10:]):
                 # only the optimizer and the DP all-reduce read them: beside the critical path, on the
                 # weight-gradient stream (the split-K GEMM over B*L rows was ~60 us per block on it)
-                streams.launch(dev, att_wgrad, keep=[dpre, h2, dqpre, g_bf], name="wgrad")
+                streams.launch(dev, att_wgrad, keep=[dpre, h2, dqpre, g_bf, gf32], name="wgrad")
             else:
                 att_wgrad()
         ds1 = torch.empty_like(x)

@@ -52,6 +52,11 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
         return _INFO
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     info = env_world()
+    # the node defaults go into the environment BEFORE the first GPU call: the HSA runtime reads its HSA_*
+    # variables once, at start-up (torch.cuda.device_count() does not start it on this image)
+    rccl_env = None
+    if info.world_size > 1 and device != "cpu" and backend in ("auto", "nccl") and torch.cuda.device_count() > 0:
+        rccl_env = rccl_node_defaults(info.world_size)
     use_gpu = torch.cuda.is_available() and device != "cpu"
     if use_gpu:
         torch.cuda.set_device(info.local_rank)
@@ -62,7 +67,7 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
         if backend == "auto":
             backend = "nccl" if use_gpu else "gloo"
         if backend == "nccl":
-            info.rccl_env = rccl_node_defaults(info.world_size)
+            info.rccl_env = rccl_env
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
@@ -99,7 +104,10 @@ def rccl_node_defaults(world_size: int) -> Optional[dict]:
     if int(os.environ.get("LOCAL_WORLD_SIZE", world_size)) != world_size:
         return None
     applied = {}
+    hsa_started = torch.cuda.is_initialized()
     for k, v in RCCL_NODE_DEFAULTS.items():
+        if k.startswith("HSA_") and hsa_started:
+            continue                    # read only at HSA start-up: setting it now would change nothing
         if k not in os.environ:
             os.environ[k] = v
             applied[k] = v

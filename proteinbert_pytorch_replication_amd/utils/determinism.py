@@ -22,7 +22,9 @@ extra small launches per block (``profiles/`` records it).  It also sets
 The fixed-order forms exist for the reference-semantics kernels with the fused global track
 (``glob_fused_ok`` shapes).  The paper-semantics kernels (``csrc/paper_local.hip``) and the general-shape
 global track (``csrc/glob.hip``) still reduce with float atomics, so :func:`backend_for` routes those
-configurations to the PyTorch path while the mode is on: the bitwise guarantee holds for every config.
+configurations to the PyTorch path while the mode is on.  ``ProteinBERT.resolved_backend`` applies that
+routing with the model's own config on every forward, so it covers ``backend="auto"``, ``bench.py``,
+library users and checkpoints loaded under another preset's flags alike.
 
 ``PBX_DETERMINISTIC=1`` in the environment is equivalent to calling :func:`enable` at import.
 """
@@ -76,9 +78,11 @@ def backend_for(requested: str, model_cfg=None) -> str:
     fixed-order kernel forms (paper semantics, unsupported global-track shapes) runs on the PyTorch
     path instead, which ``torch.use_deterministic_algorithms`` makes reproducible."""
     if _STATE["on"] and requested in ("hip", "auto") and not fixed_order_supported(model_cfg):
-        import logging
-        logging.getLogger(__name__).warning(
-            "deterministic mode: no fixed-order HIP kernels for this configuration; using the PyTorch backend")
+        if not _STATE.get("warned"):
+            import logging
+            logging.getLogger(__name__).warning(
+                "deterministic mode: no fixed-order HIP kernels for this configuration; using the PyTorch backend")
+            _STATE["warned"] = True
         return "torch"
     return requested
 

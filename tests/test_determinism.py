@@ -117,6 +117,29 @@ def test_backend_routing_without_fixed_order_kernels():
         torch.use_deterministic_algorithms(prev)
 
 
+def test_model_routes_itself_under_determinism():
+    """the routing happens in ProteinBERT.resolved_backend on the model's own config, so a
+    paper-semantics model built with backend='auto' or 'hip' (bench.py, library users, a checkpoint
+    loaded under another preset's flags) resolves to torch while the mode is on, and back to its request
+    when it is off."""
+    from proteinbert_pytorch_replication_amd.models import ProteinBERT
+    prev = torch.are_deterministic_algorithms_enabled()
+    cuda = torch.device("cuda")          # a device object only: resolved_backend never touches the GPU
+    paper = ProteinBERT(16, 20, 32, 64, 8, 2, 1, semantics="paper", backend="hip", device="cpu")
+    ref = ProteinBERT(16, 20, 128, 512, 8, 4, 1, semantics="reference", backend="hip", device="cpu")
+    try:
+        assert paper.resolved_backend(cuda) == "hip"
+        determinism.enable()
+        assert paper.resolved_backend(cuda) == "torch"
+        paper.backend = "auto"
+        assert paper.resolved_backend(cuda) == "torch"
+        assert ref.resolved_backend(cuda) == "hip"           # fixed-order kernels exist: stays on HIP
+    finally:
+        determinism.disable()
+        torch.use_deterministic_algorithms(prev)
+    assert paper.resolved_backend(torch.device("cpu")) == "torch"
+
+
 def test_deterministic_paper_semantics_bitwise_cpu():
     """Paper semantics in deterministic mode: routed to the PyTorch path (its HIP kernels reduce with float
     atomics), and two runs from the same seed agree bitwise."""

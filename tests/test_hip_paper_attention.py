@@ -71,3 +71,23 @@ def test_paper_model_step_uses_kernel_and_matches_oracle():
     losses = [step(X, Y, W).item() for _ in range(5)]
     assert all(torch.isfinite(torch.tensor(losses)))
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize("M,K,N", [(1024, 512, 256), (7, 512, 256), (512, 6, 256)])
+def test_query_products_fp32_accurate(M, K, N):
+    """the paper-semantics query products q = tanh(g Wq), dg = dqpre Wq^T and dWq = g^T dqpre run
+    as three-term bf16 hi/lo GEMMs (ops/paper_track.py mm_x3), so their error vs fp64 stays at fp32 level
+    (~1e-5 relative) instead of bf16's ~4e-3."""
+    from proteinbert_pytorch_replication_amd.ops.global_track import mm32
+    from proteinbert_pytorch_replication_amd.ops.paper_track import mm_x3
+    torch.manual_seed(M + K)
+    a = torch.randn(M, K, device="cuda")
+    b = torch.randn(K, N, device="cuda") * 0.05
+    ref = a.double() @ b.double()
+    err3 = ((mm_x3(a, b).double() - ref).norm() / ref.norm()).item()
+    err1 = ((mm32(a.bfloat16(), b.bfloat16()).double() - ref).norm() / ref.norm()).item()
+    print(f"M={M} K={K} N={N}: hi/lo rel err {err3:.2e}  plain bf16 {err1:.2e}")
+    assert err3 < 2e-5 and err3 < 0.02 * err1
+    # non-contiguous operands, as the backward passes them (g^T, Wq^T)
+    ref_t = b.t().double() @ a.t().double()
+    assert ((mm_x3(b.t(), a.t()).double() - ref_t).norm() / ref_t.norm()).item() < 2e-5
