@@ -24,8 +24,10 @@ collectives per step.
   compute stream; only the tail buckets' update trails their all-reduce.  The group-wide non-finite
   decision is taken BEFORE any update: each bucket's local gradients are tested as it is launched, and
   one 4-byte MAX all-reduce of the OR of those flags is queued ahead of the tail buckets, so every rank
-  skips or commits every bucket together.  (The test is on local gradients: a sum of finite per-rank
-  gradients that overflows fp32 is not caught, where the previous post-reduction test caught it.)
+  skips or commits every bucket together.  The reduced gradients are tested as well (identical on every
+  rank, so no extra collective): a sum of finite per-rank gradients that overflows fp32 skips the whole
+  step when it is in the head buckets, and the tail update (with the head already committed) when it
+  appears only in the tail -- no Inf / NaN ever reaches the parameters.
 * ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
   bf16-rounded gradient sums); the default is fp32.  (A bf16 reduction of only the last, exposed
   bucket -- the 18 MB global input layer -- was an unmeasured option and has been removed: no
@@ -158,6 +160,20 @@ class BucketedAllReduce:
             else:
                 self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
 
+    def _post_flag(self, start: int, end: int) -> torch.Tensor:
+        """int32 [1] device flag: 1 when the (reduced) arena gradients [start, end) hold a NaN / Inf."""
+        view = self.arena.grad[start:end]
+        if view.is_cuda:
+            from ..ops import _lib
+            ws = torch.empty(1025, dtype=torch.int32, device=view.device)
+            if view.numel() == 0:
+                return ws[1024:].zero_()
+            _lib.call("pbx_nonfinite_flag", view.data_ptr(), view.numel(), ws.data_ptr(), ws[1024:].data_ptr(),
+                      _lib.stream_ptr(view.device))
+            return ws[1024:]
+        bad = view.numel() > 0 and not bool(torch.isfinite(torch.dot(view, torch.zeros_like(view))))
+        return torch.tensor([1 if bad else 0], dtype=torch.int32, device=view.device)
+
     def _flag_reduce_and_launch_rest(self) -> None:
         """Local flags of the buckets not launched yet, the group-wide MAX of every bucket's flag (4 bytes,
         queued ahead), then those buckets' all-reduces."""
@@ -236,13 +252,23 @@ class BucketedAllReduce:
         for b in range(split_b):
             self._land(b)
         self._flag_work.wait()
-        opt.skip_flag = self._gflag if skip_nonfinite else None
-        opt.begin_step()
         split = self.buckets[split_b][0] if split_b < len(self.buckets) else self.arena.numel
+        skip = None
+        if skip_nonfinite:
+            # local flags (group OR) + the REDUCED head gradients: finite per-rank gradients whose sum
+            # overflows are caught too; the reduced values are identical on every rank, so every rank
+            # takes the same decision without another collective
+            skip = torch.maximum(self._gflag, self._post_flag(0, split))
+        opt.skip_flag = skip
+        opt.begin_step()
         opt.step_range(0, split)              # beside the tail buckets' all-reduce
         for b in range(split_b, len(self.buckets)):
             self._land(b)
         if split < self.arena.numel:
+            if skip_nonfinite:
+                # a sum that overflows only in the tail is known only now: the tail update is skipped
+                # (the head's was already committed), so no Inf / NaN ever reaches the parameters
+                opt.skip_flag = torch.maximum(skip, self._post_flag(split, self.arena.numel))
             opt.step_range(split, self.arena.numel)
         self.track_nonfinite = False
         self._flag_work = None

@@ -137,6 +137,49 @@ def test_dp_overlapped_optimizer_skips_all_buckets_on_nonfinite(tmp_path):
                        join=True)
 
 
+def _overflow_worker(rank, world, port, out_dir, where):
+    """Both ranks hold a FINITE gradient of 3e38 in one element; their SUM overflows fp32.  where='head':
+    the element is in the first bucket -> nothing is updated; 'tail': in the last bucket -> the tail's
+    update is skipped (the head's already ran) and no Inf reaches the parameters."""
+    _env(rank, world, port)
+    torch.set_num_threads(1)
+    from proteinbert_pytorch_replication_amd.parallel import dist as pdist
+    from proteinbert_pytorch_replication_amd.parallel.ddp import BucketedAllReduce
+    pdist.init_distributed(device="cpu")
+    torch.manual_seed(0)
+    m = ProteinBERT(backend="torch", **CFG)
+    opt = FusedAdam(m.parameters(), lr=1e-2)
+    ddp = BucketedAllReduce(opt.arena, bucket_mb=0.004)
+    step = PretrainStep(m, opt, ddp)
+    before = opt.arena.data.clone()
+    p = opt.arena.params[0] if where == "head" else opt.arena.params[-1]
+
+    def big(g):
+        g = g.clone()
+        g.view(-1)[0] = 3e38
+        return g
+    p.register_hook(big)
+    step(*SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=100 + rank,
+                            use_kernel=False).next_batch())
+    assert torch.isfinite(opt.arena.data).all(), f"rank {rank}: an overflowed sum reached the parameters"
+    tail0 = ddp.buckets[-1][0]
+    if where == "head":
+        assert torch.equal(opt.arena.data, before), f"rank {rank} updated despite an overflowing sum"
+    else:
+        assert torch.equal(opt.arena.data[tail0:], before[tail0:]), f"rank {rank}: tail updated"
+    torch.save(opt.arena.data, os.path.join(out_dir, f"rank{rank}.pt"))
+    pdist.destroy()
+
+
+@pytest.mark.parametrize("where", ["head", "tail"])
+def test_dp_overlapped_optimizer_catches_summed_overflow(tmp_path, where):
+    mp.start_processes(_overflow_worker, args=(2, _free_port(), str(tmp_path), where), nprocs=2,
+                       start_method="spawn", join=True)
+    a = torch.load(tmp_path / "rank0.pt", weights_only=True)
+    b = torch.load(tmp_path / "rank1.pt", weights_only=True)
+    assert torch.equal(a, b)                         # every rank took the same decision
+
+
 def _pretrain_worker(rank, world, port, save, zero=False):
     _env(rank, world, port)
     torch.set_num_threads(1)
