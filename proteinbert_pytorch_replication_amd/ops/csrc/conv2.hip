@@ -17,10 +17,7 @@
 //                 Epilogue: the pre-activations staged through LDS; all 8 waves then write
 //                 s1 = x + GELU(pre_n) + GELU(pre_w) + gb and (training) GELU'(pre_n), GELU'(pre_w)
 //                 with row-contiguous 16-B stores, plus the tile's LayerNorm (mean, M2) partial.
-//   conv_dgrad3 : both convs' dpre = dS1 * GELU'(pre) tiles (with their halos) staged once and their
-//                 central rows written for the weight gradient; waves 0-3 = narrow, 4-7 = wide, wave
-//                 q owns input channels q*32..+32; the two halves are summed through LDS in the
-//                 dx = dS1 + W^T dpre epilogue.
+//   (the data gradient is conv4.hip conv_dgrad4)
 #include "mfma.h"
 
 using namespace pbx;
@@ -59,7 +56,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gb,
     bf16_t* __restrict__ pre_n, bf16_t* __restrict__ pre_w, bf16_t* __restrict__ s1,
     float* __restrict__ stats, int L, int KS, int dil, const long long* __restrict__ tok,
-    const bf16_t* __restrict__ emb) {
+    const bf16_t* __restrict__ emb, int xlo, int xhi) {
   constexpr int TBM = BM;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NPT = TBM / 32;                               // 32-position MFMA tiles per wave
@@ -77,7 +74,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
-  const bf16_t* xsmp = x + (size_t)b * L * CH;
+  // xlo / xhi: rows of the neighbouring sequence shards stored around each sample's L rows (context
+  // parallelism): logical positions -xlo .. L + xhi - 1 are real, anything beyond is the zero padding
+  const bf16_t* xsmp = x + ((size_t)b * (xlo + L + xhi) + xlo) * CH;
   const bf16x8* fw = (cv ? fww : fwn) + cq * 64;            // wave-uniform; + frag_index(k, kb, 0) * 64 + lane
   const int NI = KS * 8;                                      // K-steps: taps x 16-channel blocks
   // A-fragment ring: step it uses fr[it & 3], the load for step it + 3 is in flight meanwhile (the
@@ -95,7 +94,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       XR * 16,
       [&](int idx) {
         const int pos = pos0 - halo + (idx >> 4);
-        if (pos < 0 || pos >= L) return make_uint4(0u, 0u, 0u, 0u);
+        if (pos < -xlo || pos >= L + xhi) return make_uint4(0u, 0u, 0u, 0u);
         const bf16_t* row = toks != nullptr ? emb + (size_t)toks[pos] * CH : xsmp + (size_t)pos * CH;
         return *reinterpret_cast<const uint4*>(row + (idx & 15) * 8);
       },
@@ -216,7 +215,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     // scalar A&S stages (gelu_scalar_n): this epilogue runs beside the other waves' MFMAs, where the
     // packed form measured 3 % slower on the kernel.  Training: GELU AND GELU' from one shared core
     // (+2 VALU per value); GELU' is what the data gradient multiplies by, so it is stored instead of the
-    // pre-activation and conv_dgrad3 no longer evaluates a GELU' core per value (~14 VALU + 2
+    // pre-activation and the data gradient no longer evaluates a GELU' core per value (~14 VALU + 2
     // transcendentals, on 1.2x the values for the halo rows)
 #ifdef PBX_CONV_PRE   // ablation: store the pre-activation, the data gradient evaluates GELU' (round-3 form)
     if (STORE && ok) {
@@ -283,186 +282,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// data gradient: D[ci][pos] = sum_conv sum_tap sum_co W[co][ci][tap] * dpre_conv[pos - shift][co]
-// (Running the LayerNorm-1 backward inside this kernel's prologue instead of the separate finalize pass
-// measured 1.5-3 % slower on the step: the prologue is load-latency bound, profiles/r2_v8_ln1_fuse_ab.txt.)
-__global__ void __launch_bounds__(512, 4) conv_dgrad3_kernel(
-    const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ pre_n,
-    const bf16_t* __restrict__ pre_w, const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw,
-    bf16_t* __restrict__ dx, bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int KS, int dil) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int T = (L + BM - 1) / BM;
-  const int tid0 = tile_id();
-  const int b = tid0 / T, t = tid0 - (tid0 / T) * T;
-  const int pos0 = t * BM;
-  const int half = KS >> 1;
-  const int halo_n = half, halo_w = half * dil;
-  const int RN = BM + 2 * halo_n;
-  unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
-  unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int cv = w >> 2, cq = w & 3;
-  const size_t sbase = (size_t)b * L * CH;
-  const bf16x8* fw = (cv ? ftw : ftn) + cq * 64;          // wave-uniform (+ lane per load)
-  const int NI = KS * 8;
-  bf16x8 fr[4];                                   // A-fragment ring, as in conv_fwd3
-  fr[0] = fw[lane];
-  fr[1] = fw[256 + lane];
-  fr[2] = fw[512 + lane];
-
-  // stage dpre = dS1 * GELU'(pre) of both convs with their halos; central rows also go to global
-#pragma unroll 1
-  for (int c = 0; c < 2; ++c) {
-    const int halo = c ? halo_w : halo_n;
-    const bf16_t* pre = c ? pre_w : pre_n;
-    bf16_t* dpo = c ? dpre_w : dpre_n;
-    unsigned char* tile = c ? aw : an;
-    const int nch = (BM + 2 * halo) * 16;
-    for (int base = tid; base < nch; base += 2 * 512) {
-      uint4 gq[2], pq[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int idx = base + i * 512;
-        const int pos = pos0 - halo + (idx >> 4);
-        const bool ok = idx < nch && pos >= 0 && pos < L;
-        const size_t off = sbase + (size_t)pos * CH + (idx & 15) * 8;
-        gq[i] = ok ? *reinterpret_cast<const uint4*>(ds1 + off) : make_uint4(0u, 0u, 0u, 0u);
-        pq[i] = ok ? *reinterpret_cast<const uint4*>(pre + off) : make_uint4(0u, 0u, 0u, 0u);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int idx = base + i * 512;
-        if (idx >= nch) break;
-        const int j = idx >> 4, ch = idx & 15;
-        const int pos = pos0 - halo + j;
-        float g[8], pv[8], o[8];
-        unpack8(gq[i], g);
-        unpack8(pq[i], pv);                         // GELU'(pre), stored by the forward
-#ifdef PBX_CONV_PRE
-        {
-          f32x2 pp[4], gd[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pp[e] = (f32x2){pv[2 * e], pv[2 * e + 1]};
-          gelu_scalar_n<4, 1>(pp, nullptr, gd);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            pv[2 * e] = gd[e].x;
-            pv[2 * e + 1] = gd[e].y;
-          }
-        }
-#endif
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = pv[e] * g[e];
-        const uint4 v = (pos >= 0 && pos < L) ? packq8(o) : make_uint4(0u, 0u, 0u, 0u);
-        if (pos >= 0 && pos < L && j >= halo && j < halo + BM)
-          *reinterpret_cast<uint4*>(dpo + sbase + (size_t)pos * CH + ch * 8) = v;
-        *reinterpret_cast<uint4*>(tile + swz256(j, ch)) = v;
-      }
-    }
-  }
-  __syncthreads();
-
-  f32x16_t acc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = zero16();
-  const int d = cv ? dil : 1;
-  const unsigned char* as = cv ? aw : an;
-  const int halo = cv ? halo_w : halo_n;
-#ifdef PBX_CONV_BPF0   // ablation: B fragments read right before their MFMAs (round-3 form)
-  for (int k = 0; k < KS; ++k) {
-    const int rb = halo + r - (k - half) * d;
-    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int it = k * 8 + kb;
-      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;
-      fr[(kb + 3) & 3] = fwk[lane];
-      __builtin_amdgcn_sched_barrier(0);
-      const int off = ((32 * kb) ^ gs) + rowb;
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(as, off + pt * 8192), acc[pt]);
-    }
-  }
-#else
-  bf16x8 bq[2][4];                                // B fragments one K-step ahead, as in conv_fwd3
-  auto rows_of = [&](int k, int& rowb, int& gs) {
-    const int rb = halo + r - (k - half) * d;
-    rowb = rb << 8;
-    gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
-  };
-  int rowb, gs;
-  rows_of(0, rowb, gs);
-#pragma unroll
-  for (int pt = 0; pt < 4; ++pt) bq[0][pt] = lds_frag(as, (0 ^ gs) + rowb + pt * 8192);
-  for (int k = 0; k < KS; ++k) {                  // tap loop / unrolled channel blocks, as in conv_fwd3
-    int rowbn, gsn;
-    rows_of(min(k + 1, KS - 1), rowbn, gsn);
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int it = k * 8 + kb;
-      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
-      fr[(kb + 3) & 3] = fwk[lane];
-      const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) bq[(kb + 1) & 1][pt] = lds_frag(as, noff + pt * 8192);
-      __builtin_amdgcn_sched_barrier(0);          // keep both prefetches ahead of this step's MFMAs
-#pragma unroll
-      for (int pt = 0; pt < 4; ++pt) acc[pt] = mfma32(fr[kb & 3], bq[kb & 1][pt], acc[pt]);
-    }
-    rowb = rowbn;
-    gs = gsn;
-  }
-#endif
-
-  // epilogue: the wide half stages its fp32 partial ([BM][128] fp32, 16-B chunks XOR-swizzled by
-  // row), the narrow half adds its own in place, then dx = ds1 + sum, row-contiguous 16-B accesses.
-  const int vrows = min(BM, L - pos0);
-  float* ft = reinterpret_cast<float*>(smem);     // 64 KB over the dpre tiles
-  auto fidx = [&](int p, int c4) { return p * CH + ((c4 ^ (p & 31)) << 2); };
-  __syncthreads();                                // every wave is done reading the dpre tiles
-  if (cv == 1) {
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c4 = (cq * 32 + 8 * g + 4 * h) >> 2;
-        *reinterpret_cast<float4*>(ft + fidx(pt * 32 + r, c4)) =
-            make_float4(acc[pt][4 * g], acc[pt][4 * g + 1], acc[pt][4 * g + 2], acc[pt][4 * g + 3]);
-      }
-  }
-  __syncthreads();
-  if (cv == 0) {
-#pragma unroll
-    for (int pt = 0; pt < 4; ++pt)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c4 = (cq * 32 + 8 * g + 4 * h) >> 2;
-        float4* f = reinterpret_cast<float4*>(ft + fidx(pt * 32 + r, c4));
-        const float4 o = *f;
-        *f = make_float4(o.x + acc[pt][4 * g], o.y + acc[pt][4 * g + 1], o.z + acc[pt][4 * g + 2],
-                         o.w + acc[pt][4 * g + 3]);
-      }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int idx = tid + 512 * i;
-    const int row = idx >> 4, c = idx & 15;
-    if (row >= vrows) continue;
-    const size_t off = sbase + (size_t)(pos0 + row) * CH + c * 8;
-    float gv[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(ds1 + off), gv);
-    const float4 f0 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c));
-    const float4 f1 = *reinterpret_cast<const float4*>(ft + fidx(row, 2 * c + 1));
-    const float fa[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = gv[e] + fa[e];
-    *reinterpret_cast<uint4*>(dx + off) = packq8(o);
-  }
-}
-
 // fp32 torch conv weight [co][ci][KS] -> bf16 fragment images: fwd[k][kb][mb][lane][8] with
 // (M = co = 32mb + (lane&31), K = ci = 16kb + 8(lane>>5) + j) and dgrad with M = ci, K = co.
 __global__ void __launch_bounds__(256) pack_conv_frag_kernel(const float* __restrict__ w, bf16_t* __restrict__ pf,
@@ -481,10 +300,6 @@ int fwd3_lds(int KS, int dil, int tbm) {
   const int ot = tbm * 256;
   return (xt > ot ? xt : ot) + ot + (3 * CH + 32) * 4;
 }
-int dgrad3_lds(int KS, int dil) {
-  const int a = (2 * BM + 2 * (KS / 2) * (1 + dil)) * 256;
-  return a > BM * CH * 4 ? a : BM * CH * 4;
-}
 }  // namespace
 
 static bool conv3_attrs_set = false;
@@ -492,33 +307,43 @@ static void set_conv3_attrs() {
   if (conv3_attrs_set) return;
   (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)conv_fwd3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)conv_dgrad3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   conv3_attrs_set = true;
 }
 
 // LayerNorm partials in `stats` are per 128-position tile: [B][ceil(L/128)][2].  fwn/fww: forward
 // fragment images of the narrow/wide weights (pbx_pack_conv_frag); C = 128 channels; gb [B][128] fp32.
-// pre_n / pre_w: GELU'(pre-activation) of the narrow / wide conv as bf16 (what conv_dgrad3 multiplies the
-// incoming gradient by), or both null (inference: no backward reads them).
+// pre_n / pre_w: GELU'(pre-activation) of the narrow / wide conv as bf16 (what the data gradient,
+// conv4.hip conv_dgrad4, multiplies the incoming gradient by), or both null (inference: no backward).
+// xlo / xhi: halo rows of the neighbouring sequence shards stored around each sample's L rows of x
+// (context parallelism: x is [B][xlo + L + xhi][128]); 0 / 0 for a whole sequence.
 static int conv_fwd3_launch(const void* x, const long long* tok, const void* emb, const void* fwn, const void* fww,
                             const float* bn, const float* bw, const float* gb, void* pre_n, void* pre_w, void* s1,
-                            float* stats, int B, int L, int KS, int dil, hipStream_t st) {
+                            float* stats, int B, int L, int KS, int dil, int xlo, int xhi, hipStream_t st) {
   set_conv3_attrs();
   const int lds = fwd3_lds(KS, dil, BM);
-  if (lds > 163840 || dil < 1 || KS < 2 || gb == nullptr) return (int)hipErrorInvalidValue;
+  if (lds > 163840 || dil < 1 || KS < 2 || gb == nullptr || xlo < 0 || xhi < 0) return (int)hipErrorInvalidValue;
+  if (tok != nullptr && (xlo || xhi)) return (int)hipErrorInvalidValue;
   const int T = (L + BM - 1) / BM;
   if ((pre_n == nullptr) != (pre_w == nullptr)) return (int)hipErrorInvalidValue;
   const auto kern = pre_n != nullptr ? conv_fwd3_kernel<true> : conv_fwd3_kernel<false>;
   hipLaunchKernelGGL(kern, dim3(B * T), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn,
                      (const bf16x8*)fww, bn, bw, gb, (bf16_t*)pre_n, (bf16_t*)pre_w, (bf16_t*)s1, stats, L, KS, dil,
-                     tok, (const bf16_t*)emb);
+                     tok, (const bf16_t*)emb, xlo, xhi);
   return pbx_launch_status();
 }
 
 PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
                              int dil, hipStream_t st) {
-  return conv_fwd3_launch(x, nullptr, nullptr, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st);
+  return conv_fwd3_launch(x, nullptr, nullptr, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, 0, 0, st);
+}
+
+// context-parallel form: x holds xlo / xhi halo rows of the neighbouring shards around each sample's L rows
+PBX_EXPORT int pbx_conv_fwd3x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
+                              const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
+                              int dil, int xlo, int xhi, hipStream_t st) {
+  return conv_fwd3_launch(x, nullptr, nullptr, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, xlo, xhi,
+                          st);
 }
 
 // The first block (reference modules.py:249-253,300 feeding :185-212): x = emb[tok] gathered in the
@@ -527,20 +352,7 @@ PBX_EXPORT int pbx_conv_fwd3t(const long long* tok, const void* emb, const void*
                               const float* bw, const float* gb, void* pre_n, void* pre_w, void* s1, float* stats,
                               int B, int L, int KS, int dil, hipStream_t st) {
   if (tok == nullptr || emb == nullptr) return (int)hipErrorInvalidValue;
-  return conv_fwd3_launch(nullptr, tok, emb, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, st);
-}
-
-PBX_EXPORT int pbx_conv_dgrad3(const void* ds1, const void* pre_n, const void* pre_w, const void* ftn,
-                               const void* ftw, void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS, int dil,
-                               hipStream_t st) {
-  set_conv3_attrs();
-  const int lds = dgrad3_lds(KS, dil);
-  if (lds > 163840 || dil < 1 || KS < 2) return (int)hipErrorInvalidValue;
-  const int T = (L + BM - 1) / BM;
-  hipLaunchKernelGGL(conv_dgrad3_kernel, dim3(B * T), dim3(512), lds, st, (const bf16_t*)ds1,
-                     (const bf16_t*)pre_n, (const bf16_t*)pre_w, (const bf16x8*)ftn, (const bf16x8*)ftw,
-                     (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, KS, dil);
-  return pbx_launch_status();
+  return conv_fwd3_launch(nullptr, tok, emb, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, 0, 0, st);
 }
 
 // fwd / dgrad fragment images (KS * 128 * 128 bf16 each) of one fp32 [128][128][KS] conv weight

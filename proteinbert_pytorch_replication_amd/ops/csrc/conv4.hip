@@ -1,29 +1,12 @@
-// Dual-dilation residue convolution forward, persistent and software-pipelined.
+// Dual-dilation residue convolution data gradient, optionally with the LayerNorm-1 backward
+// finalize fused into its staging pass (K5).
 //
 // Reference: ProteinBERT/modules.py:124-147 (Conv1d C->C, k=9, dilation 1 and 5, padding "same",
-// each + GELU) and :205-212 (x + narrow + wide + broadcast(global->local), LayerNorm over (L, C)).
+// each + GELU) and :205-212 (x + narrow + wide + broadcast(global->local), LayerNorm over (L, C)) --
+// the backward of that chain.  The forward is conv2.hip conv_fwd3.
 //
-// Why (conv2.hip conv_fwd3, round 3): per 128-position tile a workgroup ran its 288 MFMAs per wave,
-// then a VALU-heavy epilogue (two exact-erf GELUs per output, packing, stores, LayerNorm partials:
-// ~5 VALU per MFMA of the tile) with the MFMA pipe idle; PMC: mfma_busy 0.46, 8.3 VALU per MFMA,
-// issue-stall 0.41.  Two co-resident workgroups did not desynchronise enough to hide it.
-//
-// Here ONE persistent workgroup per CU (8 waves: waves 0-3 narrow conv, 4-7 wide conv, wave q owns
-// output channels 32(q&3)..+32 for all 128 positions, as in conv_fwd3) walks its tiles and runs the
-// epilogue of tile i-1 INSIDE the K loop of tile i: the previous tile's pre-activations sit in an LDS
-// staging image, and every K-step of the current tile (4 MFMAs) carries a fixed slice of that
-// epilogue (LDS/global operand loads, one GELU pair, or the combine + stores), so the VALU work issues
-// in the shadow of the matrix pipe instead of after it.  The x tile of tile i+1 streams in by
-// global->LDS DMA meanwhile (double-buffered), and the weight-fragment ring runs on across tiles.
-//
-//   LDS: 2 x-tile buffers (128 + 8 d rows x 256 B, swz256) | narrow + wide staging (2 x 32 KB, swz256)
-//        | biases (1 KB) | LayerNorm scratch      = 151 KB at d = 5: one workgroup per CU.
-//   Per tile: wait own DMA, barrier; DMA next x tile; 72 K-steps (MFMA tile i || epilogue slice of
-//   tile i-1); barrier; LayerNorm (mean, M2) of tile i-1; acc + bias -> staging (tile i).
-//
-// Outputs are those of conv_fwd3: s1 = x + GELU(pre_n) + GELU(pre_w) + gb (bf16), per-tile LayerNorm
-// (mean, M2) partials over the stored values, and (training) GELU'(pre_n), GELU'(pre_w) for the
-// data gradient (conv_dgrad3).
+// (A persistent, software-pipelined forward -- the epilogue of tile i-1 inside the K loop of tile i --
+// lived here in rounds 3-4: equal in isolation, 3.3 % slower in the step; removed in round 5.)
 #include "mfma.h"
 
 using namespace pbx;
@@ -36,298 +19,13 @@ constexpr int KS = 9;                // taps (the launcher refuses other sizes)
 constexpr int NI = KS * 8;           // K-steps per tile (taps x 16-channel blocks)
 constexpr int NPT = BM / 32;         // 32-position MFMA tiles per wave
 
-__device__ __attribute__((aligned(16))) unsigned int g_zero16_c4[4];   // zero-initialised device global
-
-// One 1-KiB global->LDS DMA wave instruction (lane i's 16 bytes land at lds_base + 16 i); inline asm
-// so hipcc does not make later ds_reads wait for it; it retires in vmcnt order.
-__device__ __forceinline__ void glds16_c4(const void* src, unsigned char* lds_base) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_base);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(dst)
-               : "memory");
-}
-
-// Tile n of workgroup j: the workgroups of one XCD (ids congruent mod 8) take a contiguous run of
-// tiles per round, so neighbouring tiles of a sample -- whose +-4d-row halos overlap -- share an L2.
-__device__ __forceinline__ long tile_of(long round, int G) {
-  const int j = blockIdx.x;
-  if ((G & 7) == 0) return round * G + (long)(j & 7) * (G >> 3) + (j >> 3);
-  return round * G + j;
-}
-
-// One thread's epilogue of the previous tile, spread over the K-steps of the current one.
-// Thread t owns rows (t + 512 i) >> 4, i = 0..3, channel chunk c = t & 15 (8 channels).
-struct Epi {
-  uint4 pn, pw, xq;                  // staged pre-activations (bf16 x 8) and the x row chunk
-  float s[8];                        // s1 accumulator: x + gb, then + GELU(pre_n) + GELU(pre_w)
-  unsigned dn[4], dw[4];             // GELU' (bf16 pairs) for the data gradient
-  f32x2 ln;                          // (sum, sum of squares) of the stored s1 values
-  float gb[8];                       // broadcast global->local vector of the tile's sample
-};
-
-template <bool STORE>
-__global__ void __launch_bounds__(512, 1) conv_fwd4_kernel(
-    const bf16_t* __restrict__ x, const bf16x8* __restrict__ fwn, const bf16x8* __restrict__ fww,
-    const float* __restrict__ bn, const float* __restrict__ bw, const float* __restrict__ gbv,
-    bf16_t* __restrict__ gdn, bf16_t* __restrict__ gdw, bf16_t* __restrict__ s1, float* __restrict__ stats,
-    int B, int L, int dil, int xlo, int xhi) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const int half = KS >> 1;
-  const int halo = half * dil;
-  const int XR = BM + 2 * halo;                 // multiple of 4 (2 halo = 8 d)
-  const int XB = XR * 256;
-  unsigned char* stn = smem + 2 * XB;           // staging: narrow | wide pre-activations [BM][256 B]
-  unsigned char* stw = stn + BM * 256;
-  float* bias = reinterpret_cast<float*>(stw + BM * 256);   // bn | bw
-  float* scratch = bias + 2 * CH;                           // 8 waves x (sum, sum of squares)
-  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int r = lane & 31, h = lane >> 5;
-  const int cv = w >> 2, cq = w & 3;
-  const int T = (L + BM - 1) / BM;
-  const long NT = (long)B * T;
-  const int G = gridDim.x;
-  const long rounds = (NT + G - 1) / G;
-  const bf16x8* fw = (cv ? fww : fwn) + cq * 64;
-  const int d = cv ? dil : 1;
-  if (tid < 2 * CH) bias[tid] = tid < CH ? bn[tid] : bw[tid - CH];
-
-  auto stage_x = [&](long tile, unsigned char* buf) {
-    const int b = (int)(tile / T), t = (int)(tile - (tile / T) * T);
-    const int pos0 = t * BM;
-    const bf16_t* xs = x + ((size_t)b * (L + xlo + xhi) + xlo) * CH;   // logical position 0
-    const int n = XR >> 2;                      // 4 rows (1 KiB) per DMA instruction
-    for (int j = w; j < n; j += 8) {
-      const int row = 4 * j + (lane >> 4);
-      const int chunk = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));   // swz256 image
-      const int pos = pos0 - halo + row;
-      const void* src = (pos >= -xlo && pos < L + xhi) ? (const void*)(xs + (ptrdiff_t)pos * CH + chunk * 8)
-                                              : (const void*)g_zero16_c4;
-      glds16_c4(src, buf + j * 1024);
-    }
-  };
-
-  // weight-fragment ring: K-step it uses fr[it & 3]; the load of fragment (it + 3) mod NI -- the next
-  // tile's first fragments at the end of a tile -- is in flight meanwhile
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<bf16x8*>(fw), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
-  auto wfrag = [&](int nf) {     // fragment nf of this wave's 32-co block: voffset lane, soffset nf
-    typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 16, nf * 4096, 0);
-    return __builtin_bit_cast(bf16x8, v);
-  };
-  bf16x8 fr[4];
-  fr[0] = wfrag(0);
-  fr[1] = wfrag(1);
-  fr[2] = wfrag(2);
-
-  // previous tile (epilogue pending)
-  long ptile = -1;
-  int pb = 0, ppos0 = 0, pvrows = 0;
-  Epi e;
-  const int ch8 = (tid & 15) * 8;
-
-  // Epilogue of the previous tile, in slices tied to the K-steps of the current one: row group i
-  // (rows (t + 512 i) >> 4) runs over taps 2i (A) and 2i + 1 (B); tap 8 reduces the LayerNorm partial.
-  //   A0 operand loads | A1 A2 A4 A6 B0 B2 B4 B5 the 8 GELU pairs (narrow 0-3, wide 4-7) | B7 combine + stores
-  // The tap loop stays a runtime loop (per-tap addresses in a few registers, as in conv_fwd3); the
-  // slice is selected by wave-uniform branches on the tap's parity.
-  auto gelu_pair = [&](const int j) {
-    const int q = j & 3;
-    const uint4& src = j < 4 ? e.pn : e.pw;
-    const unsigned word = q == 0 ? src.x : q == 1 ? src.y : q == 2 ? src.z : src.w;
-    const f32x2 in = {__uint_as_float(word << 16), __uint_as_float(word & 0xffff0000u)};
-    f32x2 g, gd;
-    if constexpr (STORE) {
-      gelu_scalar_n<1, 2>(&in, &g, &gd);
-      const unsigned pk = (unsigned)f2bf(gd.x) | ((unsigned)f2bf(gd.y) << 16);
-      if (j < 4) e.dn[q] = pk; else e.dw[q] = pk;
-    } else {
-      gelu_scalar_n<1, 0>(&in, &g, nullptr);
-    }
-    e.s[2 * q] += g.x;
-    e.s[2 * q + 1] += g.y;
-  };
-  auto epi_load = [&](int i) {
-    const int row = (tid + 512 * i) >> 4;
-    if (i == 0) {
-      const float4 g0 = *reinterpret_cast<const float4*>(gbv + (size_t)pb * CH + ch8);
-      const float4 g1 = *reinterpret_cast<const float4*>(gbv + (size_t)pb * CH + ch8 + 4);
-      e.gb[0] = g0.x; e.gb[1] = g0.y; e.gb[2] = g0.z; e.gb[3] = g0.w;
-      e.gb[4] = g1.x; e.gb[5] = g1.y; e.gb[6] = g1.z; e.gb[7] = g1.w;
-      e.ln = (f32x2){0.f, 0.f};
-    }
-    e.pn = *reinterpret_cast<const uint4*>(stn + swz256(row, tid & 15));
-    e.pw = *reinterpret_cast<const uint4*>(stw + swz256(row, tid & 15));
-    const int prow = min(ppos0 + row, L - 1);
-    e.xq = *reinterpret_cast<const uint4*>(x + ((size_t)pb * (L + xlo + xhi) + xlo + prow) * CH + ch8);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e.s[k] = 0.f;
-  };
-  auto epi_combine = [&](int i) {
-    const int row = (tid + 512 * i) >> 4;
-    const bool ok = row < pvrows;
-    float xv[8];
-    unpack8(e.xq, xv);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e.s[k] += xv[k] + e.gb[k];
-    const uint4 oq = packq8(e.s);
-    const size_t off = ((size_t)pb * L + ppos0 + row) * CH + ch8;
-    if (ok) {
-      *reinterpret_cast<uint4*>(s1 + off) = oq;
-      if constexpr (STORE) {
-        *reinterpret_cast<uint4*>(gdn + off) = make_uint4(e.dn[0], e.dn[1], e.dn[2], e.dn[3]);
-        *reinterpret_cast<uint4*>(gdw + off) = make_uint4(e.dw[0], e.dw[1], e.dw[2], e.dw[3]);
-      }
-    }
-    float orr[8];
-    unpack8(oq, orr);                           // LayerNorm partial of the stored (rounded) values
-    f32x2 rs = {0.f, 0.f};
-#pragma unroll
-    for (int k = 0; k < 8; k += 2) rs += (f32x2){orr[k] + orr[k + 1], orr[k] * orr[k] + orr[k + 1] * orr[k + 1]};
-    e.ln += ok ? rs : (f32x2){0.f, 0.f};
-  };
-  auto epi_reduce = [&]() {
-    const float sa = wave_reduce_sum(e.ln.x), sq = wave_reduce_sum(e.ln.y);
-    if (lane == 0) {
-      scratch[2 * w] = sa;
-      scratch[2 * w + 1] = sq;
-    }
-  };
-  // slice kb of tap k (kb compile-time, k runtime and wave-uniform)
-  auto epi_slice = [&](int k, const int kb) {
-    const int i = k >> 1;
-    if (k == 8) {
-      if (kb == 0) epi_reduce();
-    } else if ((k & 1) == 0) {
-      if (kb == 0) epi_load(i);
-      else if (kb == 1) gelu_pair(0);
-      else if (kb == 2) gelu_pair(1);
-      else if (kb == 4) gelu_pair(2);
-      else if (kb == 6) gelu_pair(3);
-    } else {
-      if (kb == 0) gelu_pair(4);
-      else if (kb == 2) gelu_pair(5);
-      else if (kb == 4) gelu_pair(6);
-      else if (kb == 5) gelu_pair(7);
-      else if (kb == 7) epi_combine(i);
-    }
-  };
-
-  // (sum, sum of squares) of the previous tile's 8 waves -> its (mean, M2) partial (after a barrier)
-  auto finish_stats = [&]() {
-    if (tid == 0 && ptile >= 0) {
-      float sa = 0.f, sq = 0.f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        sa += scratch[2 * i];
-        sq += scratch[2 * i + 1];
-      }
-      const float n = (float)(pvrows * CH), m = sa / n;
-      stats[ptile * 2] = m;
-      stats[ptile * 2 + 1] = fmaxf(sq - sa * m, 0.f);
-    }
-  };
-
-  long tile0 = tile_of(0, G);
-  if (tile0 < NT) stage_x(tile0, smem);
-  for (long rd = 0; rd < rounds; ++rd) {
-    const long tile = tile_of(rd, G);
-    const bool have = tile < NT;                // this workgroup has a tile this round (uniform)
-    unsigned char* xs = smem + (rd & 1) * XB;
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");   // x tile landed; staging published
-    if (rd + 1 < rounds) {
-      const long nt = tile_of(rd + 1, G);
-      if (nt < NT) stage_x(nt, smem + ((rd + 1) & 1) * XB);
-    }
-    const bool act = ptile >= 0;
-    f32x16_t acc[NPT];
-#pragma unroll
-    for (int i = 0; i < NPT; ++i) acc[i] = zero16();
-    if (have) {
-      bf16x8 bq[2][NPT];
-      auto rows_of = [&](int k, int& rowb, int& gs) {
-        const int rb = halo + r + (k - half) * d;
-        rowb = rb << 8;
-        gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
-      };
-      int rowb, gs;
-      rows_of(0, rowb, gs);
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt) bq[0][pt] = lds_frag(xs, (0 ^ gs) + rowb + pt * 8192);
-      for (int k = 0; k < KS; ++k) {
-        int rowbn, gsn;
-        rows_of(k + 1 < KS ? k + 1 : KS - 1, rowbn, gsn);
-#pragma unroll
-        for (int kb = 0; kb < 8; ++kb) {
-          const int it = k * 8 + kb;
-          const int nf = it + 3 < NI ? it + 3 : it + 3 - NI;      // ring runs on into the next tile
-          fr[(kb + 3) & 3] = wfrag(nf);
-          const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
-#pragma unroll
-          for (int pt = 0; pt < NPT; ++pt) bq[(kb + 1) & 1][pt] = lds_frag(xs, noff + pt * 8192);
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], bq[kb & 1][pt], acc[pt]);
-          if (act) epi_slice(k, kb);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        rowb = rowbn;
-        gs = gsn;
-      }
-    } else if (act) {
-      // no tile this round (grid tail): only the previous tile's epilogue
-      for (int k = 0; k < KS; ++k) {
-#pragma unroll
-        for (int kb = 0; kb < 8; ++kb) epi_slice(k, kb);
-      }
-    }
-    __syncthreads();                            // staging / scratch consumed; x buffer free
-    finish_stats();
-    ptile = -1;
-    if (have) {
-      // acc + bias -> staging (bf16 pre-activations of this tile), read by the next round's epilogue
-      unsigned char* dst = cv ? stw : stn;
-      const float* bv = bias + cv * CH;
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c0 = cq * 32 + 8 * g + 4 * h;
-          const float4 b4 = *reinterpret_cast<const float4*>(bv + c0);
-          const float v[4] = {acc[pt][4 * g] + b4.x, acc[pt][4 * g + 1] + b4.y, acc[pt][4 * g + 2] + b4.z,
-                              acc[pt][4 * g + 3] + b4.w};
-          *reinterpret_cast<uint2*>(dst + swz256e(pt * 32 + r, c0)) = packq4(v);
-        }
-      ptile = tile;
-      pb = (int)(tile / T);
-      ppos0 = (int)(tile - (long)pb * T) * BM;
-      pvrows = min(BM, L - ppos0);
-    }
-  }
-  // the last tile's epilogue
-  if (ptile >= 0) {
-    __syncthreads();
-    for (int k = 0; k < KS; ++k) {
-#pragma unroll
-      for (int kb = 0; kb < 8; ++kb) epi_slice(k, kb);
-    }
-    __syncthreads();
-    finish_stats();
-  }
-}
-
-bool conv4_attr_set = false;
 
 // ------------------------------------------------------------------------------------------------
 // Data gradient, one wave per 32 input channels over BOTH convolutions (reference modules.py:205-206
 // backward):  dx[pos][ci] = ds1[pos][ci] + sum_conv sum_tap sum_co W[co][ci][tap] dpre_conv[pos - shift][co]
 //
-// conv_dgrad3 (conv2.hip) split the two convolutions over two wave groups (8 waves, waves 4-7 = wide)
-// and summed their fp32 partials through a 64 KB LDS tile with two extra barriers before the dx pass.
-// Here each of the 4 waves runs the K loop of both convolutions (2 x 72 K-steps, 4 MFMAs each) into
+// (The round-2 form split the two convolutions over two wave groups and summed their fp32 partials through
+// a 64 KB LDS tile with two extra barriers before the dx pass.)  Here each of the 4 waves runs the K loop of both convolutions (2 x 72 K-steps, 4 MFMAs each) into
 // ONE accumulator set, so the cross-wave reduction disappears; the weight-fragment ring (buffer loads,
 // scalar offsets) runs straight from the narrow into the wide image.  dpre = ds1 * GELU'(pre) tiles
 // (GELU' stored by the forward) with their halos are staged once per workgroup; their central rows go
@@ -646,7 +344,7 @@ int conv_dgrad4_lds(int dil) {
   return a > e ? a : e;
 }
 
-// Same contract as pbx_conv_dgrad3 (KS = 9): gdn / gdw are the GELU'(pre) images the forward stored.
+// KS = 9: gdn / gdw are the GELU'(pre) images the forward (pbx_conv_fwd3) stored.
 // ilo / ihi: halo rows of ds1 and GELU' from the neighbouring shards (context parallelism; both inputs
 // [B][ilo + L + ihi][128]); outputs dx, dpre_n, dpre_w are [B][L][128].  0 / 0 for a whole sequence.
 PBX_EXPORT int pbx_conv_dgrad4x(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
@@ -692,38 +390,4 @@ PBX_EXPORT int pbx_conv_dgrad4f(const void* dh1, const void* s1, const float* st
 PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
                                void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
   return pbx_conv_dgrad4x(ds1, gdn, gdw, ftn, ftw, dx, dpre_n, dpre_w, B, L, KS_, dil, 0, 0, st);
-}
-
-int conv_fwd4_lds(int dil) { return 2 * (BM + 8 * dil) * 256 + 2 * BM * 256 + (2 * CH + 16) * 4; }
-
-// Same contract as pbx_conv_fwd3 (KS = 9 only); gdn / gdw: GELU'(pre) outputs, or both null.
-// xlo / xhi: rows of neighbouring sequence shards stored before / after each sample's L rows of x
-// (context parallelism: x is [B][xlo + L + xhi][128], logical positions -xlo .. L + xhi - 1 are real,
-// anything beyond is the conv's zero padding); 0 / 0 for a whole sequence.
-PBX_EXPORT int pbx_conv_fwd4x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                              const float* gb, void* gdn, void* gdw, void* s1, float* stats, int B, int L, int KS_,
-                              int dil, int xlo, int xhi, hipStream_t st) {
-  const int lds = conv_fwd4_lds(dil);
-  if (KS_ != KS || dil < 1 || lds > 163840 || gb == nullptr || B < 1 || L < 1 || xlo < 0 || xhi < 0)
-    return (int)hipErrorInvalidValue;
-  if ((gdn == nullptr) != (gdw == nullptr)) return (int)hipErrorInvalidValue;
-  if (!conv4_attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_fwd4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    (void)hipFuncSetAttribute((const void*)conv_fwd4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    conv4_attr_set = true;
-  }
-  int dev = 0, ncu = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-  const long NT = (long)B * ((L + BM - 1) / BM);
-  const int grid = (int)(NT < ncu ? NT : ncu);
-  const auto kern = gdn != nullptr ? conv_fwd4_kernel<true> : conv_fwd4_kernel<false>;
-  hipLaunchKernelGGL(kern, dim3(grid), dim3(512), lds, st, (const bf16_t*)x, (const bf16x8*)fwn, (const bf16x8*)fww,
-                     bn, bw, gb, (bf16_t*)gdn, (bf16_t*)gdw, (bf16_t*)s1, stats, B, L, dil, xlo, xhi);
-  return pbx_launch_status();
-}
-
-PBX_EXPORT int pbx_conv_fwd4(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                             const float* gb, void* gdn, void* gdw, void* s1, float* stats, int B, int L, int KS_,
-                             int dil, hipStream_t st) {
-  return pbx_conv_fwd4x(x, fwn, fww, bn, bw, gb, gdn, gdw, s1, stats, B, L, KS_, dil, 0, 0, st);
 }

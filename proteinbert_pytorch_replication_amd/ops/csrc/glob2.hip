@@ -1,5 +1,5 @@
-// Fused global track of one ProteinBERT block: ONE launch per block forward and one per block
-// backward ("persistent global-track kernel").
+// Fused global track of one ProteinBERT block, backward: ONE launch per block ("persistent
+// global-track kernel"); the forward is the column-split glob3.hip.
 //
 // Reference: ProteinBERT/modules.py:175-199,219-229 (g + GELU(Linear G->G) + attention -> LayerNorm(G),
 // twice) and :166-173,208-209 (the next block's global->local vector GELU(Linear G->C)), reference
@@ -20,7 +20,6 @@
 // Backward data path in the same structure; the weight gradients dW = dU^T X (K = B rows) are
 // left to three library GEMMs the caller issues off the critical path.
 #include "mfma.h"
-#include <stdlib.h>
 
 using namespace pbx;
 typedef unsigned short bf16_t;
@@ -124,181 +123,6 @@ __device__ __forceinline__ float wave_mean(const float* __restrict__ wp, int K, 
   float a = 0.f;
   for (int i = lane; i < K; i += 64) a += wp[i];
   return wave_reduce_sum(a) / (float)K;
-}
-
-// ------------------------------------------------------------------------------------------------
-// forward.  NW waves of NT column tiles each (G = 16 NT NW); NGL = 0 (last block, no gb) or 128
-// (waves 0 .. NGL/16 - 1 compute one gb column tile each).
-template <int NT, int NW, int NGL>
-__global__ void __launch_bounds__(NW * 64) glob_fwd_kernel(
-    const float* __restrict__ g, const bf16_t* __restrict__ g_bf, const float* __restrict__ vpart, int TV,
-    const float* __restrict__ wp, int K, const bf16x8* __restrict__ f1, const float* __restrict__ b1,
-    const float* __restrict__ n1w, const float* __restrict__ n1b, const bf16x8* __restrict__ f2,
-    const float* __restrict__ b2, const float* __restrict__ n2w, const float* __restrict__ n2b,
-    const bf16x8* __restrict__ fgl, const float* __restrict__ bgl, float* __restrict__ pre1, float* __restrict__ xh1,
-    float* __restrict__ r1, float* __restrict__ vsum, bf16_t* __restrict__ g1_bf, float* __restrict__ pre2,
-    float* __restrict__ xh2, float* __restrict__ r2, float* __restrict__ g2, bf16_t* __restrict__ g2_bf,
-    float* __restrict__ pregl, float* __restrict__ gb, int B, float eps) {
-  constexpr int G = NT * 16 * NW, NT3 = NGL > 0 ? 1 : 0;
-  __shared__ __attribute__((aligned(16))) unsigned char at[RB * G * 2];
-  __shared__ float red[NW * RB];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c16 = lane & 15, q = lane >> 4;
-  const int row0 = blockIdx.x * RB;
-  int grow[4];
-  bool rok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rok[i] = row0 + 4 * q + i < B;
-    grow[i] = min(row0 + 4 * q + i, B - 1);       // clamped: loads stay in bounds, stores masked
-  }
-  const int col0 = w * NT * 16;
-  const float scale = wave_mean(wp, K, lane);
-  // A tile <- g_bf rows
-  for (int idx = tid; idx < RB * G / 8; idx += NW * 64) {
-    const int row = idx / (G / 8), ch = idx % (G / 8);
-    const int gr = min(row0 + row, B - 1);
-    *reinterpret_cast<uint4*>(at + atile(row, ch, G)) =
-        *reinterpret_cast<const uint4*>(g_bf + (size_t)gr * G + ch * 8);
-  }
-  float res[NT][4], vs[NT][4];
-#pragma unroll
-  for (int t = 0; t < NT; ++t)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      res[t][i] = g[(size_t)grow[i] * G + col0 + t * 16 + c16];
-      vs[t][i] = 0.f;
-    }
-  // attention partial sums: the loads of TVU tiles are in flight together (clamped tile index, the
-  // surplus ones weighted 0: no branch, so no wait per tile)
-  constexpr int TVU = 4;
-  for (int tv0 = 0; tv0 < TV; tv0 += TVU) {
-    float v[TVU][NT][4];
-#pragma unroll
-    for (int u = 0; u < TVU; ++u) {
-      const int tv = min(tv0 + u, TV - 1);
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[u][t][i] = vpart[((size_t)grow[i] * TV + tv) * G + col0 + t * 16 + c16];
-    }
-#pragma unroll
-    for (int u = 0; u < TVU; ++u) {
-      const float m = tv0 + u < TV ? 1.f : 0.f;
-#pragma unroll
-      for (int t = 0; t < NT; ++t)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) vs[t][i] = fmaf(m, v[u][t][i], vs[t][i]);
-    }
-  }
-  __syncthreads();
-
-  auto ln_block = [&](const f4_t* acc, const float* bias, const float* gam, const float* bet, bool attn,
-                      float* __restrict__ pre_o, float* __restrict__ xh_o, float* __restrict__ r_o,
-                      float* __restrict__ out_f32, bf16_t* __restrict__ out_bf, float (*keep)[4]) {
-    float z[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int c = col0 + t * 16 + c16;
-      const float bc = bias[c];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = acc[t][i] + bc;
-        if (rok[i]) pre_o[(size_t)grow[i] * G + c] = p;
-        float v = res[t][i] + gelu_f(p);
-        if (attn) v += scale * vs[t][i];
-        z[t][i] = v;
-      }
-    }
-    float mean[4], var[4];
-    row_sums<NT, NW>(z, red, mean, lane, w);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) mean[i] *= 1.f / (float)G;
-    float d2[NT][4];
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) d2[t][i] = (z[t][i] - mean[i]) * (z[t][i] - mean[i]);
-    row_sums<NT, NW>(d2, red, var, lane, w);
-    float rs[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) rs[i] = rsqrtf(var[i] * (1.f / (float)G) + eps);
-    if (c16 == 0 && w == 0) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (rok[i]) r_o[grow[i]] = rs[i];
-    }
-    __syncthreads();                              // every wave is done reading the A tile
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      const int c = col0 + t * 16 + c16;
-      const float ga = gam[c], be = bet[c];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float xh = (z[t][i] - mean[i]) * rs[i];
-        const float o = xh * ga + be;
-        const bf16_t ob = f2bf(o);
-        keep[t][i] = o;
-        *reinterpret_cast<bf16_t*>(at + atile_e(4 * q + i, c, G)) = ob;
-        if (rok[i]) {
-          const size_t e = (size_t)grow[i] * G + c;
-          xh_o[e] = xh;
-          out_bf[e] = ob;
-          if (out_f32 != nullptr) out_f32[e] = o;
-        }
-      }
-    }
-    __syncthreads();                              // next A tile complete
-  };
-
-  // ---- g1 = LN1(g + GELU(g W1^T + b1) + scale * sum_t vpart) ----
-  {
-    f4_t acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = (f4_t){0.f, 0.f, 0.f, 0.f};
-    gemm_rows<NT>(acc, at, G, f1, w * NT, lane);
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        if (rok[i]) vsum[(size_t)grow[i] * G + col0 + t * 16 + c16] = vs[t][i];
-    float g1v[NT][4];
-    ln_block(acc, b1, n1w, n1b, true, pre1, xh1, r1, nullptr, g1_bf, g1v);
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) res[t][i] = g1v[t][i];
-  }
-  // ---- g2 = LN2(g1 + GELU(g1 W2^T + b2)) ----
-  {
-    f4_t acc[NT];
-#pragma unroll
-    for (int t = 0; t < NT; ++t) acc[t] = (f4_t){0.f, 0.f, 0.f, 0.f};
-    gemm_rows<NT>(acc, at, G, f2, w * NT, lane);
-    float g2v[NT][4];
-    ln_block(acc, b2, n2w, n2b, false, pre2, xh2, r2, g2, g2_bf, g2v);
-  }
-  // ---- gb = GELU(g2 Wgl^T + bgl) (the next block's global->local vector) ----
-  if constexpr (NT3 > 0) {
-    if (w >= NGL / 16) return;                    // (no barrier below)
-    f4_t acc[NT3];
-#pragma unroll
-    for (int t = 0; t < NT3; ++t) acc[t] = (f4_t){0.f, 0.f, 0.f, 0.f};
-    gemm_rows<NT3>(acc, at, G, fgl, w * NT3, lane);
-#pragma unroll
-    for (int t = 0; t < NT3; ++t) {
-      const int c = w * NT3 * 16 + t * 16 + c16;
-      const float bc = bgl[c];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float p = acc[t][i] + bc;
-        if (rok[i]) {
-          pregl[(size_t)grow[i] * NGL + c] = p;
-          gb[(size_t)grow[i] * NGL + c] = gelu_f(p);
-        }
-      }
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -486,17 +310,6 @@ __global__ void __launch_bounds__(256) pack_glob_frags_kernel(const float* __res
 }
 
 template <int NT, int NW, int NGL>
-void launch_fwd(int B, const void* const* p, const int* iv, float eps, hipStream_t st) {
-  hipLaunchKernelGGL((glob_fwd_kernel<NT, NW, NGL>), dim3((B + RB - 1) / RB), dim3(NW * 64), 0, st, (const float*)p[0],
-                     (const bf16_t*)p[1], (const float*)p[2], iv[0], (const float*)p[3], iv[1],
-                     (const bf16x8*)p[4], (const float*)p[5], (const float*)p[6], (const float*)p[7],
-                     (const bf16x8*)p[8], (const float*)p[9], (const float*)p[10], (const float*)p[11],
-                     (const bf16x8*)p[12], (const float*)p[13], (float*)p[14], (float*)p[15], (float*)p[16],
-                     (float*)p[17], (bf16_t*)p[18], (float*)p[19], (float*)p[20], (float*)p[21], (float*)p[22],
-                     (bf16_t*)p[23], (float*)p[24], (float*)p[25], B, eps);
-}
-
-template <int NT, int NW, int NGL>
 void launch_bwd(int B, const void* const* p, int K, float* slab, hipStream_t st) {
   hipLaunchKernelGGL((glob_bwd_kernel<NT, NW, NGL>), dim3((B + RB - 1) / RB), dim3(NW * 64), 0, st, (const float*)p[0],
                      (const float*)p[1], (const float*)p[2], (const bf16x8*)p[3], (const float*)p[4],
@@ -507,32 +320,11 @@ void launch_bwd(int B, const void* const* p, int K, float* slab, hipStream_t st)
                      (float*)p[23], (float*)p[24], (float*)p[25], (float*)p[26], (float*)p[27], (float*)p[28], B,
                      slab, K);
 }
-// forward waves per workgroup: 16 (half the column tiles per wave: shorter dependent chains per
-// row block) or 8; PBX_GLOB_WAVES overrides
-int glob_waves() {
-  static const int wv = getenv("PBX_GLOB_WAVES") ? atoi(getenv("PBX_GLOB_WAVES")) : 16;
-  return wv;
-}
 }  // namespace
 
 // G in {256, 512}; NGL in {0, 128} (the local width C = 128 of the paper configuration).
 static int pbx_glob_supported(int G, int NGL) {   // mirrored by global_track.glob_fused_ok
   return (G == 256 || G == 512) && (NGL == 0 || NGL == 128);
-}
-
-// p: g, g_bf, vpart, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b, fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2,
-//    r2, g2, g2_bf, pregl, gb   (26 pointers; fgl/bgl/pregl/gb null when NGL == 0)
-PBX_EXPORT int pbx_glob_fwd(const void* const* p, int B, int G, int NGL, int TV, int K, float eps, hipStream_t st) {
-  if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1) return (int)hipErrorInvalidValue;
-  const int iv[2] = {TV, K};
-  if (glob_waves() == 16) {
-    if (G == 512) (NGL ? launch_fwd<2, 16, 128> : launch_fwd<2, 16, 0>)(B, p, iv, eps, st);
-    else (NGL ? launch_fwd<1, 16, 128> : launch_fwd<1, 16, 0>)(B, p, iv, eps, st);
-  } else {
-    if (G == 512) (NGL ? launch_fwd<4, 8, 128> : launch_fwd<4, 8, 0>)(B, p, iv, eps, st);
-    else (NGL ? launch_fwd<2, 8, 128> : launch_fwd<2, 8, 0>)(B, p, iv, eps, st);
-  }
-  return pbx_launch_status();
 }
 
 extern "C" int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, float* dst, const float* scale,
@@ -542,26 +334,11 @@ extern "C" int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, f
 //    db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl, dwp   (29 pointers)
 // slab (nullable, deterministic mode): [ceil(B / 16)][6 G + NGL + K] fp32 column-sum partials, folded into
 // the eight gradient destinations in a fixed order
-static int g_bwd_waves = -1;
-// waves per workgroup of pbx_glob_bwd: 8 (default) or 4 (tests select both)
-PBX_EXPORT int pbx_glob_set_bwd_waves(int w) {
-  if (w != 4 && w != 8) return (int)hipErrorInvalidValue;
-  g_bwd_waves = w;
-  return 0;
-}
-
 PBX_EXPORT int pbx_glob_bwd(const void* const* p, int B, int G, int NGL, int K, float* slab, hipStream_t st) {
   if (!pbx_glob_supported(G, NGL) || B < 1 || K < 1 || K > 512) return (int)hipErrorInvalidValue;
-  // (a 16-wave build of the backward does not fit 128 VGPRs: it stays at 8 waves; PBX_GLOB_BWD_WAVES=4: a
-  // 4-wave form with the workgroup shape of conv_dgrad4, so the two share CUs when they run side by side)
-  if (g_bwd_waves < 0) g_bwd_waves = getenv("PBX_GLOB_BWD_WAVES") ? atoi(getenv("PBX_GLOB_BWD_WAVES")) : 8;
-  if (g_bwd_waves == 4) {
-    if (G == 512) (NGL ? launch_bwd<8, 4, 128> : launch_bwd<8, 4, 0>)(B, p, K, slab, st);
-    else (NGL ? launch_bwd<4, 4, 128> : launch_bwd<4, 4, 0>)(B, p, K, slab, st);
-  } else {
-    if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, slab, st);
-    else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, slab, st);
-  }
+  // 8 waves (a 16-wave build does not fit 128 VGPRs; a 4-wave form measured no better beside conv_dgrad4)
+  if (G == 512) (NGL ? launch_bwd<4, 8, 128> : launch_bwd<4, 8, 0>)(B, p, K, slab, st);
+  else (NGL ? launch_bwd<2, 8, 128> : launch_bwd<2, 8, 0>)(B, p, K, slab, st);
   int rc = pbx_launch_status();
   if (rc != 0 || slab == nullptr) return rc;
   const int rows = (B + RB - 1) / RB, ld = 6 * G + NGL + K;

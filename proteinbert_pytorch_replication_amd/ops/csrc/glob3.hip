@@ -1,5 +1,6 @@
-// Global track of one ProteinBERT block, column-split: three launches forward and three backward,
-// each over ceil(B / 16) x (G / 64) workgroups (256 at B = G = 512) instead of B / 16.
+// Global track of one ProteinBERT block, forward, column-split: three launches, each over ceil(B / 16) x
+// (G / 64) workgroups (256 at B = G = 512) instead of B / 16.  The backward is the one-launch
+// glob2.hip glob_bwd (a column-split backward measured slower beside the weight-gradient stream).
 //
 // Reference: ProteinBERT/modules.py:175-199,219-229 (g + GELU(Linear G->G) + attention -> LayerNorm(G),
 // twice) and :166-173,208-209 (the next block's global->local vector GELU(Linear G->C)), reference
@@ -11,9 +12,7 @@
 // 64-column output tile of one layer: it streams 64 KB of weights, the row LayerNorm is carried
 // between launches as per-(row, column tile) partials ((mean, M2) forward, plain sums backward) that
 // the next launch folds in its prologue while it normalises the full rows of its A tile, and the
-// kernel boundary (~2 us) is the only synchronisation.  Column sums of the bias / affine / attention
-// weight gradients go to a per-row-tile slab (every workgroup writes its own columns; deterministic)
-// folded by one launch on the weight-gradient stream.
+// kernel boundary (~2 us) is the only synchronisation.
 //
 // MFMA v_mfma_f32_16x16x32_bf16: A = 16 activation rows (bf16, XOR-swizzled LDS tile), B = weight
 // fragments in the packed layout of pbx_pack_glob_frags (one coalesced 1-KB load per fragment and
@@ -121,23 +120,6 @@ __device__ __forceinline__ void fold_ln_stats(const float2* __restrict__ part, i
     }
     st[2 * t] = m;
     st[2 * t + 1] = rsqrtf(M2 / (float)G + eps);
-  }
-}
-
-// per-row (m1, m2) = (sum dxh, sum dxh xh) / G of the LayerNorm backward from NCT column-tile sums
-__device__ __forceinline__ void fold_bwd_stats(const float2* __restrict__ part, int NCT, int G, int row0, int B,
-                                               float* st) {
-  const int t = threadIdx.x;
-  if (t < RB) {
-    const int row = min(row0 + t, B - 1);
-    float a = 0.f, c = 0.f;
-    for (int k = 0; k < NCT; ++k) {
-      const float2 p = part[(size_t)row * NCT + k];
-      a += p.x;
-      c += p.y;
-    }
-    st[2 * t] = a / (float)G;
-    st[2 * t + 1] = c / (float)G;
   }
 }
 
@@ -330,262 +312,7 @@ __global__ void __launch_bounds__(256) glob3_fwd3_kernel(
   }
 }
 
-// slab row layout (one row per 16-row tile): [db1 | dn1w | dn1b | db2 | dn2w | dn2b] (G each) | dbgl
-// (NGL) | dwp partials (G / 64)
-enum { S_DB1 = 0, S_DN1W, S_DN1B, S_DB2, S_DN2W, S_DN2B };
-
-// ---- backward 1: dugl = dgb * GELU'(pregl) (A tile, K = NGL), dg2 += dugl Wgl; LayerNorm-2 backward
-// partials (sum dxh, sum dxh xh2) per (row, column tile); dn2w / dn2b column sums ------------------
-__global__ void __launch_bounds__(256) glob3_bwd1_kernel(
-    const float* __restrict__ dg2_in, const float* __restrict__ dgb, const float* __restrict__ pregl,
-    const bf16x8* __restrict__ fglT, const float* __restrict__ xh2, const float* __restrict__ n2w,
-    float* __restrict__ dg2_out, bf16_t* __restrict__ dugl, float2* __restrict__ part, float* __restrict__ slab,
-    int ld, int B, int G, int NGL) {
-  __shared__ __attribute__((aligned(16))) unsigned char at[RB * 128 * 2];
-  __shared__ float red[4 * RB];
-  __shared__ float dsl[RB * 128];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c16 = lane & 15, q = lane >> 4;
-  const int row0 = blockIdx.x * RB, ct = blockIdx.y * 4 + w, col = ct * 16 + c16;
-  float* srow = slab + (size_t)blockIdx.x * ld;
-  int grow[4];
-  bool rok[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rok[i] = row0 + 4 * q + i < B;
-    grow[i] = min(row0 + 4 * q + i, B - 1);
-  }
-  float dg[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) dg[i] = dg2_in[(size_t)grow[i] * G + col];
-  if (NGL > 0) {
-    for (int idx = tid; idx < RB * NGL / 8; idx += 256) {
-      const int row = idx / (NGL / 8), ch = idx % (NGL / 8);
-      const int gr = min(row0 + row, B - 1);
-      float dv[8], pv[8], o[8];
-      load8(dgb + (size_t)gr * NGL + ch * 8, dv);
-      load8(pregl + (size_t)gr * NGL + ch * 8, pv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = row0 + row < B ? dv[e] * gelu_grad_f(pv[e]) : 0.f;
-      const uint4 ob = packq8(o);
-      *reinterpret_cast<uint4*>(at + atile(row, ch, NGL)) = ob;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dsl[row * 128 + ch * 8 + e] = o[e];
-      if (blockIdx.y == 0 && row0 + row < B) *reinterpret_cast<uint4*>(dugl + (size_t)gr * NGL + ch * 8) = ob;
-    }
-    __syncthreads();
-    if (blockIdx.y == 0 && tid < NGL) {            // dbgl column sums (fp32 values) of the 16 rows
-      float a = 0.f;
-#pragma unroll
-      for (int r = 0; r < RB; ++r) a += dsl[r * 128 + tid];
-      srow[6 * G + tid] = a;
-    }
-    const f4_t acc = gemm16(at, NGL, fglT, ct, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) dg[i] += acc[i];
-  }
-  const float gw = n2w[col];
-  float dxh[4], dxx[4], xv[4], sa[4], sc[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    xv[i] = xh2[(size_t)grow[i] * G + col];
-    dxh[i] = dg[i] * gw;
-    dxx[i] = dxh[i] * xv[i];
-    if (rok[i]) dg2_out[(size_t)grow[i] * G + col] = dg[i];
-  }
-  tile_row_sums(dxh, red, sa, lane, w);
-  tile_row_sums(dxx, red, sc, lane, w);
-  if (w == 0 && c16 == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (rok[i]) part[(size_t)grow[i] * (G / CT) + blockIdx.y] = make_float2(sa[i], sc[i]);
-  }
-  float t1[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) t1[i] = dg[i] * xv[i];
-  const float cw = col_sum16(t1, rok), cb = col_sum16(dg, rok);
-  if (lane < 16) {
-    srow[S_DN2W * G + col] = cw;
-    srow[S_DN2B * G + col] = cb;
-  }
-}
-
-// LayerNorm backward of one element: dz = r (dxh - m1 - xh m2), dxh = dg * gamma
-__device__ __forceinline__ float ln_bwd(float dg, float gam, float xh, float r, float m1, float m2) {
-  return r * (dg * gam - m1 - xh * m2);
-}
-
-// Prologue of backward 2 / 3: fold the partials; A tile = bf16 dpre = dz * GELU'(pre) of the 16 full
-// rows; this workgroup's columns of du (bf16) are written.
-__device__ __forceinline__ void bwd_prologue(const float* __restrict__ dgin, const float2* __restrict__ part,
-                                             const float* __restrict__ xh, const float* __restrict__ r,
-                                             const float* __restrict__ gam, const float* __restrict__ pre,
-                                             bf16_t* __restrict__ du, unsigned char* at, float* st, int row0, int B,
-                                             int G) {
-  const int tid = threadIdx.x;
-  fold_bwd_stats(part, G / CT, G, row0, B, st);
-  __syncthreads();
-  const int c0 = blockIdx.y * CT;
-  for (int idx = tid; idx < RB * G / 8; idx += 256) {
-    const int row = idx / (G / 8), ch = idx % (G / 8);
-    const int gr = min(row0 + row, B - 1);
-    const float m1 = st[2 * row], m2 = st[2 * row + 1], rr = r[gr];
-    float dv[8], xv[8], gw[8], pv[8], o[8];
-    load8(dgin + (size_t)gr * G + ch * 8, dv);
-    load8(xh + (size_t)gr * G + ch * 8, xv);
-    load8(gam + ch * 8, gw);
-    load8(pre + (size_t)gr * G + ch * 8, pv);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = row0 + row < B ? ln_bwd(dv[e], gw[e], xv[e], rr, m1, m2) * gelu_grad_f(pv[e]) : 0.f;
-    const uint4 ob = packq8(o);
-    *reinterpret_cast<uint4*>(at + atile(row, ch, G)) = ob;
-    if (ch * 8 >= c0 && ch * 8 < c0 + CT && row0 + row < B) *reinterpret_cast<uint4*>(du + (size_t)gr * G + ch * 8) = ob;
-  }
-  __syncthreads();
-}
-
-// ---- backward 2: dz2 (LayerNorm-2 backward), du2 = dz2 GELU'(pre2) (A tile), dg1 = dz2 + du2 W2;
-// LayerNorm-1 backward partials of dg1; db2 / dn1w / dn1b column sums ------------------------------
-__global__ void __launch_bounds__(256) glob3_bwd2_kernel(
-    const float* __restrict__ dg2, const float2* __restrict__ part2, const float* __restrict__ xh2,
-    const float* __restrict__ r2, const float* __restrict__ n2w, const float* __restrict__ pre2,
-    const bf16x8* __restrict__ f2T, const float* __restrict__ xh1, const float* __restrict__ n1w,
-    bf16_t* __restrict__ du2, float* __restrict__ dg1_out, float2* __restrict__ part1, float* __restrict__ slab,
-    int ld, int B, int G) {
-  __shared__ __attribute__((aligned(16))) unsigned char at[RB * GMAX * 2];
-  __shared__ float red[4 * RB];
-  __shared__ float st[2 * RB];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c16 = lane & 15, q = lane >> 4;
-  const int row0 = blockIdx.x * RB, ct = blockIdx.y * 4 + w, col = ct * 16 + c16;
-  float* srow = slab + (size_t)blockIdx.x * ld;
-  bwd_prologue(dg2, part2, xh2, r2, n2w, pre2, du2, at, st, row0, B, G);
-  int grow[4];
-  bool rok[4];
-  float dz[4], dpre[4];
-  const float gw2 = n2w[col];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rok[i] = row0 + 4 * q + i < B;
-    grow[i] = min(row0 + 4 * q + i, B - 1);
-    const size_t e = (size_t)grow[i] * G + col;
-    const int rl = 4 * q + i;
-    dz[i] = ln_bwd(dg2[e], gw2, xh2[e], r2[grow[i]], st[2 * rl], st[2 * rl + 1]);
-    dpre[i] = dz[i] * gelu_grad_f(pre2[e]);
-  }
-  const f4_t acc = gemm16(at, G, f2T, ct, lane);
-  const float gw1 = n1w[col];
-  float dg1[4], dxh[4], dxx[4], xv[4], sa[4], sc[4], t1[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dg1[i] = dz[i] + acc[i];
-    xv[i] = xh1[(size_t)grow[i] * G + col];
-    dxh[i] = dg1[i] * gw1;
-    dxx[i] = dxh[i] * xv[i];
-    t1[i] = dg1[i] * xv[i];
-    if (rok[i]) dg1_out[(size_t)grow[i] * G + col] = dg1[i];
-  }
-  tile_row_sums(dxh, red, sa, lane, w);
-  tile_row_sums(dxx, red, sc, lane, w);
-  if (w == 0 && c16 == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (rok[i]) part1[(size_t)grow[i] * (G / CT) + blockIdx.y] = make_float2(sa[i], sc[i]);
-  }
-  const float cdb2 = col_sum16(dpre, rok), cw = col_sum16(t1, rok), cb = col_sum16(dg1, rok);
-  if (lane < 16) {
-    srow[S_DB2 * G + col] = cdb2;
-    srow[S_DN1W * G + col] = cw;
-    srow[S_DN1B * G + col] = cb;
-  }
-}
-
-// ---- backward 3: dz1 (LayerNorm-1 backward), du1 = dz1 GELU'(pre1) (A tile), dg = dz1 + du1 W1,
-// dvs = scale dz1 (the attention partial-sum gradient); db1 column sums, dwp partials --------------
-__global__ void __launch_bounds__(256) glob3_bwd3_kernel(
-    const float* __restrict__ dg1, const float2* __restrict__ part1, const float* __restrict__ xh1,
-    const float* __restrict__ r1, const float* __restrict__ n1w, const float* __restrict__ pre1,
-    const float* __restrict__ vsum, const float* __restrict__ wp, int K, const bf16x8* __restrict__ f1T,
-    bf16_t* __restrict__ du1, float* __restrict__ dg, float* __restrict__ dvs, float* __restrict__ slab, int ld,
-    int B, int G, int NGL) {
-  __shared__ __attribute__((aligned(16))) unsigned char at[RB * GMAX * 2];
-  __shared__ float red[4 * RB];
-  __shared__ float st[2 * RB];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int c16 = lane & 15, q = lane >> 4;
-  const int row0 = blockIdx.x * RB, ct = blockIdx.y * 4 + w, col = ct * 16 + c16;
-  float* srow = slab + (size_t)blockIdx.x * ld;
-  bwd_prologue(dg1, part1, xh1, r1, n1w, pre1, du1, at, st, row0, B, G);
-  const float scale = mean_of(wp, K, lane);
-  int grow[4];
-  bool rok[4];
-  float dz[4], dpre[4], av[4];
-  const float gw1 = n1w[col];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    rok[i] = row0 + 4 * q + i < B;
-    grow[i] = min(row0 + 4 * q + i, B - 1);
-    const size_t e = (size_t)grow[i] * G + col;
-    const int rl = 4 * q + i;
-    dz[i] = ln_bwd(dg1[e], gw1, xh1[e], r1[grow[i]], st[2 * rl], st[2 * rl + 1]);
-    dpre[i] = dz[i] * gelu_grad_f(pre1[e]);
-    av[i] = rok[i] ? dz[i] * vsum[e] : 0.f;
-    if (rok[i]) dvs[e] = scale * dz[i];
-  }
-  const f4_t acc = gemm16(at, G, f1T, ct, lane);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (rok[i]) dg[(size_t)grow[i] * G + col] = dz[i] + acc[i];
-  const float cdb1 = col_sum16(dpre, rok);
-  if (lane < 16) srow[S_DB1 * G + col] = cdb1;
-  // dwp partial: sum over the tile of dz1 * vsum (d scale / d wp_k = 1 / K for every k)
-  float tot[4];
-  tile_row_sums(av, red, tot, lane, w);
-  if (tid == 0) {
-    float a = 0.f;
-#pragma unroll
-    for (int r = 0; r < RB; ++r) a += red[r] + red[RB + r] + red[2 * RB + r] + red[3 * RB + r];
-    srow[6 * G + NGL + blockIdx.y] = a;
-  }
-  (void)tot;
-}
-
-// fold of the slab rows into the gradients (fixed row order): segment j of [6 G + NGL] columns -> dst,
-// and dwp[k] += (sum of the dwp partials) / K
-struct GlobDst {
-  float* d[7];
-};
-__global__ void __launch_bounds__(256) glob3_fold_kernel(const float* __restrict__ slab, int rows, int ld, GlobDst dst,
-                                                         float* __restrict__ dwp, int K, int G, int NGL) {
-  __shared__ float red[256];
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const int ncol = 6 * G + NGL;
-  if (blockIdx.x < gridDim.x - 1) {
-    if (j >= ncol) return;
-    float a = 0.f;
-    for (int r = 0; r < rows; ++r) a += slab[(size_t)r * ld + j];
-    const int seg = j / G < 6 ? j / G : 6;
-    const int off = seg < 6 ? j - seg * G : j - 6 * G;
-    if (dst.d[seg] != nullptr) dst.d[seg][off] += a;
-    return;
-  }
-  // last block: the dwp total
-  const int nct = G / CT;
-  float a = 0.f;
-  for (int i = threadIdx.x; i < rows * nct; i += 256) a += slab[(size_t)(i / nct) * ld + ncol + (i % nct)];
-  red[threadIdx.x] = a;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float s = 0.f;
-    for (int i = 0; i < 256; ++i) s += red[i];
-    red[0] = s / (float)K;
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < K; k += 256) dwp[k] += red[0];
-}
 }  // namespace
-
-PBX_EXPORT int pbx_glob3_slab_cols(int G, int NGL) { return 6 * G + NGL + G / CT; }
 
 // p: g, g_bf, vpart, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b, fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2,
 //    r2, g2, g2_bf, pregl, gb, z1, z2, part1, part2   (30 pointers; fgl / bgl / pregl / gb null when NGL == 0;
@@ -601,34 +328,5 @@ PBX_EXPORT int pbx_glob3_fwd(const void* const* p, int B, int G, int NGL, int TV
                      W(16), (bf16_t*)p[18], (const bf16x8*)p[8], F(9), W(19), W(27), (float2*)p[29], B, G);
   hipLaunchKernelGGL(glob3_fwd3_kernel, grid, dim3(256), 0, st, F(27), (const float2*)p[29], F(10), F(11), eps, W(20),
                      W(21), W(22), (bf16_t*)p[23], (const bf16x8*)p[12], F(13), W(24), W(25), B, G, NGL);
-  return pbx_launch_status();
-}
-
-// p: dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum, wp, f1T, dg, dvs, du1, du2, dugl,
-//    dg2s, dg1s, part2, part1   (25 pointers; dgb / pregl / fglT / dugl null when NGL == 0; dg2s / dg1s
-//    [B][G] fp32 and part2 / part1 [B][G / 64] float2 scratch).  slab: [ceil(B / 16)][pbx_glob3_slab_cols]
-//    per-row-tile column sums (fully written here), folded by pbx_glob3_fold.
-PBX_EXPORT int pbx_glob3_bwd(const void* const* p, int B, int G, int NGL, int K, float* slab, hipStream_t st) {
-  if ((G != 256 && G != 512) || (NGL != 0 && NGL != 128) || B < 1 || K < 1) return (int)hipErrorInvalidValue;
-  const dim3 grid((B + RB - 1) / RB, G / CT);
-  const int ld = pbx_glob3_slab_cols(G, NGL);
-  auto F = [&](int i) { return (const float*)p[i]; };
-  auto W = [&](int i) { return (float*)p[i]; };
-  hipLaunchKernelGGL(glob3_bwd1_kernel, grid, dim3(256), 0, st, F(0), F(1), F(2), (const bf16x8*)p[3], F(4), F(6),
-                     W(21), (bf16_t*)p[20], (float2*)p[23], slab, ld, B, G, NGL);
-  hipLaunchKernelGGL(glob3_bwd2_kernel, grid, dim3(256), 0, st, F(21), (const float2*)p[23], F(4), F(5), F(6), F(7),
-                     (const bf16x8*)p[8], F(9), F(11), (bf16_t*)p[19], W(22), (float2*)p[24], slab, ld, B, G);
-  hipLaunchKernelGGL(glob3_bwd3_kernel, grid, dim3(256), 0, st, F(22), (const float2*)p[24], F(9), F(10), F(11),
-                     F(12), F(13), F(14), K, (const bf16x8*)p[15], (bf16_t*)p[18], W(16), W(17), slab, ld, B, G, NGL);
-  return pbx_launch_status();
-}
-
-// d: db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl (nullable when NGL == 0), dwp
-PBX_EXPORT int pbx_glob3_fold(const float* slab, int B, int G, int NGL, int K, const void* const* d, hipStream_t st) {
-  const int rows = (B + RB - 1) / RB, ld = pbx_glob3_slab_cols(G, NGL);
-  GlobDst dst;
-  for (int i = 0; i < 7; ++i) dst.d[i] = (float*)d[i];
-  const int nb = (6 * G + NGL + 255) / 256 + 1;
-  hipLaunchKernelGGL(glob3_fold_kernel, dim3(nb), dim3(256), 0, st, slab, rows, ld, dst, (float*)d[7], K, G, NGL);
   return pbx_launch_status();
 }

@@ -1,11 +1,10 @@
-// Whole-sequence LayerNorm, local MLP, local->global attention pool and their backward passes
-// (reference semantics).
+// Whole-sequence LayerNorm and local MLP forward / backward passes (reference semantics;
+// the attention pool and the LayerNorm-2 apply are csrc/pool.hip).
 //
 // Reference: ProteinBERT/modules.py:148-164 (LayerNorm over (L, C) with an [L, C] affine, twice),
 // :153-164,214-217 (Linear C->C + GELU + residual), :21-92,219 (global attention).  In reference
 // semantics the attention softmax runs over an axis whose rows are identical, so every head
-// reduces exactly to (1/K) * sum_l GELU(h Wv_j); the pool is one GEMM
-// [rows, 128] x [128, 512] with a GELU + column-sum epilogue.  Statistics of the (L, C)
+// reduces exactly to (1/K) * sum_l GELU(h Wv_j).  Statistics of the (L, C)
 // LayerNorms span the whole sequence, so every producer writes per-tile partials ((mean, M2)
 // forward, (sum dxhat, sum dxhat*xhat) backward) and every consumer combines them.
 //
@@ -26,79 +25,12 @@ __device__ __forceinline__ void load_f8(const float* p, float* v) {
   const float4 c = *reinterpret_cast<const float4*>(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = c.x; v[5] = c.y; v[6] = c.z; v[7] = c.w;
 }
-__device__ __forceinline__ void load_f4(const float* p, float* v) {
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
-}
-
-// One 1-KiB global->LDS DMA wave instruction (lane i's 16 source bytes land at lds_base + 16 i), as
-// inline asm so hipcc does not make later ds_reads wait for it (see wgrad.hip); it retires in vmcnt
-// order with the wave's other vector-memory operations.
-__device__ __forceinline__ void glds16_ln(const void* src, unsigned char* lds_base) {
-  const unsigned dst = __builtin_amdgcn_readfirstlane(
-      (unsigned)(size_t)(__attribute__((address_space(3))) unsigned char*)lds_base);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(src), "s"(dst)
-               : "memory");
-}
 
 // stage a [rows x 128] bf16 weight matrix into a swz256 LDS image (whole workgroup)
 __device__ __forceinline__ void stage_weight(unsigned char* dst, const bf16_t* __restrict__ w, int rows) {
   stage_chunks(
       rows * 16, [&](int idx) { return *reinterpret_cast<const uint4*>(w + (size_t)idx * 8); },
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(dst + swz256(idx >> 4, idx & 15)) = v; });
-}
-
-// LN-normalised B/A fragment of one position row: 8 x (8 channels kk*16 + 8h .. +8)
-// The caller passes in-bounds pointers (rows clamped); `ok` only masks the values, so every load is
-// unconditional and all 24 of them are in flight together (a load under a divergent branch costs
-// one exposed memory round trip per branch).
-// KB: channel chunks whose loads are in flight together (8: one round trip, ~160 VGPRs of operands;
-// 4: two round trips at half the registers, for the high-occupancy pool variant)
-template <int KB = 8>
-__device__ __forceinline__ void ln_row_frags(bf16x8* f, const bf16_t* __restrict__ src, const float* __restrict__ gam,
-                                             const float* __restrict__ bet, float mean, float rstd, bool ok,
-                                             int h, bf16_t* __restrict__ out) {
-#pragma unroll
-  for (int k0 = 0; k0 < 8; k0 += KB) {
-  uint4 sq[KB];
-  float4 ga[KB][2], ba[KB][2];
-#pragma unroll
-  for (int k = 0; k < KB; ++k) {
-    const int ci = (k0 + k) * 16 + 8 * h;
-    sq[k] = *reinterpret_cast<const uint4*>(src + ci);
-#ifdef PBX_ABL_NOAFFINE   // ablation builds only: the cost of the [L, C] affine loads
-    ga[k][0] = ga[k][1] = ba[k][0] = ba[k][1] = make_float4(mean, rstd, mean, rstd);
-#else
-    ga[k][0] = *reinterpret_cast<const float4*>(gam + ci);
-    ga[k][1] = *reinterpret_cast<const float4*>(gam + ci + 4);
-    ba[k][0] = *reinterpret_cast<const float4*>(bet + ci);
-    ba[k][1] = *reinterpret_cast<const float4*>(bet + ci + 4);
-#endif
-  }
-#pragma unroll
-  for (int k = 0; k < KB; ++k) {
-    const int kk = k0 + k;
-    const int ci = kk * 16 + 8 * h;
-    float sv[8], v[8];
-    unpack8(sq[k], sv);
-    const float g[8] = {ga[k][0].x, ga[k][0].y, ga[k][0].z, ga[k][0].w,
-                        ga[k][1].x, ga[k][1].y, ga[k][1].z, ga[k][1].w};
-    const float be[8] = {ba[k][0].x, ba[k][0].y, ba[k][0].z, ba[k][0].w,
-                         ba[k][1].x, ba[k][1].y, ba[k][1].z, ba[k][1].w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ok ? (sv[e] - mean) * rstd * g[e] + be[e] : 0.f;
-    const uint4 q = packq8(v);
-#ifdef PBX_ABL_NOH2   // ablation builds only: the cost of the h2 stores
-    if (ok && out != nullptr && mean > 1e30f) *reinterpret_cast<uint4*>(out + ci) = q;
-#else
-    if (ok && out != nullptr) *reinterpret_cast<uint4*>(out + ci) = q;
-#endif
-    f[kk] = __builtin_bit_cast(bf16x8, q);
-  }
-  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -239,694 +171,6 @@ __global__ void __launch_bounds__(512) ln_linear_fwd_kernel(
     const float m = sa / (float)(vrows * CH);
     st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2] = m;
     st2[((size_t)(b0 + i) * TP + blockIdx.x) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// h2 = LN(s2) (written: block output) ; vpart[b][t][j] = sum_{pos in 64-row tile t} GELU(h2[pos] . Wv[j])
-// Work item = 64 positions of one sample, owned by one wave (waves are independent: no barrier after
-// the Wv staging).  Each Wv fragment read from LDS feeds two MFMAs (the wave's two 32-row position
-// tiles), the two accumulator chains are interleaved, and the 8 Wv fragments of column block jt+1
-// are loaded while block jt runs, so neither LDS latency nor MFMA dependency stalls the wave; the
-// packed-fp32 GELU / column sums of block jt-1 fill the MFMA shadow.
-__global__ void __launch_bounds__(512) ln_attn_fwd_kernel(
-    const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
-    const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
-    float* __restrict__ vpart, int B, int L, int NJ, float eps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;                                          // NJ rows x 256 B
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int NW = blockDim.x >> 6;
-  const int T2 = (L + BML - 1) / BML;
-  const int TW = (L + 63) / 64;
-  const int NJT = NJ / 32;
-  const long items = (long)B * TW;
-  stage_weight(ws, wv, NJ);
-  __syncthreads();
-  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos0 = tw * 64;
-    float mean, rstd;
-    wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    bf16x8 hf0[8], hf1[8];
-    {
-      const int pa = pos0 + r, pb = pos0 + 32 + r;
-      const int ca = min(pa, L - 1), cb = min(pb, L - 1);          // clamped: loads stay in bounds
-      const size_t ra = ((size_t)b * L + ca) * CH, rb = ((size_t)b * L + cb) * CH;
-      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
-      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
-    }
-    float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
-    // rows beyond L are zero fragments (ln_row_frags) and GELU(0) = 0: no masking needed
-    auto colsum = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
-      f32x2 sv = {0.f, 0.f};
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x2 xv[4] = {(f32x2){c0[4 * g], c0[4 * g + 1]}, (f32x2){c0[4 * g + 2], c0[4 * g + 3]},
-                             (f32x2){c1[4 * g], c1[4 * g + 1]}, (f32x2){c1[4 * g + 2], c1[4 * g + 3]}};
-        f32x2 gv[4];
-        gelu2_fast_n<4, false>(xv, gv);
-        sv += (gv[0] + gv[1]) + (gv[2] + gv[3]);
-      }
-      float sacc = sv.x + sv.y;
-      sacc += __shfl_xor(sacc, 32, 64);
-      if (h == 0) vrow[jt * 32 + r] = sacc;
-    };
-    bf16x8 wf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256(r, kk * 2 + h));
-    f32x16_t p0 = zero16(), p1 = zero16();
-    for (int jt = 0; jt < NJT; ++jt) {
-      f32x16_t c0 = zero16(), c1 = zero16();
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        c0 = mfma32(hf0[kk], wf[kk], c0);
-        c1 = mfma32(hf1[kk], wf[kk], c1);
-      }
-      if (jt + 1 < NJT) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256((jt + 1) * 32 + r, kk * 2 + h));
-      }
-      if (jt > 0) colsum(p0, p1, jt - 1);
-      p0 = c0;
-      p1 = c1;
-    }
-    colsum(p0, p1, NJT - 1);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// h2 = LN_(L,C)(s2) as a streaming position-major pass (the pattern of ln_linear_fwd): a workgroup
-// owns PB = 32 positions, keeps their fp32 affine in registers (thread: position j, 8 channels) and
-// walks its sample group with AP samples' rows in flight per thread.  The pool forward then reads the
-// normalised rows directly.
-constexpr int AP = 4;
-__global__ void __launch_bounds__(512) ln2_apply_kernel(const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-                                                        const float* __restrict__ g2, const float* __restrict__ be2,
-                                                        bf16_t* __restrict__ h2, int B, int L, float eps) {
-  __shared__ float tab[2 * 256];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int j = tid >> 4, ch = tid & 15;
-  const int l = blockIdx.x * PB + j;
-  const bool okl = l < L;
-  const int T2 = (L + BML - 1) / BML;
-  const int nbg = gridDim.y;
-  const int b0 = (int)((long)B * blockIdx.y / nbg), b1 = (int)((long)B * (blockIdx.y + 1) / nbg);
-  const int nb = b1 - b0;                          // <= 256 (host: nbg >= ceil(B / 256))
-  for (int i = w; i < nb; i += 8) {
-    float mean, rstd;
-    wave_ln_stats(st2 + (size_t)(b0 + i) * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-    if (lane == 0) {
-      tab[2 * i] = mean;
-      tab[2 * i + 1] = rstd;
-    }
-  }
-  float gam[8] = {0, 0, 0, 0, 0, 0, 0, 0}, bet[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (okl) {
-    load_f8(g2 + (size_t)l * CH + ch * 8, gam);
-    load_f8(be2 + (size_t)l * CH + ch * 8, bet);
-  }
-  __syncthreads();
-  if (!okl) return;
-  const size_t col = (size_t)l * CH + ch * 8;
-  for (int bb = b0; bb < b1; bb += AP) {
-    uint4 q[AP];
-#pragma unroll
-    for (int k = 0; k < AP; ++k) q[k] = ldq(s2 + (size_t)min(bb + k, b1 - 1) * L * CH + col, true);
-#pragma unroll
-    for (int k = 0; k < AP; ++k) {
-      if (bb + k >= b1) break;
-      const float mean = tab[2 * (bb + k - b0)], rstd = tab[2 * (bb + k - b0) + 1];
-      float sv[8], o[8];
-      unpack8(q[k], sv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) o[e] = (sv[e] - mean) * rstd * gam[e] + bet[e];
-      *reinterpret_cast<uint4*>(h2 + (size_t)(bb + k) * L * CH + col) = packq8(o);
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Attention pool with the GELU derivative stored by the forward (v2).
-//
-// The backward of the pool needs GELU'(h2 Wv) at every (position, value column): recomputing it costs
-// the [32 x 512] projection per tile (128 MFMAs) plus GELU' (2 transcendentals per element), all to
-// multiply it by dv (the round-1 form; 1.6 % slower on the step).  Here the forward evaluates GELU and GELU' from ONE shared
-// erf/exp core, column-sums GELU as before and writes GELU' as bf16 in the exact per-lane order of
-// the backward's MFMA B operand (`gfrag`: [B][2 ceil(L/64)][NJ/32][2][64 lanes][8], one coalesced
-// 1-KB store / load per wave-instruction); the backward is then 128 MFMAs per 32-position tile fed
-// by a streamed, prefetched load, with no recompute and no transcendental.
-//
-// Fragment order (backward MFMA k-step (jt, s), lane (r = position, h), element jj):
-//   j = jt*32 + 16 s + 8 (jj >> 2) + 4 h + (jj & 3)        (= the A-operand rows of the Wv^T reads)
-// The forward holds D[pos][j] (lane = column j, 16 positions in registers, so the column sums stay
-// in-lane); each 32x32 block of GELU' goes through a per-wave LDS tile Gt[j][pos] (ds_write_b64 of
-// 4 contiguous positions) and comes back transposed (ds_read_b64_tr_b16) as two fragments.
-constexpr int GT_STRIDE = 72;       // bytes per Gt row (32 positions + 8 B pad: spreads the banks)
-constexpr int GT_BYTES = 32 * GT_STRIDE;
-
-#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/build_flags.sh st -DPBX_STAMPS): per-phase clocks
-__device__ long long* pbx_stamp_buf;
-#define PBX_STAMP(k)                                                                       \
-  do {                                                                                     \
-    if (blockIdx.x < 4 && lane == 0 && (k) < 64)                                           \
-      pbx_stamp_buf[(blockIdx.x * 8 + w) * 64 + (k)] = (long long)clock64();               \
-  } while (0)
-#else
-#define PBX_STAMP(k) do {} while (0)
-#endif
-
-// Work item: 64 positions (two 32-position MFMA tiles; each Wv fragment read from LDS feeds two MFMAs;
-// ~248 VGPRs, two waves per SIMD).  NI: GELU pairs interleaved per core call.
-// PRENORM: s2 already holds the normalised rows (h2 from ln2_apply_kernel); no statistics, no affine
-// loads and no h2 stores (the [L, C] fp32 affine re-read per 64-position item cost ~35 us of ~175)
-template <int NWAVE, int NI, bool PRENORM, bool STOREG = true>   // STOREG: GELU' fragments for attn_bwd2
-__global__ void __launch_bounds__(64 * NWAVE) ln_attn_fwd2_kernel(
-    const bf16_t* __restrict__ s2, const float* __restrict__ st2, const float* __restrict__ g2,
-    const float* __restrict__ be2, const bf16_t* __restrict__ wv, bf16_t* __restrict__ h2,
-    float* __restrict__ vpart, bf16x8* __restrict__ gfrag, int B, int L, int NJ, float eps) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;                                          // NJ rows x 256 B
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int q = tr_q(lane), tc = tr_c(lane);
-  unsigned char* gt = smem + NJ * 256 + w * GT_BYTES;               // this wave's transpose tile
-  const int NW = blockDim.x >> 6;
-  const int T2 = (L + BML - 1) / BML;
-  const int TW64 = (L + 63) / 64;
-  const int TW = TW64;                              // work items per sample
-  constexpr int NP = 2;                             // 32-position MFMA tiles per work item
-  const int NJT = NJ / 32;
-  const long items = (long)B * TW;
-  PBX_STAMP(0);
-  stage_weight(ws, wv, NJ);
-  __syncthreads();
-#ifdef PBX_DESYNC   // experiment builds: the second wave of each SIMD starts PBX_DESYNC x 8k cycles late
-  if (w >= 4)
-    for (int i = 0; i < PBX_DESYNC; ++i) __builtin_amdgcn_s_sleep(127);
-#endif
-  PBX_STAMP(1);
-  int sb = 2;
-  for (long item = (long)blockIdx.x * NW + w; item < items; item += (long)gridDim.x * NW, sb += 20) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos0 = tw * 32 * NP;
-    PBX_STAMP(sb);
-    bf16x8 hf0[8], hf1[8];
-    if constexpr (PRENORM) {
-      const int pa = pos0 + r, pb = pos0 + 32 + r;
-      const bf16_t* ra = s2 + ((size_t)b * L + min(pa, L - 1)) * CH + 8 * h;
-      const bf16_t* rb = s2 + ((size_t)b * L + min(pb, L - 1)) * CH + 8 * h;
-      uint4 qa[8], qb[8];
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        qa[kk] = *reinterpret_cast<const uint4*>(ra + kk * 16);
-        qb[kk] = *reinterpret_cast<const uint4*>(rb + kk * 16);
-      }
-      const uint4 z = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        hf0[kk] = __builtin_bit_cast(bf16x8, pa < L ? qa[kk] : z);
-        hf1[kk] = __builtin_bit_cast(bf16x8, pb < L ? qb[kk] : z);
-      }
-      PBX_STAMP(sb + 1);
-    } else {
-      float mean, rstd;
-      wave_ln_stats(st2 + (size_t)b * T2 * 2, T2, BML, L, CH, eps, mean, rstd);
-      PBX_STAMP(sb + 1);
-      const int pa = pos0 + r;
-      const int ca = min(pa, L - 1);
-      const size_t ra = ((size_t)b * L + ca) * CH;
-      ln_row_frags(hf0, s2 + ra, g2 + (size_t)ca * CH, be2 + (size_t)ca * CH, mean, rstd, pa < L, h, h2 + ra);
-      const int pb = pos0 + 32 + r;
-      const int cb = min(pb, L - 1);
-      const size_t rb = ((size_t)b * L + cb) * CH;
-      ln_row_frags(hf1, s2 + rb, g2 + (size_t)cb * CH, be2 + (size_t)cb * CH, mean, rstd, pb < L, h, h2 + rb);
-    }
-    PBX_STAMP(sb + 2);
-    float* vrow = vpart + ((size_t)b * TW + tw) * NJ;
-    // fragment base of this item's 32-position tiles: [b][2 ceil(L/64)][jt][s][lane]
-    bf16x8* gdst = gfrag + ((size_t)b * 2 * TW64 + NP * tw) * NJT * 2 * 64 + lane;
-    auto epi = [&](const f32x16_t& c0, const f32x16_t& c1, int jt) {
-      f32x2 sv = {0.f, 0.f};
-      if constexpr (!STOREG) {
-        // GELU only (the backward recomputes GELU', attn_bwd3)
-        constexpr int NPAIR = 8 * NP;
-#pragma unroll
-        for (int c8 = 0; c8 < NPAIR; c8 += NI) {
-          f32x2 xv[NI], gv[NI];
-#pragma unroll
-          for (int k = 0; k < NI; ++k) {
-            const int pi = c8 + k;
-            const f32x16_t& c = (pi >> 3) ? c1 : c0;
-            xv[k] = (f32x2){c[2 * (pi & 7)], c[2 * (pi & 7) + 1]};
-          }
-          gelu2_fast_n<NI, false>(xv, gv);
-#pragma unroll
-          for (int k = 0; k < NI; ++k) sv += gv[k];
-        }
-        float sacc = sv.x + sv.y;
-        sacc += __shfl_xor(sacc, 32, 64);
-        if (h == 0) vrow[jt * 32 + r] = sacc;
-        return;
-      }
-      // GELU / GELU' of the item's 32x32 tiles: NI pairs per interleaved core call
-      constexpr int NPAIR = 8 * NP;
-      f32x2 gdall[NPAIR];
-#pragma unroll
-      for (int c8 = 0; c8 < NPAIR; c8 += NI) {
-        f32x2 xv[NI], gv[NI], gd[NI];
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-          const int pi = c8 + k;                  // pair index 0..15: tile pi >> 3, values 2 (pi & 7) ..
-          const f32x16_t& c = (pi >> 3) ? c1 : c0;
-          xv[k] = (f32x2){c[2 * (pi & 7)], c[2 * (pi & 7) + 1]};
-        }
-        gelu2_both_n<NI>(xv, gv, gd);
-#pragma unroll
-        for (int k = 0; k < NI; ++k) {
-          sv += gv[k];
-          gdall[c8 + k] = gd[k];
-        }
-      }
-#pragma unroll
-      for (int pt = 0; pt < NP; ++pt) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          // positions 8g + 4h .. +3 of column j = r -> Gt[r][8g + 4h]
-          const f32x2 a = gdall[pt * 8 + 2 * g], bq = gdall[pt * 8 + 2 * g + 1];
-          uint2 pk;
-          pk.x = (unsigned)f2bf(a.x) | ((unsigned)f2bf(a.y) << 16);
-          pk.y = (unsigned)f2bf(bq.x) | ((unsigned)f2bf(bq.y) << 16);
-          *reinterpret_cast<uint2*>(gt + r * GT_STRIDE + (8 * g + 4 * h) * 2) = pk;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          const int rlo = 16 * s + 4 * h + q;
-          const bf16x8 f = cat_tr(lds_tr(gt, rlo * GT_STRIDE + tc * 2), lds_tr(gt, (rlo + 8) * GT_STRIDE + tc * 2));
-#ifdef PBX_ABL_NOGSTORE   // ablation builds only: the cost of the GELU' fragment stores (B > 0 always)
-          if (B < 0)
-#endif
-          gdst[((size_t)pt * NJT * 2 + jt * 2 + s) * 64] = f;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-      float sacc = sv.x + sv.y;
-      sacc += __shfl_xor(sacc, 32, 64);
-      if (h == 0) vrow[jt * 32 + r] = sacc;
-    };
-    bf16x8 wf[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256(r, kk * 2 + h));
-    f32x16_t p0 = zero16(), p1 = zero16();
-    for (int jt = 0; jt < NJT; ++jt) {
-      f32x16_t c0 = zero16(), c1 = zero16();
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        c0 = mfma32(hf0[kk], wf[kk], c0);
-        c1 = mfma32(hf1[kk], wf[kk], c1);
-      }
-      if (jt + 1 < NJT) {
-#pragma unroll
-        for (int kk = 0; kk < 8; ++kk) wf[kk] = lds_frag(ws, swz256((jt + 1) * 32 + r, kk * 2 + h));
-      }
-      if (jt > 0) epi(p0, p1, jt - 1);
-      p0 = c0;
-      p1 = c1;
-      PBX_STAMP(sb + 3 + jt);
-    }
-    epi(p0, p1, NJT - 1);
-    PBX_STAMP(sb + 19);
-  }
-}
-
-// attention pool backward from the stored GELU' fragments + LayerNorm-2 backward partials:
-//   dh2[pos][ci] = dh2_in + sum_j Wv[j][ci] dv[b][j] GELU'[pos][j]
-// Work item = one 32-position tile, one wave per SIMD (4 waves, <= 512 registers).  Every load of an
-// item is issued at its start, in the order the wave consumes them (vmcnt retires in issue order):
-// the dv row, all 2 NJT GELU' fragments of the tile (one coalesced 1-KiB load each, ~32 KiB in
-// flight per wave), then the epilogue operands; no load is outstanding across the item loop's back
-// edge, so the compiler's waits stay exact.
-// FIXTW: the grid stride is a multiple of the tiles per sample, so every item of a wave has the same
-// 32 positions and their [L, C] affine gamma is loaded once per wave, not per item (~16 of ~72 KB per
-// item; the compiler's vmcnt tracking wants the item loads branch-free, hence a template flag)
-template <int NJT, bool FIXTW>
-__global__ void __launch_bounds__(256) attn_bwd2_kernel(
-    const bf16x8* __restrict__ gfrag, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
-    const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, float eps) {
-  constexpr int NJ = NJT * 32;
-  constexpr int NF = 2 * NJT;                       // fragments (k-steps) per 32-position tile
-  constexpr int NDV = NJ / 256;                     // 1-KiB DMA instructions per dv row
-  constexpr int NW = 4;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int q = tr_q(lane), tc = tr_c(lane);
-  const int T2 = (L + BML - 1) / BML;
-  const int TW = (L + 31) / 32;
-  const int TWG = 2 * ((L + 63) / 64);              // 32-position tiles per sample in gfrag
-  const int TV = (L + BMV - 1) / BMV;
-  const long items = (long)B * TW;
-  const long stride = (long)gridDim.x * NW;
-  stage_weight(ws, wv, NJ);
-  // per-wave dv rows, double-buffered: item k reads slot k & 1; the DMA of item k+1's row into the
-  // other slot is issued with item k's epilogue operands (whose waits retire it)
-  unsigned char* dvslot = ws + NJ * 256 + w * 2 * NJ * 4;
-  int woff[4], woff8[4];   // Wv^T fragment offsets at step 0; step i adds 16 i rows = 4096 i bytes
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    woff[ct] = swz256e(4 * h + q, ct * 32 + tc);
-    woff8[ct] = swz256e(4 * h + q + 8, ct * 32 + tc);
-  }
-  auto dv_src = [&](long it) {
-    const int b = (int)(it / TW), tw = (int)(it - (it / TW) * TW);
-    return dvpart + ((size_t)b * TV + (tw * 32) / BMV) * NJ;
-  };
-  long item = (long)blockIdx.x * NW + w;
-  float4 gq4[4][4];
-  if constexpr (FIXTW) {
-    const int pc = min((int)(item % TW) * 32 + r, L - 1);
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ct * 32 + 8 * i + 4 * h);
-  }
-  if (item < items) {
-    const float* dvg = dv_src(item);
-#pragma unroll
-    for (int k = 0; k < NDV; ++k) glds16_ln(dvg + lane * 4 + 256 * k, dvslot + 1024 * k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  int slot = 0;
-  for (; item < items; item += stride, slot ^= 1) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos = tw * 32 + r;
-    const bool okb = pos < L;
-    const bf16x8* gsrc = gfrag + ((size_t)b * TWG + tw) * NF * 64 + lane;
-    const float* dv = reinterpret_cast<const float*>(dvslot + slot * NJ * 4);
-    const bool has_next = item + stride < items;
-    const float* dvn = dv_src(has_next ? item + stride : item);
-    bf16x8 ring[NF];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      ring[i] = gsrc[i * 64];
-      __builtin_amdgcn_sched_barrier(0);      // keep the issue order = the consumption order
-    }
-    const int pc = min(pos, L - 1);
-    const size_t roff = ((size_t)b * L + pc) * CH;
-    // branch-free loads (a load under a branch makes the compiler's vmcnt tracking fall back to
-    // vmcnt(0) at the merge): a missing dh2_in reads s2 and is masked
-    const bf16_t* dsrc = dh2_in != nullptr ? dh2_in : s2;
-    const float dmask = dh2_in != nullptr ? 1.f : 0.f;
-    const float* stb = st2 + (size_t)b * T2 * 2;
-    uint2 dq[4][4], sq[4][4];
-    float2 pm0, pm1;
-    // the epilogue operands are issued EPI steps before the end of the tile: vmcnt counts at most 63
-    // outstanding operations per wave (2 + 2 NJT ring + 50 would overflow it if issued up front)
-    auto epi_loads = [&]() {
-      if (has_next) {
-#pragma unroll
-        for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
-      }
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ci0 = ct * 32 + 8 * i + 4 * h;
-          dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
-          sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
-          if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
-        }
-      pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
-      pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
-    };
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    f32x16_t y[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    constexpr int EPI = NF < 8 ? NF : 8;
-#pragma unroll
-    for (int i = 0; i < NF; ++i) {
-      if (i == NF - EPI) {
-        __builtin_amdgcn_sched_barrier(0);
-        epi_loads();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      float dvv[8], gv[8];
-      load_f4(dv + 16 * i + 4 * h, dvv);            // j = jt*32 + 16 s (= 16 i) + 4 h + ...
-      load_f4(dv + 16 * i + 8 + 4 * h, dvv + 4);
-      unpack8(__builtin_bit_cast(uint4, ring[i]), gv);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) gv[e] *= dvv[e];
-      const bf16x8 fb = pack8(gv);
-      const unsigned char* wsi = ws + 4096 * i;
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct) {
-        const bf16x8 fw = cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct]));
-        y[ct] = mfma32(fw, fb, y[ct]);
-      }
-    }
-    // LN2 statistics of sample b (Chan merge of the tile partials; T2 <= 128 from the early loads)
-    float mean, rstd;
-    if (T2 <= 128) {
-      float n = 0.f, m = 0.f, M2 = 0.f;
-      if (lane < T2) chan_merge(n, m, M2, (float)(min(BML, L - lane * BML) * CH), pm0.x, pm0.y);
-      if (lane + 64 < T2) chan_merge(n, m, M2, (float)(min(BML, L - (lane + 64) * BML) * CH), pm1.x, pm1.y);
-      wave_chan(n, m, M2);
-      mean = m;
-      rstd = rsqrtf(M2 / n + eps);
-    } else {
-      wave_ln_stats(stb, T2, BML, L, CH, eps, mean, rstd);
-    }
-    float sa = 0.f, sc = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ci0 = ct * 32 + 8 * g + 4 * h;
-        float din[4], sv[4], o[4];
-        unpack4(dq[ct][g], din);
-        unpack4(sq[ct][g], sv);
-        const float gg[4] = {gq4[ct][g].x, gq4[ct][g].y, gq4[ct][g].z, gq4[ct][g].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = bfround(fmaf(din[e], dmask, y[ct][4 * g + e]));
-          const float xh = (sv[e] - mean) * rstd;
-          const float dxh = o[e] * gg[e];
-          sa += okb ? dxh : 0.f;
-          sc += okb ? dxh * xh : 0.f;
-        }
-        if (okb) *reinterpret_cast<uint2*>(dh2 + roff + ci0) = packq4(o);
-      }
-    }
-    sa = wave_reduce_sum(sa);
-    sc = wave_reduce_sum(sc);
-    if (lane == 0) {
-      sums2[((size_t)b * TW + tw) * 2] = sa;
-      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
-    }
-  }
-}
-
-// attention pool backward that RECOMPUTES GELU'(h2 Wv) instead of streaming the stored fragments
-// (268 MB per block at B = L = 512, the dominant traffic of attn_bwd2):
-//   zT[j][pos]  = sum_c Wv[j][c] h2[pos][c]      MFMA, A = Wv rows (LDS), B = the tile's h2 rows (registers)
-//   uT[j][pos]  = dv[b][j] GELU'(zT[j][pos])     VALU on the 16 accumulator values of each lane
-//   dh^T[c][pos] += sum_j Wv[j][c] uT[j][pos]    MFMA, A = Wv^T read transposed from LDS
-// The D layout of zT (lane = position, rows 4h + {0..3, 8..11} + 16 s of a 32-row chunk) is the B
-// operand of the second product with its K order permuted to {4h + 0..3, 8 + 4h + 0..3} per 16-step,
-// which is exactly the order the transposed Wv reads of attn_bwd2 deliver: no data movement between
-// the two MFMAs.  The GELU' of chunk jt runs while the MFMAs of chunk jt + 1's zT are in flight.
-// Epilogue (dh2 = bf16(dh2_in + dh), LN2 partials) as attn_bwd2.  One wave per SIMD.
-template <int NJT, bool FIXTW, int NW>
-__global__ void __launch_bounds__(64 * NW) attn_bwd3_kernel(
-    const bf16_t* __restrict__ h2, const bf16_t* __restrict__ s2, const float* __restrict__ st2,
-    const float* __restrict__ g2, const bf16_t* __restrict__ dh2_in, const float* __restrict__ dvpart, int BMV,
-    const bf16_t* __restrict__ wv, bf16_t* __restrict__ dh2, float* __restrict__ sums2, int B, int L, float eps) {
-  constexpr int NJ = NJT * 32;
-  constexpr int NDV = NJ / 256;                     // 1-KiB DMA instructions per dv row
-  // NW = 4: one wave per SIMD, every load of an item issued up front; NW = 8: two waves per SIMD sharing
-  // one Wv image (LDS 128 + 32 KB), the epilogue operands loaded after the MFMA / GELU' body (<= 256
-  // registers a wave) -- the other wave's VALU / MFMA work covers that latency
-  constexpr bool EARLY = NW == 4;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* ws = smem;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int q = tr_q(lane), tc = tr_c(lane);
-  const int T2 = (L + BML - 1) / BML;
-  const int TW = (L + 31) / 32;
-  const int TV = (L + BMV - 1) / BMV;
-  const long items = (long)B * TW;
-  const long stride = (long)gridDim.x * NW;
-  stage_weight(ws, wv, NJ);
-  unsigned char* dvslot = ws + NJ * 256 + w * 2 * NJ * 4;
-  int woff[4], woff8[4];   // Wv^T fragment offsets at 16-step 0; step i adds 16 i rows = 4096 i bytes
-#pragma unroll
-  for (int ct = 0; ct < 4; ++ct) {
-    woff[ct] = swz256e(4 * h + q, ct * 32 + tc);
-    woff8[ct] = swz256e(4 * h + q + 8, ct * 32 + tc);
-  }
-  auto dv_src = [&](long it) {
-    const int b = (int)(it / TW), tw = (int)(it - (it / TW) * TW);
-    return dvpart + ((size_t)b * TV + (tw * 32) / BMV) * NJ;
-  };
-  long item = (long)blockIdx.x * NW + w;
-  float4 gq4[4][4];
-  if constexpr (FIXTW) {
-    const int pc = min((int)(item % TW) * 32 + r, L - 1);
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ct * 32 + 8 * i + 4 * h);
-  }
-  if (item < items) {
-    const float* dvg = dv_src(item);
-#pragma unroll
-    for (int k = 0; k < NDV; ++k) glds16_ln(dvg + lane * 4 + 256 * k, dvslot + 1024 * k);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  int slot = 0;
-  for (; item < items; item += stride, slot ^= 1) {
-    const int b = (int)(item / TW), tw = (int)(item - (item / TW) * TW);
-    const int pos = tw * 32 + r;
-    const bool okb = pos < L;
-    const float* dv = reinterpret_cast<const float*>(dvslot + slot * NJ * 4);
-    const bool has_next = item + stride < items;
-    const float* dvn = dv_src(has_next ? item + stride : item);
-    const int pc = min(pos, L - 1);
-    const size_t roff = ((size_t)b * L + pc) * CH;
-    // the tile's h2 rows as B fragments (lane: position r, channels 16 kk + 8 h ..), issued first
-    uint4 hq[8];
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) hq[kk] = *reinterpret_cast<const uint4*>(h2 + roff + kk * 16 + 8 * h);
-    __builtin_amdgcn_sched_barrier(0);
-    const bf16_t* dsrc = dh2_in != nullptr ? dh2_in : s2;
-    const float dmask = dh2_in != nullptr ? 1.f : 0.f;
-    const float* stb = st2 + (size_t)b * T2 * 2;
-    uint2 dq[4][4], sq[4][4];
-    float2 pm0, pm1;
-    // epilogue operands and the next item's dv row
-    auto epi_loads = [&]() {
-      if (has_next) {
-#pragma unroll
-        for (int k = 0; k < NDV; ++k) glds16_ln(dvn + lane * 4 + 256 * k, dvslot + (slot ^ 1) * NJ * 4 + 1024 * k);
-      }
-#pragma unroll
-      for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int ci0 = ct * 32 + 8 * i + 4 * h;
-          dq[ct][i] = *reinterpret_cast<const uint2*>(dsrc + roff + ci0);
-          sq[ct][i] = *reinterpret_cast<const uint2*>(s2 + roff + ci0);
-          if constexpr (!FIXTW) gq4[ct][i] = *reinterpret_cast<const float4*>(g2 + (size_t)pc * CH + ci0);
-        }
-      pm0 = *reinterpret_cast<const float2*>(stb + 2 * min(lane, T2 - 1));
-      pm1 = *reinterpret_cast<const float2*>(stb + 2 * min(lane + 64, T2 - 1));
-    };
-    if constexpr (EARLY) epi_loads();   // in flight during the whole MFMA / GELU' body
-    bf16x8 hf[8];
-    const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) hf[kk] = __builtin_bit_cast(bf16x8, okb ? hq[kk] : zq);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    f32x16_t y[4];
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) y[ct] = zero16();
-    auto zchunk = [&](int jt) {
-      f32x16_t z = zero16();
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) z = mfma32(lds_frag(ws, swz256(jt * 32 + r, kk * 2 + h)), hf[kk], z);
-      return z;
-    };
-    f32x16_t zc = zchunk(0);
-#pragma unroll EARLY ? 2 : 1
-    for (int jt = 0; jt < NJT; ++jt) {
-      f32x16_t zn = zc;
-      if (jt + 1 < NJT) zn = zchunk(jt + 1);          // in flight during this chunk's GELU'
-      f32x2 xv[8], gd[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) xv[i] = (f32x2){zc[2 * i], zc[2 * i + 1]};
-      gelu2_fast_n<8, true>(xv, gd);
-      // reg 4g + e <-> j = 32 jt + 8 g + 4 h + e
-      float u[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const float4 d4 = *reinterpret_cast<const float4*>(dv + jt * 32 + 8 * g + 4 * h);
-        u[4 * g] = gd[2 * g].x * d4.x;
-        u[4 * g + 1] = gd[2 * g].y * d4.y;
-        u[4 * g + 2] = gd[2 * g + 1].x * d4.z;
-        u[4 * g + 3] = gd[2 * g + 1].y * d4.w;
-      }
-      const bf16x8 b0 = pack8(u), b1 = pack8(u + 8);
-#pragma unroll
-      for (int sidx = 0; sidx < 2; ++sidx) {
-        const unsigned char* wsi = ws + 4096 * (2 * jt + sidx);
-#pragma unroll
-        for (int ct = 0; ct < 4; ++ct) {
-          const bf16x8 fw = cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct]));
-          y[ct] = mfma32(fw, sidx ? b1 : b0, y[ct]);
-        }
-      }
-      zc = zn;
-    }
-    if constexpr (!EARLY) epi_loads();
-    // LN2 statistics of sample b (Chan merge of the tile partials; T2 <= 128 from the early loads)
-    float mean, rstd;
-    if (T2 <= 128) {
-      float n = 0.f, m = 0.f, M2 = 0.f;
-      if (lane < T2) chan_merge(n, m, M2, (float)(min(BML, L - lane * BML) * CH), pm0.x, pm0.y);
-      if (lane + 64 < T2) chan_merge(n, m, M2, (float)(min(BML, L - (lane + 64) * BML) * CH), pm1.x, pm1.y);
-      wave_chan(n, m, M2);
-      mean = m;
-      rstd = rsqrtf(M2 / n + eps);
-    } else {
-      wave_ln_stats(stb, T2, BML, L, CH, eps, mean, rstd);
-    }
-    float sa = 0.f, sc = 0.f;
-#pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int ci0 = ct * 32 + 8 * g + 4 * h;
-        float din[4], sv[4], o[4];
-        unpack4(dq[ct][g], din);
-        unpack4(sq[ct][g], sv);
-        const float gg[4] = {gq4[ct][g].x, gq4[ct][g].y, gq4[ct][g].z, gq4[ct][g].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = bfround(fmaf(din[e], dmask, y[ct][4 * g + e]));
-          const float xh = (sv[e] - mean) * rstd;
-          const float dxh = o[e] * gg[e];
-          sa += okb ? dxh : 0.f;
-          sc += okb ? dxh * xh : 0.f;
-        }
-        if (okb) *reinterpret_cast<uint2*>(dh2 + roff + ci0) = packq4(o);
-      }
-    }
-    sa = wave_reduce_sum(sa);
-    sc = wave_reduce_sum(sc);
-    if (lane == 0) {
-      sums2[((size_t)b * TW + tw) * 2] = sa;
-      sums2[((size_t)b * TW + tw) * 2 + 1] = sc;
-    }
-    // the next item's dv row (DMA issued above) must be in LDS before its first read
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
   }
 }
 
@@ -1385,21 +629,7 @@ extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
 static bool ln_attrs_set = false;
 static void set_ln_attrs() {
   if (ln_attrs_set) return;
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln_linear_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<16, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd2_kernel<8, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, true, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<16, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)attn_bwd3_kernel<8, false, 8>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-  (void)hipFuncSetAttribute((const void*)ln_attn_fwd2_kernel<8, 4, true, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln2_linear_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   (void)hipFuncSetAttribute((const void*)ln1_finalize_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
   ln_attrs_set = true;
@@ -1422,106 +652,6 @@ PBX_EXPORT int pbx_ln_linear_fwd(const void* s1, const float* st1, int T1, int B
   set_ln_attrs();
   hipLaunchKernelGGL(ln_linear_fwd_kernel, grid, dim3(512), lds, st, (const bf16_t*)s1, st1, T1, BM1, g1, be1,
                      (const bf16_t*)wl, bl, (bf16_t*)pre_l, (bf16_t*)s2, st2, B, L, eps);
-  return pbx_launch_status();
-}
-
-// nw: waves per workgroup; vpart is [B][ceil(L / 64)][NJ] (one row per 64-position wave tile)
-PBX_EXPORT int pbx_ln_attn_fwd(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
-                               void* h2, float* vpart, int B, int L, int NJ, int nw, float eps, hipStream_t st) {
-  set_ln_attrs();
-  if (NJ % 64 != 0 || NJ * 256 > 163840 || nw < 1 || nw > 8) return (int)hipErrorInvalidValue;
-  const long items = (long)B * ((L + 63) / 64);
-  long wgl = (items + nw - 1) / nw;
-  if (wgl > num_cus()) wgl = num_cus();
-  hipLaunchKernelGGL(ln_attn_fwd_kernel, dim3((int)wgl), dim3(64 * nw), NJ * 256, st, (const bf16_t*)s2, st2, g2, be2,
-                     (const bf16_t*)wv, (bf16_t*)h2, vpart, B, L, NJ, eps);
-  return pbx_launch_status();
-}
-
-// dvpart rows follow the forward tiling (bmv positions, a multiple of 32); sums2 is [B][ceil(L / 32)][2]
-// v2 pool: also writes gfrag (bf16 GELU' fragments, B * 2 ceil(L/64) * NJ * 32 elements).  8 waves per
-// workgroup (two per SIMD), 4 GELU pairs per interleaved core call; measured against 4 waves x 8 / 16
-// pairs and 12 waves of 32-position items (profiles/r2_v8_pool_32pos_ab.txt): equal or slower.
-#ifdef PBX_STAMPS
-PBX_EXPORT int pbx_set_stamps(long long* buf) {
-  return (int)hipMemcpyToSymbol(HIP_SYMBOL(pbx_stamp_buf), &buf, sizeof(buf));
-}
-#endif
-
-PBX_EXPORT int pbx_ln_attn_fwd2(const void* s2, const float* st2, const float* g2, const float* be2, const void* wv,
-                                void* h2, float* vpart, void* gfrag, int B, int L, int NJ, float eps, int prenorm,
-                                hipStream_t st) {
-  set_ln_attrs();
-  constexpr int nw = 8;
-  if (NJ % 64 != 0 || NJ * 256 + nw * GT_BYTES > 163840) return (int)hipErrorInvalidValue;
-  if (!prenorm && gfrag == nullptr) return (int)hipErrorInvalidValue;   // the GELU-only form reads h2 rows
-  const long items2 = (long)B * ((L + 63) / 64);
-  long wg2 = (items2 + nw - 1) / nw;
-  if (wg2 > num_cus()) wg2 = num_cus();
-  if (prenorm) {
-    // h2 = LN(s2) first (streaming pass), then the pool on the normalised rows
-    const int tp = (L + PB - 1) / PB;
-    int nbg = (2 * num_cus() + tp - 1) / tp;
-    nbg = max(nbg, (B + 255) / 256);
-    nbg = min(nbg, B);
-    hipLaunchKernelGGL(ln2_apply_kernel, dim3(tp, nbg), dim3(512), 0, st, (const bf16_t*)s2, st2, g2, be2,
-                       (bf16_t*)h2, B, L, eps);
-    if (gfrag != nullptr)
-      hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
-                         st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
-                         B, L, NJ, eps);
-    else   // the backward recomputes GELU' (attn_bwd3): GELU column sums only
-      hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, true, false>), dim3((int)wg2), dim3(64 * nw),
-                         NJ * 256 + nw * GT_BYTES, st, (const bf16_t*)h2, st2, g2, be2, (const bf16_t*)wv,
-                         (bf16_t*)h2, vpart, (bf16x8*)nullptr, B, L, NJ, eps);
-  } else {
-    hipLaunchKernelGGL((ln_attn_fwd2_kernel<nw, 4, false>), dim3((int)wg2), dim3(64 * nw), NJ * 256 + nw * GT_BYTES,
-                       st, (const bf16_t*)s2, st2, g2, be2, (const bf16_t*)wv, (bf16_t*)h2, vpart, (bf16x8*)gfrag,
-                       B, L, NJ, eps);
-  }
-  return pbx_launch_status();
-}
-
-// v2 pool backward (NJ = 256 or 512): reads gfrag instead of recomputing h2 Wv
-PBX_EXPORT int pbx_attn_bwd2(const void* gfrag, const void* s2, const float* st2, const float* g2,
-                             const void* dh2_in, const float* dvpart, int bmv, const void* wv, void* dh2,
-                             float* sums2, int B, int L, int NJ, float eps, hipStream_t st) {
-  set_ln_attrs();
-  const int nw = 4;
-  if ((NJ != 256 && NJ != 512) || bmv % 32 != 0) return (int)hipErrorInvalidValue;
-  const long items = (long)B * ((L + 31) / 32);
-  long wgl = (items + nw - 1) / nw;
-  if (wgl > num_cus()) wgl = num_cus();
-  const int lds = NJ * 256 + nw * 2 * NJ * 4;
-  const bool fix = ((wgl * nw) % ((L + 31) / 32)) == 0;
-  const auto kern = NJ == 512 ? (fix ? attn_bwd2_kernel<16, true> : attn_bwd2_kernel<16, false>)
-                              : (fix ? attn_bwd2_kernel<8, true> : attn_bwd2_kernel<8, false>);
-  hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st,
-                     (const bf16x8*)gfrag, (const bf16_t*)s2, st2, g2, (const bf16_t*)dh2_in, dvpart, bmv,
-                     (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
-  return pbx_launch_status();
-}
-
-// recomputing pool backward (NJ = 256 or 512): h2 = the block output rows the forward pool read
-PBX_EXPORT int pbx_attn_bwd3(const void* h2, const void* s2, const float* st2, const float* g2, const void* dh2_in,
-                             const float* dvpart, int bmv, const void* wv, void* dh2, float* sums2, int B, int L,
-                             int NJ, float eps, int wide, hipStream_t st) {
-  set_ln_attrs();
-  const int nw = wide ? 8 : 4;
-  if ((NJ != 256 && NJ != 512) || bmv % 32 != 0) return (int)hipErrorInvalidValue;
-  const long items = (long)B * ((L + 31) / 32);
-  long wgl = (items + nw - 1) / nw;
-  if (wgl > num_cus()) wgl = num_cus();
-  const int lds = NJ * 256 + nw * 2 * NJ * 4;
-  const bool fix = ((wgl * nw) % ((L + 31) / 32)) == 0;
-  decltype(&attn_bwd3_kernel<16, true, 4>) kern;
-  if (wide)   // two waves per SIMD: the gamma rows are loaded per item (no FIXTW registers)
-    kern = NJ == 512 ? attn_bwd3_kernel<16, false, 8> : attn_bwd3_kernel<8, false, 8>;
-  else
-    kern = NJ == 512 ? (fix ? attn_bwd3_kernel<16, true, 4> : attn_bwd3_kernel<16, false, 4>)
-                     : (fix ? attn_bwd3_kernel<8, true, 4> : attn_bwd3_kernel<8, false, 4>);
-  hipLaunchKernelGGL(kern, dim3((int)wgl), dim3(64 * nw), lds, st, (const bf16_t*)h2, (const bf16_t*)s2, st2, g2,
-                     (const bf16_t*)dh2_in, dvpart, bmv, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L, eps);
   return pbx_launch_status();
 }
 
@@ -1559,7 +689,7 @@ PBX_EXPORT int pbx_ln2_linear_bwd(const void* dh2, const void* s2, const float* 
                                   int det, int fold, int consts_ready, hipStream_t st) {
   set_ln_attrs();
   const int T2 = (L + PB - 1) / PB;
-  // consts_ready: the pool backward (pbx_attn_bwd4c) already wrote consts and zeroed dgb_zero
+  // consts_ready: the caller already wrote consts and zeroed dgb_zero
   if (!consts_ready)
     hipLaunchKernelGGL(ln2_consts_kernel, dim3((B + 3) / 4), dim3(256), 0, st, st2, T2, PB, sums2, TS2, st1, T1, BM1,
                        consts, dgb_zero, B, L, eps);

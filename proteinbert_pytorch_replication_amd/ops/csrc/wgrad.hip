@@ -476,7 +476,7 @@ extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
 
 // Rows of the per-workgroup slab pbx_wgrad_tok needs ([R][2][9][V][128] fp32).
 PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
-  static const int cap = getenv("PBX_WGRAD_TOK_R") ? atoi(getenv("PBX_WGRAD_TOK_R")) : 256;   // sweep knob (128: +50 % time)
+  constexpr int cap = 256;   // (128: +50 % time)
   const long NT = (long)B * ((L + TBM - 1) / TBM);
   return (int)(NT < cap ? NT : cap);
 }

@@ -14,7 +14,6 @@ flat-arena ``.grad`` views.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -79,12 +78,8 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
     return dh, dz, dbo_part
 
-_lib.register("pbx_glob_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P, _P])
 _lib.register("pbx_glob3_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])
-_lib.register("pbx_glob3_bwd", [_P, _I, _I, _I, _I, _P, _P])
-_lib.register("pbx_glob3_fold", [_P, _I, _I, _I, _I, _P, _P])
-_lib.register("pbx_glob3_slab_cols", [_I, _I])
 _lib.register("pbx_pack_glob_frags", [_P, _P, _P, _I, _I, _P])
 
 LN_EPS = 1e-5
@@ -200,8 +195,9 @@ _lib.register("pbx_ann_wt", [_P, _P, _I, _I, _P])
 _lib.register("pbx_ann_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_ann_csc", [_P, _I, _I, _P, _P, _P, _P])
 _lib.register("pbx_ann_wgrad", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
-# sparse GO input layer (csrc/annot.hip); PBX_ANN_SPARSE=0 selects the dense MFMA-GEMM form
-ANN_SPARSE = os.environ.get("PBX_ANN_SPARSE", "1") != "0"
+# sparse GO input layer (csrc/annot.hip) where pbx_ann_supported; the dense MFMA-GEMM form otherwise
+# (tests flip this flag to check both forms)
+ANN_SPARSE = True
 
 
 def ann_sparse_ok(B: int, A: int, G: int) -> bool:
@@ -293,11 +289,11 @@ class InputLayerFn(torch.autograd.Function):
         if early and not all(_Grads(list(ctx.params)).direct):
             streams.cancel_fork(dev, "ann")   # returned gradients are read by autograd on this stream
             early = False
-        if (streams.GLOBAL_ENABLED or early) and dev.type == "cuda":
-            # weight gradients only: an aux stream (ops/streams.py) -- "ann", forked by the first local
-            # block's backward right after dgb was final, or the global-track stream
+        if early:
+            # weight gradients only: the "ann" aux stream (ops/streams.py), forked by the first local
+            # block's backward right after dgb was final
             extra = list(ctx.csc[:3]) if getattr(ctx, "csc", None) is not None else []
-            with streams.on_aux(dev, "ann" if early else "global", keep=[*saved, dg, dgb, *extra]) as scope:
+            with streams.on_aux(dev, "ann", keep=[*saved, dg, dgb, *extra]) as scope:
                 out = InputLayerFn._backward(ctx, saved, dg, dgb)
                 scope.keep(*[t for t in out if isinstance(t, torch.Tensor)])
             return out
@@ -348,23 +344,16 @@ def _ptrs(*ts) -> ctypes.Array:
     return arr
 
 
-# one-launch global-track kernels (csrc/glob2.hip); PBX_GLOBAL_FUSED=0 selects the library-GEMM path
-GLOBAL_FUSED = os.environ.get("PBX_GLOBAL_FUSED", "1") != "0"
-# column-split global track (csrc/glob3.hip: 3 launches per direction over ceil(B/16) x G/64 workgroups)
-# vs the one-launch form (csrc/glob2.hip, B/16 workgroups), per direction.  The backward runs beside the
-# conv weight gradient on the aux stream, where the three short launches queue behind its workgroups
-# (6 + 43 + 45 us vs 52 us for the one-launch form, profiles/r3h_critpath.txt): forward split, backward not.
-GLOB3 = os.environ.get("PBX_GLOB3", "1") != "0"              # forward
-GLOB3_BWD = os.environ.get("PBX_GLOB3_BWD", "0") != "0"      # backward
-
-
-# global-track weight gradients as one batched GEMM launch (PBX_BATCH_WGRAD=0: three split-K GEMMs + folds)
-BATCH_WGRAD = os.environ.get("PBX_BATCH_WGRAD", "1") != "0"
+# global-track kernels: the column-split forward (csrc/glob3.hip: 3 launches over ceil(B/16) x G/64
+# workgroups) and the one-launch backward (csrc/glob2.hip, B/16 workgroups: a column-split backward runs
+# beside the conv weight gradient on the aux stream, where its three short launches queued behind the
+# weight-gradient workgroups -- 6 + 43 + 45 vs 52 us, profiles/r3h_critpath.txt).  Other shapes take the
+# library-GEMM GlobalBlockFn.
 
 
 def glob_fused_ok(G: int, NGL: int) -> bool:
     """Shapes the fused global-track kernels are compiled for (pbx_glob_supported)."""
-    return GLOBAL_FUSED and G in (256, 512) and NGL in (0, 128)
+    return G in (256, 512) and NGL in (0, 128)
 
 
 _lib.register("pbx_pack_batch", [_P, _P, _I, _P])
@@ -428,19 +417,13 @@ class FusedGlobalBlockFn(torch.autograd.Function):
             vp, TVk = vp.sum(dim=1, keepdim=True), 1
         gc, gbc = g.contiguous(), g_bf.contiguous()
 
-        if GLOB3:
-            NCT = G // 64
-            z1, z2 = e(B, G), e(B, G)
-            part1, part2 = e(B, NCT, 2), e(B, NCT, 2)
-            _lib.call("pbx_glob3_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
-                                             fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
-                                             gb if NGL else None, z1, z2, part1, part2),
-                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
-        else:
-            _lib.call("pbx_glob_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
-                                            fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
-                                            gb if NGL else None),
-                      B, G, NGL, TVk, K, LN_EPS, _s(dev))
+        NCT = G // 64
+        z1, z2 = e(B, G), e(B, G)
+        part1, part2 = e(B, NCT, 2), e(B, NCT, 2)
+        _lib.call("pbx_glob3_fwd", _ptrs(gc, gbc, vp, wp, f1, b1, n1w, n1b, f2, b2, n2w, n2b,
+                                         fgl, bgl, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2, g2_bf, pregl,
+                                         gb if NGL else None, z1, z2, part1, part2),
+                  B, G, NGL, TVk, K, LN_EPS, _s(dev))
         ctx.save_for_backward(g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT)
         ctx.params = (w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl)
         ctx.meta = (TV, NGL)
@@ -450,21 +433,10 @@ class FusedGlobalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dg2, _dg2bf, dgb):
-        saved = ctx.saved_tensors
-        dev = saved[1].device
-        if streams.GLOBAL_ENABLED and dev.type == "cuda":
-            # on the global-track aux stream: it starts once the next block's LN1 finalize has
-            # produced dgb (streams.fork in LocalBlockFn.backward) and overlaps that block's conv data
-            # gradient; the local-block backward of this block waits for dvpart (streams.wait_ready)
-            with streams.on_aux(dev, "global", keep=[*saved, dg2, dgb]) as scope:
-                out = FusedGlobalBlockFn._backward(ctx, saved, dg2, dgb, on_aux=True)
-                scope.keep(*[t for t in out if isinstance(t, torch.Tensor)])
-            streams.mark_ready(dev, "global", [out[0], out[2]])
-            return out
-        return FusedGlobalBlockFn._backward(ctx, saved, dg2, dgb)
+        return FusedGlobalBlockFn._backward(ctx, ctx.saved_tensors, dg2, dgb)
 
     @staticmethod
-    def _backward(ctx, saved, dg2, dgb, on_aux=False):
+    def _backward(ctx, saved, dg2, dgb):
         g_bf, pre1, xh1, r1, vsum, g1_bf, pre2, xh2, r2, g2_bf, pregl, f1T, f2T, fglT = saved
         w1, b1, n1w, n1b, w2, b2, n2w, n2b, wp, wgl, bgl = ctx.params
         TV, NGL = ctx.meta
@@ -482,43 +454,26 @@ class FusedGlobalBlockFn(torch.autograd.Function):
         du1 = torch.empty((B, G), dtype=BF16, device=dev)
         du2 = torch.empty((B, G), dtype=BF16, device=dev)
         dugl = torch.empty((B, NGL), dtype=BF16, device=dev) if NGL else None
-        slab = None
-        if GLOB3_BWD:
-            NCT = G // 64
-            e = lambda *shape: torch.empty(shape, dtype=F32, device=dev)  # noqa: E731
-            slab = e((B + 15) // 16, _lib.lib().pbx_glob3_slab_cols(G, NGL))
-            _lib.call("pbx_glob3_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum,
-                                             wp, f1T, dg, dvs, du1, du2, dugl, e(B, G), e(B, G), e(B, NCT, 2),
-                                             e(B, NCT, 2)),
-                      B, G, NGL, wp.numel(), slab.data_ptr(), _s(dev))
-        else:
-            _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum,
-                                            wp, f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
-                                            dbgl if NGL else None, dwp),
-                      B, G, NGL, wp.numel(), _lib.ptr(_det_slab((B + 15) // 16, 6 * G + NGL + wp.numel(), dev)),
-                      _s(dev))
+        _lib.call("pbx_glob_bwd", _ptrs(dg2, dgb, pregl, fglT, xh2, r2, n2w, pre2, f2T, xh1, r1, n1w, pre1, vsum,
+                                        wp, f1T, dg, dvs, du1, du2, dugl, db1, dn1w, dn1b, db2, dn2w, dn2b,
+                                        dbgl if NGL else None, dwp),
+                  B, G, NGL, wp.numel(), _lib.ptr(_det_slab((B + 15) // 16, 6 * G + NGL + wp.numel(), dev)),
+                  _s(dev))
 
         def weight_grads():
-            if slab is not None:
-                # the per-row-tile column sums (bias / LayerNorm affine / attention-weight gradients)
-                _lib.call("pbx_glob3_fold", slab.data_ptr(), B, G, NGL, wp.numel(),
-                          _ptrs(db1, dn1w, dn1b, db2, dn2w, dn2b, dbgl if NGL else None, dwp), _s(dev))
             # dW = dU^T X for W1, W2 and the next block's global->local weight: one batched launch,
             # K = B rows, accumulated straight into the gradient destinations (no split-K slabs)
             probs = [(du1, g_bf, dw1), (du2, g1_bf, dw2)] + ([(dugl, g2_bf, dwgl)] if NGL else [])
-            if BATCH_WGRAD and all(d.is_contiguous() and d.dtype == F32 for _, _, d in probs):
+            if all(d.is_contiguous() and d.dtype == F32 for _, _, d in probs):
                 gemm_batch(probs, ta=True, tb=False, accumulate=True)
             else:
                 for a, b, d in probs:
                     addmm_into(d, a.t(), b)
 
         direct = all(gr.direct[i] for i in (0, 4)) and (not NGL or gr.direct[9])
-        if slab is not None:
-            direct = direct and all(gr.direct[i] for i in (1, 2, 3, 5, 6, 7, 8)) and (not NGL or gr.direct[10])
-        if direct and streams.ENABLED and dev.type == "cuda" and not on_aux:
-            # dW = dU^T X (K = B rows) and the column-sum fold are off the critical path: the aux
-            # (weight-gradient) stream
-            streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf, slab], name="wgrad")
+        if direct and streams.ENABLED and dev.type == "cuda":
+            # dW = dU^T X (K = B rows) is off the critical path: the aux (weight-gradient) stream
+            streams.launch(dev, weight_grads, keep=[du1, du2, dugl, g_bf, g1_bf, g2_bf], name="wgrad")
         else:
             weight_grads()
         dvpart = dvs.unsqueeze(1).expand(B, TV, G)
@@ -574,17 +529,7 @@ class GlobalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dg2, _dg2bf, dgb):
-        saved = ctx.saved_tensors
-        dev = saved[1].device
-        if streams.GLOBAL_ENABLED and dev.type == "cuda":
-            # on the global-track aux stream: it overlaps the main stream's conv data gradient of the
-            # next block; the next local-block backward waits for dvpart (streams.wait_ready)
-            with streams.on_aux(dev, "global", keep=[*saved, dg2, dgb]) as scope:
-                out = GlobalBlockFn._backward(ctx, saved, dg2, dgb)
-                scope.keep(*out)
-            streams.mark_ready(dev, "global", [out[0], out[2]])
-            return out
-        return GlobalBlockFn._backward(ctx, saved, dg2, dgb)
+        return GlobalBlockFn._backward(ctx, ctx.saved_tensors, dg2, dgb)
 
     @staticmethod
     def _backward(ctx, saved, dg2, dgb):
@@ -624,8 +569,7 @@ class GlobalBlockFn(torch.autograd.Function):
         return (dg, None, dvpart, *gr.finish())
 
 
-# the GO head's forward on the "head" aux stream beside the local head (PBX_HEAD_AUX=0: in sequence)
-HEAD_AUX = os.environ.get("PBX_HEAD_AUX", "1") != "0"
+# the GO head's forward runs on the "head" aux stream beside the local head (when aux streams are on)
 
 
 class HeadsLossFn(torch.autograd.Function):
@@ -645,7 +589,7 @@ class HeadsLossFn(torch.autograd.Function):
         V = wo.shape[0]
         A = wa.shape[0]
         loss = torch.zeros(2, dtype=F32, device=dev)
-        if HEAD_AUX and streams.ENABLED and dev.type == "cuda":
+        if streams.ENABLED and dev.type == "cuda":
             # the GO head (GEMM + VALU-heavy BCE epilogue) on its own stream beside the memory-bound
             # local head; the loss sum waits for both
             res = []

@@ -1,15 +1,16 @@
-"""Autograd wrappers of the fused CDNA4 local-track kernels (``csrc/conv2.hip``, ``csrc/wgrad.hip``,
-``csrc/ln.hip``).
+"""Autograd wrappers of the fused CDNA4 local-track kernels (``csrc/conv2.hip``, ``csrc/conv4.hip``,
+``csrc/wgrad.hip``, ``csrc/ln.hip``, ``csrc/pool.hip``).
 
 One :class:`LocalBlockFn` call is the whole local track of one ``ProteinBERTBlock`` in reference
 semantics (reference ``ProteinBERT/modules.py:201-219``)::
 
     s1 = x + GELU(conv_d1(x)) + GELU(conv_d5(x)) + gb       (conv_fwd3: 1 launch)
     h1 = LN_(L,C)(s1); s2 = h1 + GELU(h1 Wl^T + bl)           (ln_linear_fwd: 1 launch)
-    h2 = LN_(L,C)(s2); vpart = sum_tile GELU(h2 Wv_cat^T)     (ln_attn_fwd2: 1 launch)
+    h2 = LN_(L,C)(s2); vpart = sum_tile GELU(h2 Wv_cat^T)     (pool_fwd, csrc/pool.hip: 1 launch)
 
-and its backward is 7 launches (attention pool + LN2 partials, LN2 constants, LN2 + MLP, MLP dW fold,
-LN1 finalize, conv data gradient, conv weight gradient + its slab fold).  Activations are bf16
+and its backward is 6-7 launches on the main stream (attention pool with GELU' recomputed + LN2
+partials, LN2 constants, LN2 + MLP, conv data gradient with the LN1 finalize fused in) plus the conv
+weight gradient, its slab fold and the MLP dW fold on the weight-gradient stream.  Activations are bf16
 ``[B, L, 128]`` channels-last; parameters stay fp32 masters and are packed to bf16 kernel layouts
 once per forward.  The global track (``[B, 512]`` vectors) is :mod:`.global_track`.
 
@@ -18,7 +19,6 @@ Every op raises if the HIP library is missing — there is no silent eager fallb
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Dict, Optional, Tuple
 
 import torch
@@ -30,24 +30,15 @@ from .global_track import bf16_of
 
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
+_lib.register("pbx_conv_fwd3x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_fwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_fwd4x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4x", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_dgrad3", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
 _lib.register("pbx_wgrad2", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_wgrad_tok", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P])
 _lib.register("pbx_ln_linear_fwd", [_P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _I, _F, _P])
-_lib.register("pbx_ln_attn_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
-_lib.register("pbx_ln_attn_fwd2", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
-_lib.register("pbx_attn_bwd2", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _P])
-_lib.register("pbx_attn_bwd3", [_P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _F, _I, _P])
-_lib.register("pbx_attn_bwd4", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _I, _P])
-_lib.register("pbx_attn_bwd4c", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _I, _I, _P, _P, _P])
-_lib.register("pbx_pack_wvt_frag", [_P, _P, _I, _P])
 _lib.register("pbx_pool_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P])
 _lib.register("pbx_pool_bwd", [_P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _P,
@@ -69,30 +60,6 @@ LN_EPS = 1e-5     # nn.LayerNorm default (reference modules.py:148-164)
 
 
 BM1 = 128         # positions per conv-forward workgroup (= the tile of the LayerNorm-1 partials)
-# pool forward: 1 = LayerNorm-2 as its own streaming pass, the pool reads normalised rows (A/B knob)
-POOL_PRENORM = int(os.environ.get("PBX_POOL_PRENORM", "1"))
-# pool backward: 0 (default) = the forward stores GELU' as bf16 backward-operand fragments (268 MB per block at
-# B = L = 512) and attn_bwd2 streams them; 1 = memory-lean: the forward keeps only the GELU column sums
-# (83 vs 112 us) and attn_bwd3 recomputes GELU'(h2 Wv) on MFMA + VALU from the h2 rows (263 vs 208 us beside the
-# weight gradient): ~1 % slower per step, 1.6 GB less activation memory per step
-# (profiles/r3x_pool_recompute_ab.txt)
-POOL_RECOMPUTE = int(os.environ.get("PBX_POOL_RECOMPUTE", "0"))
-# pool backward: 1 (default) = weight-stationary attn_bwd4 (csrc/pool_bwd.hip: dv folded into the
-# register-resident Wv^T operand, GELU' tiles DMA'd into a 64 KB LDS double buffer, two workgroups per
-# CU); 0 = attn_bwd2 (whole Wv in 128 KB of LDS, dv applied per streamed fragment on the VALU)
-POOL_BWD4 = int(os.environ.get("PBX_POOL_BWD4", "1"))
-POOL_BWD4_TPW = int(os.environ.get("PBX_POOL_BWD4_TPW", "0"))   # tiles per workgroup (0: launcher's choice)
-# 1: attn_bwd4 runs one workgroup per sample and also writes the LayerNorm-2 / -1 backward constants (one
-# launch less per block: pbx_attn_bwd4c); 0: the launcher's tile split + ln2_consts_kernel
-POOL_CONSTS_FUSED = int(os.environ.get("PBX_POOL_CONSTS_FUSED", "1"))
-POOL_CONSTS_MIN_B: Optional[int] = None     # smallest batch for that form (None: two workgroups per CU)
-# attn_bwd3 at two waves per SIMD (8-wave workgroups sharing one Wv image) instead of one
-POOL_BWD3_WIDE = int(os.environ.get("PBX_POOL_BWD3_WIDE", "1"))
-# 1 (default): recompute-form pool (csrc/pool.hip: LN2 apply fused into the pool forward, GELU' recomputed in
-# the backward, no GELU' tensor); 0: the stored-GELU' kernels above
-POOL_V5 = int(os.environ.get("PBX_POOL_V5", "1"))
-
-
 def attn_pool_supported(NJ: int) -> bool:
     """The attention-pool kernels are built for H * value_dim = NJ in (256, 512)."""
     return NJ in (256, 512)
@@ -106,39 +73,21 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
-# conv forward: 0 (default) = conv_fwd3 (csrc/conv2.hip, epilogue after each tile's MFMAs); 1 = persistent
-# conv_fwd4 (csrc/conv4.hip: the epilogue of tile i-1 runs inside the K loop of tile i).  Equal in
-# isolation (197.5 vs 198.9 us, profiles/r4_conv_ab.txt) but 3.3 % slower in the step (76.0k vs 78.7k seq/s)
-CONV_FWD4 = int(os.environ.get("PBX_CONV_FWD4", "0"))
-
-
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream, xlo: int = 0,
              xhi: int = 0) -> None:
     """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward).
     ``xlo``/``xhi``: rows of the neighbouring sequence shards around each sample's L rows of ``x``
     (context parallelism, :mod:`..parallel.cp_fused`)."""
-    if xlo or xhi:
-        _lib.call("pbx_conv_fwd4x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
-                  gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, xlo, xhi, stream)
-        return
-    _lib.call("pbx_conv_fwd4" if CONV_FWD4 and KS == 9 else "pbx_conv_fwd3", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
-              gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, stream)
-
-
-# conv data gradient: 1 (default) = conv_dgrad4 (csrc/conv4.hip: 4 waves, each over both convs into one
-# accumulator set, no cross-wave LDS reduction); 0 = conv_dgrad3 (csrc/conv2.hip)
-CONV_DGRAD4 = int(os.environ.get("PBX_CONV_DGRAD4", "1"))
+    _lib.call("pbx_conv_fwd3x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+              gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, xlo, xhi, stream)
 
 
 def conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream, ilo: int = 0, ihi: int = 0) -> None:
     """``pre_n``/``pre_w``: the GELU'(pre-activation) images :func:`conv_fwd` stored; ``ilo``/``ihi``:
-    neighbouring shards' rows around ``ds1`` / GELU' (context parallelism)."""
-    if ilo or ihi:
-        _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
-                  wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, ilo, ihi, stream)
-        return
-    _lib.call("pbx_conv_dgrad4" if CONV_DGRAD4 and KS == 9 else "pbx_conv_dgrad3", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
-              wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, stream)
+    neighbouring shards' rows around ``ds1`` / GELU' (context parallelism).  csrc/conv4.hip conv_dgrad4:
+    4 waves, each over both convs into one accumulator set."""
+    _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(),
+              wtw.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, ilo, ihi, stream)
 
 
 _DWL_SLAB: Dict[int, torch.Tensor] = {}
@@ -183,36 +132,18 @@ def _grad_dst(p: torch.Tensor, shape) -> Tuple[torch.Tensor, bool]:
 
 
 # the first block's weight gradient is the last kernel of the backward (the main stream only has the
-# embedding / input-layer tail left beside it): it takes every CU (PBX_WGRAD_TAIL_FULL=0: 7/8 as the rest)
-WGRAD_TAIL_FULL = os.environ.get("PBX_WGRAD_TAIL_FULL", "1") != "0"
-# the local-MLP dWl / dbl slab folds run on the weight-gradient stream (PBX_LN2_LATE_FOLD=0: on the main
+# embedding / input-layer tail left beside it): it takes every CU (the other blocks' take 7/8)
+WGRAD_TAIL_FULL = True
+# the local-MLP dWl / dbl slab folds run on the weight-gradient stream (False: on the main
 # stream right after the LN2 / MLP backward kernel)
-LN2_LATE_FOLD = os.environ.get("PBX_LN2_LATE_FOLD", "1") != "0"
-# PBX_DGRAD_STREAM=1: the conv data gradient of blocks 1.. on its own aux stream ("dg") so the previous
-# block's global-track backward (next on the main stream) runs beside it.  Measured 1.9 % SLOWER
-# (profiles/r4_dgrad_stream_ab.txt): the one-launch global backward (8-wave workgroups) only finds CUs as
-# conv_dgrad4's 2-per-CU workgroups drain and stretches from 51 to ~210 us.  Off.
-DGRAD_STREAM = os.environ.get("PBX_DGRAD_STREAM", "0") == "1"
+LN2_LATE_FOLD = True
 # the LN1 backward finalize fused into the conv data gradient (csrc/conv4.hip conv_dgrad4<FIN>): dS1 is
-# computed in the staging pass and never stored (PBX_DGRAD_FIN=0: ln1_finalize + conv_dgrad4); not in the
+# computed in the staging pass and never stored (False: ln1_finalize + conv_dgrad4); not in the
 # deterministic mode (its dgb column sums are float atomics per tile) nor under context parallelism
-DGRAD_FIN = os.environ.get("PBX_DGRAD_FIN", "1") != "0"
-# PBX_WGRAD_DEFER=1: a block's conv weight gradient (aux stream) is launched after the NEXT block's pool
-# backward instead of right after its own data gradient, so it overlaps the LN2 / MLP backward, the LN1
-# finalize and the data gradient rather than the memory-bound pool backward (experiment, off by default)
-WGRAD_DEFER = os.environ.get("PBX_WGRAD_DEFER", "0") == "1"
-_DEFERRED: List = []
-
-
-def flush_deferred() -> None:
-    while _DEFERRED:
-        _DEFERRED.pop(0)()
-
-
-streams.pre_join_hooks.append(flush_deferred)
-# the input layer's backward starts beside the first block's conv data gradient (PBX_INPUT_BWD_EARLY=0:
+DGRAD_FIN = True
+# the input layer's backward starts beside the first block's conv data gradient (False:
 # on the main stream after it)
-INPUT_BWD_EARLY = os.environ.get("PBX_INPUT_BWD_EARLY", "1") != "0"
+INPUT_BWD_EARLY = True
 
 
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
@@ -225,8 +156,6 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     # (R = 56 on 256 CUs): the aux-stream weight gradient runs beside the main-stream backward, and
     # leaving it a few CUs measured +2.4 % on the step over R = 64 (R = 48: +1.3 %, 32: -0.4 %)
     R = max(8, (7 * _num_cus(dev) // (16 * nconv)) // 8 * 8)
-    if os.environ.get("PBX_WGRAD_R"):       # sweep knob (tools/gpu_r3_rs.sh)
-        R = int(os.environ["PBX_WGRAD_R"])
     if full_chip:
         R = max(8, (_num_cus(dev) // (2 * nconv)) // 8 * 8)
     R = min(R, ntiles)
@@ -244,17 +173,17 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
 
 
 # the first block's conv weight gradient through the token one-hot (csrc/wgrad.hip wgrad_tok: its input is
-# the embedding bf16(E[tok]), so dW = E^T S with S a 32-row one-hot GEMM); PBX_WGRAD_TOK=0: wgrad2 over the
+# the embedding bf16(E[tok]), so dW = E^T S with S a 32-row one-hot GEMM); False: wgrad2 over the
 # 128 embedding channels
-WGRAD_TOK = os.environ.get("PBX_WGRAD_TOK", "1") != "0"
+WGRAD_TOK = True
 # ... and its conv data gradient is folded away: the block input is the embedding, so only
 # dE = sum_{tok} (dS1 + conv^T dpre) is needed -- the dS1 part in one pass that also writes dpre
 # (pbx_embed_dpre), the conv^T part as bf16(W)-weighted sums of the weight gradient's one-hot S
-# (pbx_wgrad_tok).  PBX_EMBED_FOLD=0: conv data gradient + embedding backward as for any block.
-EMBED_FOLD = os.environ.get("PBX_EMBED_FOLD", "1") != "0"
+# (pbx_wgrad_tok).  False: conv data gradient + embedding backward as for any block.
+EMBED_FOLD = True
 # ... and (reference semantics) its conv gathers emb[tok] in the staging pass: the [B, L, 128] embedding
-# output is never written (PBX_EMBED_GATHER=0: embed_fwd + conv_fwd3)
-EMBED_GATHER = os.environ.get("PBX_EMBED_GATHER", "1") != "0"
+# output is never written (False: embed_fwd + conv_fwd3)
+EMBED_GATHER = True
 
 
 def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: int, KS: int) -> bool:
@@ -372,34 +301,14 @@ class LocalBlockFn(torch.autograd.Function):
                   wl_b.data_ptr(), bl.data_ptr(), _p(pre_l), s2.data_ptr(), st2.data_ptr(), B, L, LN_EPS, stream)
         if cp is not None:
             cp.fix_stats(st2, PB)
+        # LN2 apply + attention pool in one launch (csrc/pool.hip); the backward recomputes GELU' from h2
         h2 = torch.empty_like(xt)
-        if POOL_V5:
-            # LN2 apply + attention pool in one launch (csrc/pool.hip); the backward recomputes GELU' from h2
-            TV = (L + 31) // 32                 # one vpart row per 32-position tile
-            vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
-            _lib.call("pbx_pool_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(), wv_bf16.data_ptr(),
-                      h2.data_ptr(), vpart.data_ptr(), B, L, NJ, LN_EPS, stream)
-            recompute, gfrag = True, None
-        else:
-            TV = (L + 63) // 64                 # one vpart row per 64-position wave tile
-            vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
-            recompute = need_bwd and POOL_RECOMPUTE and POOL_PRENORM
-            if need_bwd:
-                # recompute: GELU column sums only, the backward re-derives GELU' from h2 (attn_bwd3); else GELU'
-                # of the pool as bf16 backward-operand fragments: [B][2 ceil(L/64) tiles of 32][NJ * 32]
-                gfrag = None if recompute else torch.empty((B, 2 * TV, NJ * 32), dtype=torch.bfloat16, device=dev)
-                _lib.call("pbx_ln_attn_fwd2", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                          wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), _p(gfrag), B, L, NJ, LN_EPS,
-                          POOL_PRENORM, stream)
-            else:
-                # forward-only pool (GELU only, 8 independent waves per workgroup)
-                gfrag = None
-                _lib.call("pbx_ln_attn_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(),
-                          wv_bf16.data_ptr(), h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 8, LN_EPS, stream)
-        # the pool backward's operand: the GELU' fragments, or the block output rows h2 it recomputes them from
-        ctx.recompute = recompute
-        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2 if recompute else gfrag, wtn, wtw,
-                              wl_b, wv_bf16, g1, be1, g2, be2)
+        TV = (L + 31) // 32                     # one vpart row per 32-position tile
+        vpart = torch.empty((B, TV, NJ), dtype=torch.float32, device=dev)
+        _lib.call("pbx_pool_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(), wv_bf16.data_ptr(),
+                  h2.data_ptr(), vpart.data_ptr(), B, L, NJ, LN_EPS, stream)
+        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2,
+                              be2)
         ctx.hlo = hlo
         ctx.tok = (tok, emb) if cp is None and wgrad_tok_ok(tok, emb, L, KS) else None
         ctx.emb_grad = bool(emb_grad)
@@ -413,10 +322,8 @@ class LocalBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, dvpart):
-        # dvpart: produced by the global-track backward on its aux stream (PBX_GLOBAL_STREAM=1); dh2: by
-        # the next block's conv data gradient on the "dg" stream
-        streams.wait_ready(dvpart, dh2)
-        (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, gfrag, wtn, wtw, wl_b, wv_bf16, g1, be1, g2,
+        streams.wait_ready(dvpart, dh2)         # producers on an aux stream (none by default)
+        (x_ext, pre_n, pre_w, s1, st1, pre_l, s2, st2, h2, wtn, wtw, wl_b, wv_bf16, g1, be1, g2,
          be2) = ctx.saved_tensors
         cp, hlo = ctx.cp, ctx.hlo
         x = s1                                  # shape / dtype / device template of the [B, L, C] activations
@@ -430,27 +337,21 @@ class LocalBlockFn(torch.autograd.Function):
             # this shard's rows of the [L, C] affine gradients (the kernels accumulate into them)
             dg1, dbe1, dg2, dbe2 = (cp.rows(t) for t in (dg1, dbe1, dg2, dbe2))
         dh2 = None if dh2 is None else dh2.to(torch.bfloat16).contiguous()
-        if POOL_V5:
-            # pool backward (csrc/pool.hip): GELU' recomputed from h2 (= gfrag here), LN2 partials per 32-position
-            # tile; the LN2 / LN1 constants come from ln2_consts_kernel inside pbx_ln2_linear_bwd
-            TA = (L + 31) // 32
-            if dvpart is None:
-                dv, dv_tiles = torch.zeros((B, NJ), dtype=torch.float32, device=dev), 1
-            elif dvpart.dim() == 3 and (dvpart.shape[1] == 1 or dvpart.stride(1) == 0):
-                dv, dv_tiles = dvpart[:, 0, :].float().contiguous(), 1     # one gradient row per sample
-            else:
-                dv, dv_tiles = dvpart.float().contiguous(), TA
-            dh2t = torch.empty_like(x)
-            sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-            consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
-            dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
-            consts_ready = 0
-            _lib.call("pbx_pool_bwd", gfrag.data_ptr(), g2.data_ptr(), be2.data_ptr(), _p(dh2), dv.data_ptr(), dv_tiles,
-                      wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, stream)
+        # pool backward (csrc/pool.hip): GELU' recomputed from h2, LN2 partials per 32-position tile; the LN2 /
+        # LN1 constants come from ln2_consts_kernel inside pbx_ln2_linear_bwd
+        TA = (L + 31) // 32
+        if dvpart is None:
+            dv, dv_tiles = torch.zeros((B, NJ), dtype=torch.float32, device=dev), 1
+        elif dvpart.dim() == 3 and (dvpart.shape[1] == 1 or dvpart.stride(1) == 0):
+            dv, dv_tiles = dvpart[:, 0, :].float().contiguous(), 1     # one gradient row per sample
         else:
-            TA, dh2t, sums2, consts, dgb, consts_ready = LocalBlockFn._pool_bwd_v4(
-                ctx, gfrag, s2, st2, g2, dh2, dvpart, wv_bf16, st1, cp, B, L, T1, NJ, dev, stream)
-        flush_deferred()                         # the previous (deeper) block's deferred weight gradient
+            dv, dv_tiles = dvpart.float().contiguous(), TA
+        dh2t = torch.empty_like(x)
+        sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
+        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
+        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
+        _lib.call("pbx_pool_bwd", h2.data_ptr(), g2.data_ptr(), be2.data_ptr(), _p(dh2), dv.data_ptr(), dv_tiles,
+                  wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, stream)
         if cp is not None:
             cp.fix_sums(sums2)
         # LN2 finalize + local MLP backward + LN1 partials + both [L, C] affine gradients
@@ -472,7 +373,7 @@ class LocalBlockFn(torch.autograd.Function):
                   g2.data_ptr(), pre_l.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, g1.data_ptr(),
                   be1.data_ptr(), wl_b.data_ptr(), consts.data_ptr(), dh1.data_ptr(), sums1.data_ptr(),
                   dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(), dbl.data_ptr(),
-                  dgb.data_ptr(), B, L, LN_EPS, *slab_args, det, int(not late_fold), consts_ready, stream)
+                  dgb.data_ptr(), B, L, LN_EPS, *slab_args, det, int(not late_fold), 0, stream)
         if late_fold:
             def fold(slab=fslab, rows=rows, dwl=dwl, dbl=dbl):
                 st = _lib.stream_ptr(dev)
@@ -484,17 +385,11 @@ class LocalBlockFn(torch.autograd.Function):
         dpw = torch.empty_like(x)
         if cp is not None:
             cp.fix_sums(sums1)
-        dg_aux = (DGRAD_STREAM and cp is None and not ctx.tail and streams.ENABLED and not streams.GLOBAL_ENABLED
-                  and dev.type == "cuda")
         # the LN1 finalize fused into the conv data gradient (DGRAD_FIN; its dgb is final only after it)
-        fin = (DGRAD_FIN and cp is None and not ctx.emb_grad and not dg_aux and CONV_DGRAD4 and KS == 9
-               and dev.type == "cuda" and not fused_deterministic())
+        fin = (DGRAD_FIN and cp is None and not ctx.emb_grad and KS == 9 and dev.type == "cuda"
+               and not fused_deterministic())
 
         def dgb_ready():
-            if streams.GLOBAL_ENABLED:
-                # the previous block's global-track backward (next autograd node, aux stream) needs only
-                # dgb: let it start here, beside the conv data gradient below
-                streams.fork(dev, "global")
             if ctx.tail and INPUT_BWD_EARLY and streams.ENABLED and dev.type == "cuda":
                 # first block: the input layer's backward (the last autograd node but one) needs only dgb
                 # and the global-track gradient, both final here -- it runs on the "ann" stream beside this
@@ -521,12 +416,6 @@ class LocalBlockFn(torch.autograd.Function):
             # first block, folded: no conv data gradient (the conv part of dE comes with the weight gradient)
             demb, dE_direct = embed_fold_bwd(*ctx.tok, ds1, pre_n, pre_w, dpn, dpw, params[0], params[2], stream)
             dE = demb[2]
-        elif dg_aux:
-            streams.launch(dev, lambda: conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil,
-                                                   _lib.stream_ptr(dev)),
-                           keep=[ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw], name="dg")
-            streams.mark_ready(dev, "dg", [dx])
-            streams.chain(dev, "wgrad", "dg")   # the weight gradient reads dpre_n / dpre_w
         elif cp is None:
             conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
         else:
@@ -547,16 +436,7 @@ class LocalBlockFn(torch.autograd.Function):
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and (demb is None or dE_direct) and streams.ENABLED:
             # the weight gradient goes to the aux stream: off the critical path, only the optimizer
             # and the DP all-reduce read it (its inputs stay referenced until the join)
-            if WGRAD_DEFER and not ctx.tail and cp is None and dev.type == "cuda":
-                conv_params = list(params[:4])
-
-                def deferred(wg=wg, keep=keep, conv_params=conv_params):
-                    streams.launch(dev, wg, keep=keep, name="wgrad")
-                    notify_grads_ready(conv_params)     # DP buckets see them once their kernel is enqueued
-                _DEFERRED.append(deferred)
-                direct = [p for p in direct if not any(p is c for c in conv_params)]
-            else:
-                streams.launch(dev, wg, keep=keep, name="wgrad")
+            streams.launch(dev, wg, keep=keep, name="wgrad")
         else:
             wg()
         if direct:
@@ -564,49 +444,6 @@ class LocalBlockFn(torch.autograd.Function):
         pgrads = [None if d else g for (g, d) in dsts]
         gemb = dE if demb is not None and not dE_direct else None
         return (dx, dgb, *pgrads, None, None, None, None, None, None, gemb, None)
-
-    @staticmethod
-    def _pool_bwd_v4(ctx, gfrag, s2, st2, g2, dh2, dvpart, wv_bf16, st1, cp, B, L, T1, NJ, dev, stream):
-        BMV = 64                                # positions per forward vpart row
-        TV = (L + BMV - 1) // BMV
-        if dvpart is None:
-            dvpart = torch.zeros((B, TV, NJ), dtype=torch.float32, device=dev)
-        if dvpart.dim() == 3 and dvpart.stride(1) == 0:
-            # same gradient for every forward tile (it comes from sum_t vpart): one row per sample
-            dvpart = dvpart[:, 0, :].float().contiguous()
-            BMV = (L + 31) // 32 * 32
-        dvpart = dvpart.float().contiguous()
-        # attention pool + LN2 partials
-        TA = (L + 31) // 32                      # LN2 partials per 32-position wave tile
-        dh2t = torch.empty_like(s2)
-        bwd4 = POOL_BWD4 and not ctx.recompute and dvpart.dim() == 2
-        if bwd4:
-            TA *= 4                              # attn_bwd4: one partial per (tile, wave)
-        sums2 = torch.empty((B, TA, 2), dtype=torch.float32, device=dev)
-        consts = torch.empty((B, 8), dtype=torch.float32, device=dev)
-        dgb = torch.empty((B, CH), dtype=torch.float32, device=dev)      # zeroed by the consts writer
-        # one workgroup per sample only when the batch alone fills two workgroups per CU (long sequences at
-        # small B keep the tile split); CP rewrites the LN2 partials group-wide between the pool backward and
-        # the constants: separate launch
-        min_b = POOL_CONSTS_MIN_B if POOL_CONSTS_MIN_B is not None else 2 * _num_cus(dev)
-        consts_ready = int(bool(bwd4 and POOL_CONSTS_FUSED and cp is None and dev.type == "cuda" and B >= min_b))
-        if consts_ready:
-            _lib.call("pbx_attn_bwd4c", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
-                      LN_EPS, st1.data_ptr(), T1, BM1, consts.data_ptr(), dgb.data_ptr(), stream)
-        elif bwd4:
-            _lib.call("pbx_attn_bwd4", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), wvt_frag(wv_bf16).data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ,
-                      LN_EPS, POOL_BWD4_TPW, stream)
-        elif ctx.recompute:
-            _lib.call("pbx_attn_bwd3", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                      POOL_BWD3_WIDE, stream)
-        else:
-            _lib.call("pbx_attn_bwd2", gfrag.data_ptr(), s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), _p(dh2),
-                      dvpart.data_ptr(), BMV, wv_bf16.data_ptr(), dh2t.data_ptr(), sums2.data_ptr(), B, L, NJ, LN_EPS,
-                      stream)
-        return TA, dh2t, sums2, consts, dgb, consts_ready
 
 
 def embed_tokens(tokens: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
@@ -663,20 +500,6 @@ def _wv_bf16(att) -> torch.Tensor:
         cached = (key, att.value_weight_cat().t().to(torch.bfloat16).contiguous())
         att._pbx_wv_cache = cached
     return cached[1]
-
-
-def wvt_frag(wv_bf16: torch.Tensor) -> torch.Tensor:
-    """Wv^T MFMA A-operand fragment image of a bf16 ``[NJ, 128]`` value weight (attn_bwd4's stationary
-    operand), cached on the tensor: in reference semantics the value weights are untrained buffers and
-    their bf16 copy is itself cached across steps (:func:`_wv_bf16`), so the image is built once."""
-    key = (wv_bf16._version, wv_bf16.data_ptr())
-    cached = getattr(wv_bf16, "_pbx_wvt", None)
-    if cached is not None and cached[0] == key:
-        return cached[1]
-    out = torch.empty_like(wv_bf16)
-    _lib.call("pbx_pack_wvt_frag", wv_bf16.data_ptr(), out.data_ptr(), wv_bf16.shape[0], _lib.stream_ptr(wv_bf16.device))
-    wv_bf16._pbx_wvt = (key, out)
-    return out
 
 
 def conv_images(wn: torch.Tensor, ww: torch.Tensor):

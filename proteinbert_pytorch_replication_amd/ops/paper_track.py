@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import ctypes
 import math
-import os
 
 import torch
 
@@ -52,31 +51,14 @@ _lib.register("pbx_paper_head_parts", [ctypes.c_long])
 _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 
 # paper attention form: "fused" (csrc/paper_fused.hip: K/V projections on MFMA inside the attention
-# kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}) or "split" (library K/V GEMM +
-# csrc/paper_attn.hip core); PBX_PAPER_ATTN=split selects the latter
-PAPER_ATTN = os.environ.get("PBX_PAPER_ATTN", "fused")
+# kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}); other head counts take "split" (in-tree
+# K/V GEMM + csrc/paper_attn.hip core; tests force it to check the fallback)
+PAPER_ATTN = "fused"
 FUSED_CHUNK_F = 256                         # positions per forward work item
-FUSED_BWD_WAVES = int(os.environ.get("PBX_PF_BWD_WAVES", "8"))   # backward: 32 positions per wave
-
-# weight gradients of the K/V projections and of the local head (K = B*L reductions): the in-tree
-# split-K MFMA GEMM (default) or chunked library bmm (PBX_PAPER_WGRAD=bmm, A/B)
-PAPER_WGRAD_GEMM = os.environ.get("PBX_PAPER_WGRAD", "gemm") != "bmm"
-# the attention projections' weight gradients on the weight-gradient stream (PBX_PAPER_ATT_WGRAD_AUX=0: on
-# the main stream, inline)
-ATT_WGRAD_AUX = os.environ.get("PBX_PAPER_ATT_WGRAD_AUX", "1") != "0"
+FUSED_BWD_WAVES = 8                         # backward: 32 positions per wave
 
 LN_EPS = 1e-5
 TR = 32          # positions per work item of the paper LayerNorm kernels
-
-
-def _split_k_chunks(R: int, cap: int = 128) -> int:
-    """Number of row chunks for the split-K weight-gradient GEMMs (K = B*L rows): the library GEMM
-    of a [128, R] x [R, 768] product has 12 output tiles, i.e. 12 busy CUs; chunked bmm gives
-    chunks x 12 tiles and the chunk partials are summed in fp32."""
-    for c in range(cap, 0, -1):
-        if R % c == 0:
-            return c
-    return 1
 
 
 class PaperBlockFn(torch.autograd.Function):
@@ -208,14 +190,9 @@ class PaperBlockFn(torch.autograd.Function):
 
             def att_wgrad(dpre=dpre, h2=h2, dqpre=dqpre, g_bf=g_bf, gf32=gf32):
                 # attention projection weight gradients: dWk | dWv = h2^T dpre (K = B*L), dWq = g^T dqpre
-                if PAPER_WGRAD_GEMM:
-                    # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
-                    dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
-                    _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)               # [C, N] fp32
-                else:
-                    nc = _split_k_chunks(R)
-                    dwcat = torch.bmm(h2.view(nc, R // nc, C).transpose(1, 2), dpre.view(nc, R // nc, -1),
-                                      out_dtype=F32).sum(dim=0)                           # [C, N] fp32
+                # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
+                dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
+                _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)                   # [C, N] fp32
                 dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
                 dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
                 G = g_bf.shape[1]
@@ -223,7 +200,7 @@ class PaperBlockFn(torch.autograd.Function):
                 dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
                 return [dwcat, dwq]
 
-            if ATT_WGRAD_AUX and streams.ENABLED and dev.type == "cuda" and all(d for _, d in dsts[10:]):
+            if streams.ENABLED and dev.type == "cuda" and all(d for _, d in dsts[10:]):
                 # only the optimizer and the DP all-reduce read them: beside the critical path, on the
                 # weight-gradient stream (the split-K GEMM over B*L rows was ~60 us per block on it)
                 streams.launch(dev, att_wgrad, keep=[dpre, h2, dqpre, g_bf, gf32], name="wgrad")
@@ -238,8 +215,6 @@ class PaperBlockFn(torch.autograd.Function):
                   dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
                   dbl.data_ptr(), *dwl_slab(dev), B, L, stream)
         dgb = dgbp.sum(dim=1)
-        if streams.GLOBAL_ENABLED:
-            streams.fork(dev, "global")
         dpn, dpw = torch.empty_like(x), torch.empty_like(x)
         demb, dE_direct, dx = None, True, None
         if ctx.emb_grad:
@@ -333,14 +308,9 @@ class PaperHeadsLossFn(torch.autograd.Function):
         _lib.call("pbx_colsum_add", loss_part.data_ptr(), parts, 1, loss.data_ptr(), None, st)
         dbo = torch.zeros(V, dtype=F32, device=dev)
         _lib.call("pbx_colsum_add", dbo_part.data_ptr(), parts, V, dbo.data_ptr(), None, st)
-        if PAPER_WGRAD_GEMM:
-            dwo32 = torch.empty((32, C), dtype=F32, device=dev)
-            _gemm(dzl, hb, dwo32, ta=True, tb=False)                                        # K = B*L: split-K
-            dwo = dwo32[:V]
-        else:
-            nc = _split_k_chunks(R)
-            dwo = torch.bmm(dzl[:, :V].reshape(nc, -1, V).transpose(1, 2), hb.view(nc, -1, C),
-                            out_dtype=F32).sum(dim=0)
+        dwo32 = torch.empty((32, C), dtype=F32, device=dev)
+        _gemm(dzl, hb, dwo32, ta=True, tb=False)                                            # K = B*L: split-K
+        dwo = dwo32[:V]
         dz, dba, gx = go_head_forward(g2_bf, wa, ba, y_g, w_g, loss[1:])
         ctx.save_for_backward(dh, dwo, dbo, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)

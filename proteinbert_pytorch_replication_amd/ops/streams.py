@@ -4,12 +4,11 @@ Two pieces of one block's backward do not feed the critical path directly:
 
 * ``wgrad``  - the conv weight gradient (``pbx_wgrad`` + slab reduction, ~1 ms of a 5 ms
   paper-config step): only the optimizer and the DP all-reduce read it;
-* ``dg``     - the conv data gradient of blocks 1.. (ops/local_track.py DGRAD_STREAM): the previous
-  block's global-track backward, next on the main stream, is dispatched beside it instead of after it;
-  the next local-block backward waits for its ``dx`` (:func:`wait_ready`);
-* ``global`` - the global-track backward of the previous block (~0.1 ms of small GEMMs and row
-  LayerNorms per block): its outputs are consumed by the NEXT local-block backward, so it can run
-  beside this block's conv data gradient instead of after it (opt-in, see GLOBAL_ENABLED).
+* ``head`` / ``ann`` - the GO head's forward beside the local head, the input layer's backward beside
+  the first block's conv data gradient (ops/global_track.py).
+
+(Rounds 2-4 also measured the conv data gradient and the global-track backward on streams of their own:
+1.9 % and 1 % slower -- their kernels only found CUs as the critical-path kernels drained; removed.)
 
 Issuing them on their own HIP streams lets the hardware run them beside the main-stream kernels.
 Protocol (eager and under hipGraph capture, where fork/join become graph edges):
@@ -36,13 +35,6 @@ from typing import Dict, Iterable, List, Optional, Tuple
 import torch
 
 ENABLED = os.environ.get("PBX_AUX_STREAM", "1") != "0"            # conv weight gradient
-# The global-track backward on its own stream measured SLOWER on MI355X (round 2, when it still ran on
-# library GEMMs: 5.2 -> 5.4-5.8 ms/step, paper config): its small GEMMs took CUs from the critical-path conv data gradient beside
-# the weight-gradient stream; a high-priority critical-path stream did not recover it.  Round 3, with the
-# one-kernel global backward: still 1 % slower, and 1 % slower again with the global stream at high
-# priority (profiles/r3o_global_stream_prio_ab.txt: it gets CUs only as the data gradient drains).  Off.
-GLOBAL_ENABLED = os.environ.get("PBX_GLOBAL_STREAM", "0") == "1"
-
 _streams: Dict[Tuple[int, str], torch.cuda.Stream] = {}
 _pending: Dict[int, List[torch.Tensor]] = {}
 _used: Dict[int, set] = {}
@@ -99,20 +91,14 @@ _events: Dict[Tuple[int, int], torch.cuda.Event] = {}
 # Under hipGraph capture a fork whose aux body starts at the main stream's current tail makes that tail
 # node have two children, and the graph executor continues a node's queue with its FIRST child in
 # capture order -- the aux body (e.g. the conv weight gradient) would take the main chain's queue and
-# the critical path would wait behind it.  PBX_GRAPH_MARKER=1 (default) captures an empty main-stream
-# kernel before the aux body so the main chain is the first child (tests/test_graph_step.py).
-GRAPH_MARKER = os.environ.get("PBX_GRAPH_MARKER", "1") != "0"
-# PBX_STREAM_FAST=0: per-call wait_stream events and the torch.cuda.stream context (A/B of the host cost)
-_FAST = os.environ.get("PBX_STREAM_FAST", "1") != "0"
+# the critical path would wait behind it.  An empty main-stream kernel is captured before the aux body so
+# the main chain is the first child (tests/test_graph_step.py).
 
 
 def _wait(dst: torch.cuda.Stream, src: torch.cuda.Stream) -> None:
     """``dst`` waits for the work enqueued on ``src`` so far.  ``Stream.wait_stream`` creates a new
     event per call (~20 such hand-offs per step); a wait binds to the event's latest record at the
     time it is enqueued, so one cached event per (dst, src) pair is reused."""
-    if not _FAST:
-        dst.wait_stream(src)
-        return
     key = (dst.cuda_stream, src.cuda_stream)
     ev = _events.get(key)
     if ev is None:
@@ -147,7 +133,7 @@ def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
     aux = _aux(device, name)
     if not _forked.pop((idx, name), False):
         _wait(aux, main)
-        if GRAPH_MARKER and torch.cuda.is_current_stream_capturing():
+        if torch.cuda.is_current_stream_capturing():
             from . import _lib
             _lib.call("pbx_noop", main.cuda_stream)
     scope = _AuxScope(idx)
@@ -156,11 +142,6 @@ def on_aux(device: torch.device, name: str, keep: Iterable[torch.Tensor] = ()):
     _main[idx] = main
     # set_stream in place of the torch.cuda.stream context (the step enters ~20 of these scopes;
     # the context manager's device bookkeeping cost ~20 us of host time each)
-    if not _FAST:
-        with torch.cuda.stream(aux):
-            yield scope
-        _queue_join()
-        return
     torch.cuda.set_stream(aux)
     try:
         yield scope
@@ -209,15 +190,9 @@ def wait_ready(*tensors) -> None:
                     _wait(cur, _streams[key])
 
 
-# callables run at the start of join(): launches that a backward deferred (ops/local_track.py WGRAD_DEFER)
-pre_join_hooks: List = []
-
-
 def join() -> None:
     """Main stream(s) wait for every aux stream; release the tensors kept for them."""
     _callback_queued["v"] = False
-    for hook in pre_join_hooks:
-        hook()
     for idx, keep in list(_pending.items()):
         if not keep and not _used.get(idx):
             continue

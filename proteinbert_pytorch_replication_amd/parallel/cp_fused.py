@@ -6,7 +6,7 @@ What couples the slices (reference ``ProteinBERT/modules.py:124-151,201-231``) a
 exchanged:
 
 * the narrow / wide dilated convolutions need ``4 d`` = 20 neighbour rows on each side: the halo is
-  gathered once per block (``halo_rows``) and the conv kernels read it in place (``pbx_conv_fwd4x`` /
+  gathered once per block (``halo_rows``) and the conv kernels read it in place (``pbx_conv_fwd3x`` /
   ``pbx_wgrad2x`` take ``xlo`` / ``xhi`` halo rows; the data gradient ``pbx_conv_dgrad4x`` reads the
   neighbours' ``ds1`` and GELU' rows the same way, so no gradient is sent back);
 * ``LayerNorm((L, C))`` statistics are per sample over the WHOLE sequence: the kernels' per-tile

@@ -50,8 +50,8 @@ def torch_local(x, gb, blk):
                                         (1024, 2, False), (4096, 1, False), (512, 3, True), (300, 2, True),
                                         (4096, 1, True)])
 def test_local_block_forward(L, B, frozen):
-    """frozen: no input needs a gradient (frozen-encoder / inference forward): the forward-only pool
-    kernel (pbx_ln_attn_fwd) runs and no backward state is written."""
+    """frozen: no input needs a gradient (frozen-encoder / inference forward): no backward state (conv
+    GELU' images, MLP pre-activation) is written."""
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
     m, blk = make_block(L)
     if frozen:
@@ -68,29 +68,14 @@ def test_local_block_forward(L, B, frozen):
     assert e_v < 1.5e-2
 
 
-# pool backward: attn_bwd4 (weight-stationary, csrc/pool_bwd.hip) / attn_bwd2 (stored GELU' fragments, Wv in
-# LDS) / attn_bwd3 (GELU' recomputed) at 1 or 2 waves per SIMD; tpw: attn_bwd4 tiles per workgroup;
 # conv: 3 = conv_fwd3 + conv_dgrad4 with the LN1 finalize fused in (default), 5 = the same with a separate
-# ln1_finalize, 4 = persistent conv_fwd4 + conv_dgrad4, 2 = conv_fwd3 + conv_dgrad3
-@pytest.mark.parametrize("recompute,wide,bwd4,tpw,conv", [(0, 1, 1, 0, 3), (0, 1, 1, 3, 3), (0, 1, 1, 16, 3),
-                                                          (0, 1, 0, 0, 3),
-                                                          (1, 1, 0, 0, 3), (1, 0, 0, 0, 3), (0, 1, 1, 0, 4),
-                                                          (0, 1, 1, 0, 2), (0, 1, 1, 0, 5)])
+# ln1_finalize; the pool is csrc/pool.hip (GELU' recomputed in the backward)
+@pytest.mark.parametrize("conv", [3, 5])
 @pytest.mark.parametrize("L,B", [(512, 2), (200, 3), (4096, 1), (300, 40), (64, 4)])
-def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatch):
+def test_local_block_backward(L, B, conv, monkeypatch):
     from proteinbert_pytorch_replication_amd.ops import local_track
     from proteinbert_pytorch_replication_amd.ops.local_track import local_block
-    monkeypatch.setattr(local_track, "CONV_FWD4", int(conv == 4))
-    monkeypatch.setattr(local_track, "CONV_DGRAD4", int(conv != 2))
     monkeypatch.setattr(local_track, "DGRAD_FIN", conv != 5)
-    monkeypatch.setattr(local_track, "POOL_RECOMPUTE", recompute)
-    monkeypatch.setattr(local_track, "POOL_BWD3_WIDE", wide)
-    monkeypatch.setattr(local_track, "POOL_BWD4", bwd4)
-    monkeypatch.setattr(local_track, "POOL_BWD4_TPW", tpw)
-    # tpw = 0: one workgroup per sample writing the LN constants too (pbx_attn_bwd4c, the default when the
-    # batch fills the chip; forced here for every B); tpw > 0: the tile-split pbx_attn_bwd4 + ln2_consts_kernel
-    monkeypatch.setattr(local_track, "POOL_CONSTS_FUSED", int(tpw == 0))
-    monkeypatch.setattr(local_track, "POOL_CONSTS_MIN_B", 0)
     m, blk = make_block(L, seed=1)
     x0 = torch.randn(B, L, 128, device="cuda").to(torch.bfloat16)
     gb0 = torch.randn(B, 128, device="cuda") * 0.5
@@ -122,7 +107,7 @@ def test_local_block_backward(L, B, recompute, wide, bwd4, tpw, conv, monkeypatc
 
 @pytest.mark.parametrize("B,L,P", [(2, 256, 2), (3, 300, 3)])
 def test_cp_halo_conv_kernels_match_whole_sequence(B, L, P):
-    """The context-parallel conv launchers (pbx_conv_fwd4x / pbx_conv_dgrad4x / pbx_wgrad2x: neighbour
+    """The context-parallel conv launchers (pbx_conv_fwd3x / pbx_conv_dgrad4x / pbx_wgrad2x: neighbour
     rows in place, csrc/conv4.hip, csrc/wgrad.hip) on P shards with 20-row halos reproduce the whole-
     sequence kernels (parallel/cp_fused.py's exchange, done here by slicing)."""
     from proteinbert_pytorch_replication_amd.ops import local_track as lt
