@@ -144,7 +144,11 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const int it = k * 8 + kb;
+#ifdef PBX_ABL_AFIX   // ablation builds only: 4 weight fragments reused (L1-resident) -- the L2 weight stream's cost
+      const bf16x8* fwk = fw + ((it + 3) & 3) * 256;
+#else
       const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
+#endif
       fr[(kb + 3) & 3] = fwk[lane];
       const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
 #pragma unroll

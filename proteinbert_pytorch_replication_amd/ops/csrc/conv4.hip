@@ -77,7 +77,11 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
       const_cast<bf16x8*>(ftw + cq * 64), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
   auto wfrag = [&](int it) {      // K-step it of 2 NI: narrow image for it < NI, then the wide one
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+#ifdef PBX_ABL_AFIX   // ablation builds only: 4 weight fragments reused (L1-resident) -- the L2 weight stream's cost
+    const int li = it & 3;
+#else
     const int li = it < NI ? it : it - NI;
+#endif
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(it < NI ? rn : rw, lane * 16, li * 4096, 0);
     return __builtin_bit_cast(bf16x8, v);
   };

@@ -33,6 +33,7 @@ constexpr int BM = 128;          // positions per tile
 constexpr int KS = 9;
 
 __device__ __attribute__((aligned(16))) unsigned int g_zero16[4];   // zero-initialised device global
+__device__ __attribute__((aligned(16))) unsigned int g_ones16[4] = {~0u, ~0u, ~0u, ~0u};   // token -1 (no token)
 
 // One 1-KiB LDS-DMA wave instruction: lane i's 16 source bytes land at lds_base + 16 i.  Issued as
 // inline asm so hipcc does not treat every later ds_read as a possible alias of the in-flight DMA
@@ -335,7 +336,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
     for (int i = w; i <= n0 + n1; i += 8) {
       if (i == n0 + n1) {                      // tokens pos0 .. pos0 + 127: 2 per lane (L even)
         const int p = pos0 + 2 * lane;
-        const void* src = p < L ? (const void*)(tok + (size_t)b * L + p) : (const void*)g_zero16;
+        const void* src = p < L ? (const void*)(tok + (size_t)b * L + p) : (const void*)g_ones16;
         glds16(src, buf + (rows0 + rows1) * 256);
         continue;
       }
@@ -357,6 +358,18 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
   for (int k = 0; k < KS; ++k) acc[k] = zero16();
   const int hal = cv ? hal1 : hal0;
   const int colb = ct * 32 + tc;
+  // per-lane B-fragment byte offsets at k-step 0: B[k = src][col = co] = dpre[src - s_k][co] of tap k is
+  // tile row hal + (4 - k) d + kb*16 + 8h + j; swz256's XOR depends on row & 15 only, so k-step kb adds
+  // kb * 4096 B (an immediate of the unrolled k-step loop) -- no per-read address arithmetic
+  const int cvb = cv ? rows0 * 256 : 0;
+  int boff[KS], boff4[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    const int rb = hal + (KS / 2 - k) * d + 8 * h + q;
+    boff[k] = cvb + swz256e(rb, colb);
+    boff4[k] = cvb + swz256e(rb + 4, colb);
+  }
+  const int toff = (rows0 + rows1) * 256 + 8 * h * 8;   // this lane's 8 source tokens (int64) at k-step 0
   if (t0 < t1) stage(t0, smem);
   for (long tile = t0; tile < t1; ++tile) {
     unsigned char* cur = smem + ((tile - t0) & 1) * buf_bytes;
@@ -366,49 +379,48 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
 #ifndef PBX_TOK_NOSTAGE   // ablation builds only (tools/ubench/build_flags.sh)
     if (tile + 1 < t1) stage(tile + 1, nxt);
 #endif
-    const int pos0 = (int)(tile - (tile / T) * T) * TBM;
-    const unsigned char* base = cur + (cv ? rows0 * 256 : 0);
-    const long long* ts = reinterpret_cast<const long long*>(cur + (rows0 + rows1) * 256);
-    // B[k = src][col = co] = dpre[src - s_k][co] of tap k: tile row hal + (4 - k) d + kb*16 + 8h + j
-    auto read_b = [&](int kb, bf16x8 (&fb)[KS]) {
-#pragma unroll
-      for (int k = 0; k < KS; ++k) {
-        const int rb = hal + (KS / 2 - k) * d + kb * 16 + 8 * h + q;
-        fb[k] = cat_tr(lds_tr(base, swz256e(rb, colb)), lds_tr(base, swz256e(rb + 4, colb)));
-      }
-    };
-    // A[i = v][k = src]: lane's token row v = r, sources kb*16 + 8h + j (positions >= L: no token)
-    auto onehot = [&](int kb) {
-      const uint4* tp = reinterpret_cast<const uint4*>(ts + kb * 16 + 8 * h);
-      const uint4 t0 = tp[0], t1 = tp[1], t2 = tp[2], t3 = tp[3];
-      const unsigned tv[8] = {t0.x, t0.z, t1.x, t1.z, t2.x, t2.z, t3.x, t3.z};
-      typedef __attribute__((ext_vector_type(8))) unsigned short u16x8;
-      u16x8 oh;
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        oh[j] = (pos0 + kb * 16 + 8 * h + j < L && tv[j] == (unsigned)r) ? (unsigned short)0x3F80 : (unsigned short)0;
-      return __builtin_bit_cast(bf16x8, oh);
-    };
-    // every LDS read of a K-step is issued before its 9 MFMAs (one exposed LDS latency per step, which
-    // the SIMD's other wave covers; a second fragment set for a one-step-ahead prefetch spills)
-#pragma unroll 1
-    for (int kb = 0; kb < TBM / 16; ++kb) {
-      bf16x8 fb[KS];
+    // (k-step kb, tap k) steps s = kb * 9 + k: the B fragment of step s + 2 is read while the MFMA of
+    // step s runs (3-slot ring); the one-hot A operand of k-step kb + 1 (A[i = v][k = src] = [tok == v],
+    // lane's v = r; positions >= L were staged as token -1) is built during taps 3..7 of k-step kb
+    constexpr int NS = (TBM / 16) * KS;
+    bf16x8 fb[3], fa[2];
+    unsigned tk[8];
+    auto read_b = [&](int st) {
+      const unsigned char* c = cur + (st / KS) * 4096;
 #ifdef PBX_TOK_NOLDS      // ablation builds only (tools/ubench/build_flags.sh): B fragments without LDS reads
-#pragma unroll
-      for (int k = 0; k < KS; ++k) fb[k] = __builtin_bit_cast(bf16x8, make_uint4(kb + k, lane, 0u, 0u));
+      fb[st % 3] = __builtin_bit_cast(bf16x8, make_uint4(st, lane, 0u, 0u));
 #else
-      read_b(kb, fb);
+      fb[st % 3] = cat_tr(lds_tr(c, boff[st % KS]), lds_tr(c, boff4[st % KS]));
 #endif
+    };
+    auto read_tok = [&](int kb) {
+      const unsigned* tp = reinterpret_cast<const unsigned*>(cur + toff + kb * 128);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) tk[j] = tp[2 * j];          // low words (tokens < 32, or -1)
+    };
+    auto make_a = [&](int kb) {
+      typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+      u32x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        o[e] = (tk[2 * e] == (unsigned)r ? 0x3F80u : 0u) | (tk[2 * e + 1] == (unsigned)r ? 0x3F800000u : 0u);
 #ifdef PBX_TOK_NOONEHOT   // ablation builds only: a constant A operand
-      const bf16x8 a = __builtin_bit_cast(bf16x8, make_uint4(0x3F80u * (unsigned)(r == kb), 0u, 0u, 0u));
-#else
-      const bf16x8 a = onehot(kb);
+      o = u32x4{0x3F80u * (unsigned)(r == kb), 0u, 0u, 0u};
 #endif
-      __builtin_amdgcn_sched_barrier(0);
+      fa[kb & 1] = __builtin_bit_cast(bf16x8, o);
+    };
+    read_tok(0);
+    make_a(0);
+    read_b(0);
+    read_b(1);
 #pragma unroll
-      for (int k = 0; k < KS; ++k) acc[k] = mfma32(a, fb[k], acc[k]);
+    for (int st = 0; st < NS; ++st) {
+      const int kb = st / KS, k = st % KS;
+      if (st + 2 < NS) read_b(st + 2);
+      if (k == 3 && kb + 1 < TBM / 16) read_tok(kb + 1);
+      if (k == 7 && kb + 1 < TBM / 16) make_a(kb + 1);
       __builtin_amdgcn_sched_barrier(0);
+      acc[k] = mfma32(fa[kb & 1], fb[st % 3], acc[k]);
     }
   }
   // slab [R][2][KS][V][128]: D row = token v, column = channel
