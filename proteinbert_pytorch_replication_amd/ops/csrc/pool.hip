@@ -13,7 +13,8 @@
 //     into a swizzled LDS image; a workgroup owns ONE 32-position tile and walks a group of samples, so
 //     the tile's [L, C] LayerNorm affine rows are staged into the remaining LDS once as well;
 //   * forward: s2 rows -> LN2 apply (fp32 affine from LDS) -> h2 (stored: block output) -> MFMA against
-//     Wv -> exact-erf GELU -> column sums, all in registers (no ln2_apply pass, no GELU' store);
+//     Wv -> GELU (logistic form fitted to the erf GELU, see PBX_POOL_GELU_FAST) -> column sums, all in
+//     registers (no ln2_apply pass, no GELU' store);
 //   * backward: h2 rows -> zT = Wv h2^T (MFMA) -> u = dv * GELU'(zT) on the VALU -> dh2^T += Wv^T u (MFMA).
 //     The D layout of zT (lane = position, rows 8 g + 4 h + e of a 32-row block) IS the B operand of the
 //     second product when its K order is permuted to {16 s + 8 (jj >> 2) + 4 h + (jj & 3)}, which the
@@ -63,25 +64,19 @@ __device__ __forceinline__ void pin8(float* a) {
   asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
 }
 
-// interleave of one pipelined column block: 8 MFMAs, each followed by one LDS fragment read and a share
-// of the previous block's ~240 GELU VALU instructions
+// GELU cores (measured on one box, B = 1024, L = 512, round 5; tools/ubench/pool_run3.sh):
+//   forward : A&S-erf 203-206 us | 2-term logistic (default, max |err| 2.9e-4, vpart rel 1.2e-4) 159 us |
+//             3-term logistic (2.9e-5) 177-182 us | no GELU at all (ablation) 114 us
+//   backward: A&S-erf GELU' 294-296 us | tanh-form GELU' (default, max |err| 8.7e-4, below the bf16 rounding
+//             of u = dv GELU') 275-279 us | no GELU' (ablation) 232 us
 #ifndef PBX_POOL_GELU_TANH
-#define PBX_POOL_GELU_TANH 0
+#define PBX_POOL_GELU_TANH 1
 #endif
-#ifndef PBX_POOL_SCHED
-#define PBX_POOL_SCHED 1
+#ifndef PBX_POOL_GELU_FAST
+#define PBX_POOL_GELU_FAST 1
 #endif
-#if PBX_POOL_SCHED
-#define POOL_FWD_SCHED()                                                           \
-  do {                                                                             \
-    _Pragma("unroll") for (int i_ = 0; i_ < 8; ++i_) {                             \
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                           \
-      __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                           \
-      __builtin_amdgcn_sched_group_barrier(0x002, 28, 0);                          \
-    }                                                                              \
-  } while (0)
-#else
-#define POOL_FWD_SCHED() do {} while (0)
+#ifndef PBX_ABL_NOGELU   // ablation builds only
+#define PBX_ABL_NOGELU 0
 #endif
 
 // sample range of workgroup row blockIdx.y
@@ -216,6 +211,52 @@ __global__ void __launch_bounds__(64 * NWV) pool_fwd_kernel(
       asm volatile("" : "+v"(cn));                                      \
       wf[kk] = lds_frag(nb, swz256(r, (kk) * 2 + h));                   \
       __builtin_amdgcn_sched_barrier(0);
+#if PBX_ABL_NOGELU   // ablation builds only: the column sums of x (no GELU) -- the VALU-free bound
+      float sm = 0.f;
+      POOL_MF(0) POOL_MF(1) POOL_MF(2) POOL_MF(3) POOL_MF(4) POOL_MF(5)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sm += x[i];
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(6)
+#elif PBX_POOL_GELU_FAST
+      // logistic form: GELU(x) ~ x sigma(x k(t)), t = x^2, fitted (minimax on [-14, 14]) to the exact erf GELU:
+      //   1: k = 1.59934 + 0.0696829 t                          max |err| 2.9e-4, 7 VALU per value
+      //   2: k = 1.59497 + 0.0739707 t - 6.93343e-4 t^2, t <= 49  max |err| 2.9e-5, 9 VALU per value
+      // evaluated as x / (1 + exp2(-log2(e) x k(t)))
+      POOL_MF(0)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) t[i] = x[i] * x[i];
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(1)
+#pragma unroll
+#if PBX_POOL_GELU_FAST == 2
+      for (int i = 0; i < 16; ++i) {
+        const float tt = fminf(t[i], 49.0f);
+        t[i] = fmaf(tt, fmaf(tt, 0.0010002823f, -0.10671716f), -2.3010488f) * x[i];
+      }
+#else
+      for (int i = 0; i < 16; ++i) t[i] = fmaf(t[i], -0.10053117f, -2.3073633f) * x[i];
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(2)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_exp2f(t[i]);
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(3)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) e[i] = __builtin_amdgcn_rcpf(e[i] + 1.0f);
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(4)
+      float sm = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm = fmaf(x[i], e[i], sm);
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(5)
+#pragma unroll
+      for (int i = 8; i < 16; ++i) sm = fmaf(x[i], e[i], sm);
+      __builtin_amdgcn_sched_barrier(0);
+      POOL_MF(6)
+#else
       POOL_MF(0)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
@@ -249,6 +290,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_fwd_kernel(
 #pragma unroll
       for (int i = 0; i < 16; ++i) sm += fmaf(fabsf(x[i]), pl[i], x[i] * 0.5f);   // GELU
       __builtin_amdgcn_sched_barrier(0);
+#endif
       POOL_MF(7)
 #undef POOL_MF
       sm += __shfl_xor(sm, 32, 64);
@@ -368,7 +410,24 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       bf16x8 bu0, bu1;
       // GELU' stages of the 8 values of 16-step s (regs 8 s .. 8 s + 7 of zo), Zelen-Severo form of
       // A&S 7.1.26: e = phi(x), Phi = 0.5 + sign(x) h, GELU' = Phi + x phi
-#if PBX_POOL_GELU_TANH
+#if PBX_ABL_NOGELU   // ablation builds only: u = dv x (no GELU') -- the VALU-free bound
+      auto stA = [&](int) {};
+      auto stB = [&]() {};
+      auto stC = [&]() {};
+      auto stD = [&]() {};
+      auto stE = [&](int s) {
+        float u[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const float4 d = dd[2 * s + (i >> 2)];
+          const float dj = (i & 3) == 0 ? d.x : (i & 3) == 1 ? d.y : (i & 3) == 2 ? d.z : d.w;
+          u[i] = zo[8 * s + i] * dj;
+        }
+        pin8(u);
+        return pack8(u);
+      };
+      (void)t; (void)e; (void)pl;
+#elif PBX_POOL_GELU_TANH
       // tanh-form GELU' (max |err| 8.7e-4 vs the erf form, below the bf16 rounding of u): sigma = 1 / (1 + e),
       // e = exp(-2 k(x)), k(x) = c (x + 0.044715 x^3); GELU' = sigma + x k'(x) 2 sigma (1 - sigma)
       auto stA = [&](int s) {

@@ -1,0 +1,82 @@
+"""GPU numerics of the recompute-form attention pool (csrc/pool.hip) against plain PyTorch fp32.
+
+Reference semantics (ProteinBERT/modules.py:49-60,87-92,162-164,214-219): the forward applies
+the second (L, C) LayerNorm and sums GELU(h2 Wv) over each 32-position tile; the backward recomputes GELU'
+from h2 and returns dh2 = dh2_in + (dv GELU'(h2 Wv)) Wv plus the LayerNorm-2 backward partials.  The
+kernels evaluate fitted GELU / GELU' cores (2-term logistic, max |err| 2.9e-4; tanh form, 8.7e-4): the
+oracle uses the exact erf forms, so the bounds below include that approximation.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from proteinbert_pytorch_replication_amd.ops import _lib
+from proteinbert_pytorch_replication_amd.ops import local_track  # noqa: F401  (registers the launchers)
+
+pytestmark = pytest.mark.gpu
+
+
+def _stats(s2f, L):
+    B = s2f.shape[0]
+    T2 = (L + 31) // 32
+    st2 = torch.empty(B, T2, 2, device=s2f.device)
+    for t in range(T2):
+        x = s2f[:, 32 * t:min(L, 32 * t + 32)].reshape(B, -1)
+        m = x.mean(1)
+        st2[:, t, 0] = m
+        st2[:, t, 1] = ((x - m[:, None]) ** 2).sum(1)
+    return st2
+
+
+def _gelu_d(z):
+    return 0.5 * (1 + torch.erf(z / 2 ** 0.5)) + z * torch.exp(-0.5 * z * z) / (2 * torch.pi) ** 0.5
+
+
+@pytest.mark.parametrize("B,L,NJ,tiles", [(2, 500, 512, False), (3, 64, 512, True), (5, 77, 256, False),
+                                          (1, 1000, 512, True)])
+def test_pool_kernels_vs_fp32(B, L, NJ, tiles):
+    """tiles: the vpart gradient per 32-position tile (dv_tiles = ceil(L/32)) instead of one row per sample."""
+    dev = torch.device("cuda")
+    st = _lib.stream_ptr(dev)
+    C = 128
+    torch.manual_seed(B * L + NJ)
+    TW = (L + 31) // 32
+    s2 = (torch.randn(B, L, C, device=dev) * 2 + 0.3).to(torch.bfloat16)
+    st2 = _stats(s2.float(), L)
+    g2 = torch.randn(L, C, device=dev) * 0.3 + 1
+    be2 = torch.randn(L, C, device=dev) * 0.2
+    wv = (torch.randn(NJ, C, device=dev) * 0.1).to(torch.bfloat16)
+    h2 = torch.empty_like(s2)
+    vpart = torch.empty(B, TW, NJ, device=dev)
+    _lib.call("pbx_pool_fwd", s2.data_ptr(), st2.data_ptr(), g2.data_ptr(), be2.data_ptr(), wv.data_ptr(),
+              h2.data_ptr(), vpart.data_ptr(), B, L, NJ, 1e-5, st)
+    x = s2.float()
+    m = x.mean((1, 2), keepdim=True)
+    v = ((x - m) ** 2).mean((1, 2), keepdim=True)
+    h2r = (x - m) / torch.sqrt(v + 1e-5) * g2 + be2
+    z = h2.float() @ wv.float().t()                                 # from the kernel's bf16 h2
+    pad = TW * 32 - L
+    vr = F.pad(F.gelu(z), (0, 0, 0, pad)).view(B, TW, 32, NJ).sum(2)
+    dh2_in = (torch.randn(B, L, C, device=dev) * 0.5).to(torch.bfloat16)
+    if tiles:
+        dv = torch.randn(B, TW, NJ, device=dev) * 0.1
+        dvp = dv.repeat_interleave(32, dim=1)[:, :L]               # per-position view of the tile rows
+    else:
+        dv = torch.randn(B, NJ, device=dev) * 0.1
+        dvp = dv[:, None, :]
+    dh2 = torch.empty_like(s2)
+    sums2 = torch.empty(B, TW, 2, device=dev)
+    _lib.call("pbx_pool_bwd", h2.data_ptr(), g2.data_ptr(), be2.data_ptr(), dh2_in.data_ptr(), dv.data_ptr(),
+              TW if tiles else 1, wv.data_ptr(), dh2.data_ptr(), sums2.data_ptr(), B, L, NJ, st)
+    torch.cuda.synchronize()
+    dr = dh2_in.float() + (_gelu_d(z) * dvp) @ wv.float()
+    sa = F.pad(dr * g2, (0, 0, 0, pad)).view(B, TW, 32, C).sum((2, 3))
+    sc = F.pad(dr * (h2.float() - be2), (0, 0, 0, pad)).view(B, TW, 32, C).sum((2, 3))
+    e_h = (h2.float() - h2r).abs().max().item()
+    e_v = ((vpart - vr).abs().max() / vr.abs().max()).item()
+    e_d = ((dh2.float() - dr).abs().max() / dr.abs().max()).item()
+    e_sa = ((sums2[..., 0] - sa).abs().max() / sa.abs().max()).item()
+    e_sc = ((sums2[..., 1] - sc).abs().max() / sc.abs().max()).item()
+    print(f"B={B} L={L} NJ={NJ}: h2 {e_h:.2e} vpart {e_v:.2e} dh2 {e_d:.2e} sums {e_sa:.2e} {e_sc:.2e}")
+    # observed on MI355X (round 5): h2 1.6e-2 (bf16 of |h2| ~ 8), vpart 1.2e-4, dh2 3.6e-3, sums 1.8e-3
+    assert e_h < 0.05 and e_v < 1e-3 and e_d < 1e-2 and e_sa < 1e-2 and e_sc < 1e-2
