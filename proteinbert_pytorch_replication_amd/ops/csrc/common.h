@@ -144,6 +144,41 @@ __device__ __forceinline__ void gelu_scalar_n(const f32x2* x, f32x2* g, f32x2* g
   }
 }
 
+// Fitted logistic GELU core: GELU(x) ~ x s, s = sigma(x k(t)), k(t) = 1.59934 + 0.0696829 t, t = x^2 (minimax
+// fit to the erf GELU on [-14, 14]: max |err| 2.9e-4 in GELU, 7.8e-4 in GELU' = s + x s (1 - s) (k + 2 t k1),
+// both below the bf16 rounding of the stored values), evaluated as s = 1 / (1 + exp2(-log2(e) x k(t))):
+// 7 VALU per GELU, 11 for GELU and GELU' together (the A&S erf form above: 14 / 15).  Saturates cleanly:
+// x -> -inf gives s = 0 (exp2 -> inf), x -> +inf gives s = 1.
+template <int N, int MODE>   // MODE 0: GELU, 1: GELU', 2: both (g and gd)
+__device__ __forceinline__ void gelu_logistic_n(const f32x2* x, f32x2* g, f32x2* gd) {
+  constexpr int M = 2 * N;
+  float xs[M], t[M], s[M];
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    xs[i] = (i & 1) ? x[i >> 1].y : x[i >> 1].x;
+    t[i] = xs[i] * xs[i];
+    s[i] = fmaf(t[i], -0.10053117f, -2.3073633f) * xs[i];      // -log2(e) x k(t)
+  }
+#pragma unroll
+  for (int i = 0; i < M; ++i) s[i] = __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(s[i]) + 1.0f);
+#pragma unroll
+  for (int i = 0; i < M; ++i) {
+    float gv = 0.f, dv = 0.f;
+    if (MODE != 1) gv = xs[i] * s[i];
+    if (MODE != 0) {
+      const float kd = fmaf(t[i], 0.20904868f, 1.59934236f);   // k + 2 t k1
+      dv = fmaf(xs[i] * fmaf(-s[i], s[i], s[i]), kd, s[i]);
+    }
+    if (i & 1) {
+      if (MODE != 1) g[i >> 1].y = gv;
+      if (MODE != 0) gd[i >> 1].y = dv;
+    } else {
+      if (MODE != 1) g[i >> 1].x = gv;
+      if (MODE != 0) gd[i >> 1].x = dv;
+    }
+  }
+}
+
 // N independent pairs evaluated stage by stage (every stage of all N before the next): the
 // one-pair forms above compile to a serial dependency chain with an s_nop between dependent packed
 // ops; N interleaved chains fill those slots and the transcendental latencies.
@@ -152,6 +187,11 @@ __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
 #ifdef PBX_ABL_NOGELU   // ablation builds only (tools/ubench/build_flags.sh): the cost of the GELU chains
 #pragma unroll
   for (int i = 0; i < N; ++i) out[i] = x[i] * 0.5f;
+  return;
+#endif
+#ifndef PBX_GELU_ERF   // default: the fitted logistic core (A/B builds with -DPBX_GELU_ERF keep the erf forms)
+  if (GRAD) gelu_logistic_n<N, 1>(x, nullptr, out);
+  else gelu_logistic_n<N, 0>(x, out, nullptr);
   return;
 #endif
 #ifdef PBX_SCALAR_GELU
@@ -214,6 +254,10 @@ __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd
     g[i] = x[i] * 0.5f;
     gd[i] = x[i] * 0.25f;
   }
+  return;
+#endif
+#ifndef PBX_GELU_ERF
+  gelu_logistic_n<N, 2>(x, g, gd);
   return;
 #endif
 #ifdef PBX_SCALAR_GELU

@@ -216,25 +216,18 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       gi[e] = (f32x2){pn[2 * e], pn[2 * e + 1]};
       gi[4 + e] = (f32x2){pw[2 * e], pw[2 * e + 1]};
     }
-    // scalar A&S stages (gelu_scalar_n): this epilogue runs beside the other waves' MFMAs, where the
-    // packed form measured 3 % slower on the kernel.  Training: GELU AND GELU' from one shared core
-    // (+2 VALU per value); GELU' is what the data gradient multiplies by, so it is stored instead of the
-    // pre-activation and the data gradient no longer evaluates a GELU' core per value (~14 VALU + 2
-    // transcendentals, on 1.2x the values for the halo rows)
-#ifdef PBX_CONV_PRE   // ablation: store the pre-activation, the data gradient evaluates GELU' (round-3 form)
-    if (STORE && ok) {
-      *reinterpret_cast<uint4*>(pre_n + off) = pnq;
-      *reinterpret_cast<uint4*>(pre_w + off) = pwq;
-    }
-    if (true) {
-      gelu_scalar_n<4, 0>(gi, go, nullptr);
-      gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
-    } else
+    // scalar GELU stages: this epilogue runs beside the other waves' MFMAs, where packed-fp32 forms measured
+    // slower.  Training: GELU AND GELU' from one shared core; GELU' is what the data gradient multiplies by,
+    // so it is stored instead of the pre-activation and the data gradient evaluates no GELU' core
+#ifdef PBX_GELU_ERF   // A/B builds only: the A&S erf core (15 VALU per GELU + GELU', 14 per GELU)
+#define CONV_GELU gelu_scalar_n
+#else                       // fitted logistic core (common.h: 11 / 7 VALU, |err| <= 7.8e-4 / 2.9e-4)
+#define CONV_GELU gelu_logistic_n
 #endif
     if constexpr (STORE) {
       f32x2 gd[8];
-      gelu_scalar_n<4, 2>(gi, go, gd);
-      gelu_scalar_n<4, 2>(gi + 4, go + 4, gd + 4);
+      CONV_GELU<4, 2>(gi, go, gd);
+      CONV_GELU<4, 2>(gi + 4, go + 4, gd + 4);
       float dn[8], dw[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -248,9 +241,10 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
         *reinterpret_cast<uint4*>(pre_w + off) = packq8(dw);
       }
     } else {
-      gelu_scalar_n<4, 0>(gi, go, nullptr);
-      gelu_scalar_n<4, 0>(gi + 4, go + 4, nullptr);
+      CONV_GELU<4, 0>(gi, go, nullptr);
+      CONV_GELU<4, 0>(gi + 4, go + 4, nullptr);
     }
+#undef CONV_GELU
     float o[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {

@@ -50,10 +50,10 @@ __device__ __forceinline__ void stage_rows(unsigned char* dst, const bf16_t* __r
 __device__ __forceinline__ int aff_off(int pos, int chunk) {   // float offset; chunk = ch / 4 (0..31)
   return pos * CH + ((chunk ^ (pos & 15)) << 2);
 }
-// bf16 [32 pos][128 ch] affine image, 8-B units XOR-swizzled by pos: a ds_read_b64 lane group (32
-// positions, one unit) hits 32 distinct bank pairs
-__device__ __forceinline__ int affx_off(int pos, int unit) {   // bf16 offset; unit = ch / 4 (0..31)
-  return pos * CH + ((unit ^ pos) << 2);
+// bf16 [32 pos][128 ch] affine image, 16-B units (8 channels) XOR-swizzled by (pos & 15): a ds_read_b128
+// lane group (16 positions, one unit) hits 16 distinct bank quads
+__device__ __forceinline__ int affy_off(int pos, int unit4) {   // bf16 offset of 4-channel unit (0..31)
+  return pos * CH + ((((unit4 >> 1) ^ (pos & 15)) << 3) | ((unit4 & 1) << 2));
 }
 
 __device__ __forceinline__ float4 lds_f4(const float* p) { return *reinterpret_cast<const float4*>(p); }
@@ -77,6 +77,9 @@ __device__ __forceinline__ void pin8(float* a) {
 #endif
 #ifndef PBX_ABL_NOGELU   // ablation builds only
 #define PBX_ABL_NOGELU 0
+#endif
+#ifdef PBX_STAMPS       // instrumented builds only (-DPBX_STAMPS)
+__device__ unsigned long long pbx_pool_stamps[256 * 64 * 8 * 4];   // [workgroup][wave][wait, loop, epi, n]
 #endif
 
 // sample range of workgroup row blockIdx.y
@@ -346,7 +349,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
     const float* src = (which ? be2 : g2) + (size_t)min(p, L - 1) * CH + unit * 4;
     const float4 v = *reinterpret_cast<const float4*>(src);
     const float vv[4] = {v.x, v.y, v.z, v.w};
-    *reinterpret_cast<uint2*>(affh + which * TP * CH + affx_off(pr, unit)) = packq4(vv);
+    *reinterpret_cast<uint2*>(affh + which * TP * CH + affy_off(pr, unit)) = packq4(vv);
   }
   // Wv^T fragment offsets (transposed reads) at 16-step 0; step i adds 16 i rows = 4096 i bytes
   int woff[4], woff8[4];
@@ -376,7 +379,15 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       dvr[k] = *reinterpret_cast<const float4*>(dv + ((size_t)bb * dv_tiles + dv_tile) * NJ + 256 * k + 4 * lane);
   };
   load_item(b);
+#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/poolstamps.py): per-wave phase cycle totals
+  unsigned long long st_wait = 0, st_loop = 0, st_epi = 0, st_n = 0;
+#endif
   for (; b < b1; b += NWV) {
+#ifdef PBX_STAMPS
+    const unsigned long long s0 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long s1 = __builtin_amdgcn_s_memtime();
+#endif
     bf16x8 hf[8];
     const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
 #pragma unroll
@@ -548,26 +559,21 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       bstep(z1, z0, jt, jt + 1, true);
       bstep(z0, z1, jt + 1, jt + 2, true);
     }
-    uint2 dq[4][4];      // epilogue operand: in flight during the last two blocks
+    // epilogue operand dh2_in in the B-fragment channel layout (lane (r, h): channels 16 K + 8 h + 0..7), loads
+    // in flight during the last two blocks
+    uint2 dq[16];        // (8-B loads: 16-B ones need aligned register quads, which spill here)
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) dq[ct][g] = *reinterpret_cast<const uint2*>(dsrc + roff + ct * 32 + 8 * g + 4 * h);
+    for (int q = 0; q < 16; ++q) dq[q] = *reinterpret_cast<const uint2*>(dsrc + roff + 16 * (q >> 1) + 8 * h + 4 * (q & 1));
     bstep(z1, z0, NJT - 2, NJT - 1, true);
     bstep(z0, z1, NJT - 1, NJT - 1, false);
+#ifdef PBX_STAMPS
+    const unsigned long long s2 = __builtin_amdgcn_s_memtime();
+#endif
     load_item(min(b + NWV, b1 - 1));                 // next item: in flight during the epilogue
-    // h2 in the accumulator layout: lane (r, h) needs channels 16 K + 8 H + 4 h + (0..3) for both H; its
-    // B fragments hold 16 K + 8 h + (0..7).  Exchange with the partner lane r ^ 32: each sends the half
-    // the other needs (h = 0: its upper 4 channels, h = 1: its lower 4).  Afterwards the (x, y) dwords
-    // of hv[K] hold H = 0, (z, w) hold H = 1.
-    uint4 hv[8];
-#pragma unroll
-    for (int kk = 0; kk < 8; ++kk) {
-      const uint4 o = __builtin_bit_cast(uint4, hf[kk]);   // zero past L
-      const unsigned s0 = h ? o.x : o.z, s1 = h ? o.y : o.w;
-      const unsigned r0 = (unsigned)__shfl_xor((int)s0, 32, 64), r1 = (unsigned)__shfl_xor((int)s1, 32, 64);
-      hv[kk] = h ? make_uint4(r0, r1, o.z, o.w) : make_uint4(o.x, o.y, r0, r1);
-    }
+    // dh2^T in the B-fragment layout too: y[ct][4 g + e] is channel ct*32 + 8 g + 4 h + e; a permlane32 swap
+    // of the (g, g + 1) registers leaves lane half h with g = 2 m + h of both halves, i.e. channels
+    // ct*32 + 16 m + 8 h + {e, 4 + e}.  Then h2 is hf itself, and dh2_in / dh2 / the affine rows move as
+    // 16-B rows (8 buffer_store_b128 per lane instead of 16 b64: the store issue was the epilogue's bound)
     int rh = r;                                  // opaque: keeps the affine LDS addresses inside the loop
     asm volatile("" : "+v"(rh));
     const bf16_t* gamh = affh + rh * CH;
@@ -576,32 +582,50 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
         __builtin_amdgcn_make_buffer_rsrc(dh2 + (size_t)b * L * CH, (short)0, L * CH * 2, 0x00020000);
     float sa = 0.f, sc = 0.f;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct) {
+    for (int kk = 0; kk < 8; ++kk) {
+      const int ct = kk >> 1, m = kk & 1;
+      float o[8], din[8], hh[8], gg[8], bb[8];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c0 = ct * 32 + 8 * g + 4 * h;             // channels c0 .. c0 + 3 = affine unit c0 / 4
-        const int K = 2 * ct + (g >> 1), H = g & 1;
-        const uint2 hq2 = H ? make_uint2(hv[K].z, hv[K].w) : make_uint2(hv[K].x, hv[K].y);
-        const int uo = (((c0 >> 2) ^ rh) & 31) << 2;
-        float din[4], hh[4], gg[4], bb[4], o[4];
-        unpack4(dq[ct][g], din);
-        unpack4(hq2, hh);
-        unpack4(*reinterpret_cast<const uint2*>(gamh + uo), gg);
-        unpack4(*reinterpret_cast<const uint2*>(beth + uo), bb);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = bfround(fmaf(din[e], dmask, y[ct][4 * g + e]));
-          sa = fmaf(o[e], gg[e], sa);
-          sc = fmaf(o[e], hh[e] - bb[e], sc);
-        }
-        const uint2 oq = packq4(o);
-        __builtin_amdgcn_raw_buffer_store_b64((u32x2){oq.x, oq.y}, dr, vo + 8 * h, (ct * 32 + 8 * g) * 2, 0);
+      for (int e = 0; e < 4; ++e) {
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(y[ct][8 * m + e]),
+                                                         __float_as_uint(y[ct][8 * m + 4 + e]), false, false);
+        o[e] = __uint_as_float(sw[0]);
+        o[4 + e] = __uint_as_float(sw[1]);
       }
+      const int uo = (((2 * kk + h) ^ (rh & 15)) << 3);         // 16-B unit 2 kk + h of row rh (affy layout)
+      unpack4(dq[2 * kk], din);
+      unpack4(dq[2 * kk + 1], din + 4);
+      unpack8(__builtin_bit_cast(uint4, hf[kk]), hh);             // zero past L
+      unpack8(*reinterpret_cast<const uint4*>(gamh + uo), gg);
+      unpack8(*reinterpret_cast<const uint4*>(beth + uo), bb);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        o[e] = bfround(fmaf(din[e], dmask, o[e]));
+        sa = fmaf(o[e], gg[e], sa);
+        sc = fmaf(o[e], hh[e] - bb[e], sc);
+      }
+      const uint4 oq = packq8(o);
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){oq.x, oq.y, oq.z, oq.w}, dr, vo + 16 * h, kk * 32, 0);
+      __builtin_amdgcn_sched_barrier(0);   // one 16-B row at a time (hoisted affine reads of all 8 spill)
     }
     sa = wave_reduce_sum(ok ? sa : 0.f);
     sc = wave_reduce_sum(ok ? sc : 0.f);
     if (lane == 0) *reinterpret_cast<float2*>(sums2 + ((size_t)b * TW + tp) * 2) = make_float2(sa, sc);
+#ifdef PBX_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long s3 = __builtin_amdgcn_s_memtime();
+    st_wait += s1 - s0;
+    st_loop += s2 - s1;
+    st_epi += s3 - s2;
+    ++st_n;
+#endif
   }
+#ifdef PBX_STAMPS
+  if (lane == 0) {
+    unsigned long long* o = pbx_pool_stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NWV + w) * 4;
+    o[0] = st_wait; o[1] = st_loop; o[2] = st_epi; o[3] = st_n;
+  }
+#endif
 }
 
 bool pool_attrs_set = false;
@@ -661,3 +685,9 @@ PBX_EXPORT int pbx_pool_bwd(const void* h2, const float* g2, const float* be2, c
                      (const bf16_t*)dh2_in, dv, dv_tiles, (const bf16_t*)wv, (bf16_t*)dh2, sums2, B, L);
   return pbx_launch_status();
 }
+
+#ifdef PBX_STAMPS
+PBX_EXPORT int pbx_pool_stamps_read(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_pool_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif

@@ -221,3 +221,13 @@ def collective_stream(device: torch.device):
         comm.wait_stream(_streams[(idx, name)])
     with torch.cuda.stream(comm):
         yield
+
+
+def join_collectives(device: torch.device) -> None:
+    """Current stream waits for the communication stream of :func:`collective_stream` (its non-finite flag
+    kernels; the collectives themselves are joined by ``work.wait()``).  Under hipGraph capture every stream
+    forked into the capture must rejoin the capturing stream before the capture ends."""
+    s = _streams.get((_idx(device), "comm"))
+    if s is not None:
+        _wait(torch.cuda.current_stream(_idx(device)), s)
+

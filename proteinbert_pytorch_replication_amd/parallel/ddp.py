@@ -226,6 +226,8 @@ class BucketedAllReduce:
         self._next = len(self.buckets)
         for b in range(len(self.buckets)):
             self._land(b)
+        if self.arena.grad.is_cuda:
+            streams.join_collectives(self.arena.grad.device)
         if average:
             self.arena.grad.div_(self.world)
         self.start_step()
@@ -270,6 +272,8 @@ class BucketedAllReduce:
                 # (the head's was already committed), so no Inf / NaN ever reaches the parameters
                 opt.skip_flag = torch.maximum(skip, self._post_flag(split, self.arena.numel))
             opt.step_range(split, self.arena.numel)
+        if self.arena.grad.is_cuda:
+            streams.join_collectives(self.arena.grad.device)
         self.track_nonfinite = False
         self._flag_work = None
         self.start_step()

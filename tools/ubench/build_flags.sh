@@ -4,7 +4,7 @@
 # usage: tools/ubench/build_flags.sh <name> [hipcc flags...]
 set -e
 name=$1; shift
-src=proteinbert_pytorch_replication_amd/ops/csrc
+src=${SRC:-proteinbert_pytorch_replication_amd/ops/csrc}
 d=$(mktemp -d)
 mkdir -p tools/ubench/abl
 objs=""
