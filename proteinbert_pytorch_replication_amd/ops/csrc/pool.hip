@@ -64,6 +64,58 @@ __device__ __forceinline__ void pin8(float* a) {
   asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
 }
 
+// Backward operand type: PBX_POOL_F16 (default) runs both backward GEMMs on v_mfma_f32_32x32x16_f16 with an f16
+// Wv image, so GELU' is evaluated on packed-f16 VALU (v_pk_* f16: two values per ~4-cycle issue slot instead of
+// one per fp32 instruction) and u = dv GELU' is the f16 B operand as it stands.  dv is scaled per sample by a
+// power of two (max |dv| -> [0.5, 1)) so u stays in the f16 normal range; the epilogue undoes it exactly.
+#ifndef PBX_POOL_F16
+#define PBX_POOL_F16 1
+#endif
+typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+#if PBX_POOL_F16
+typedef __attribute__((ext_vector_type(8))) _Float16 opx8;
+__device__ __forceinline__ f32x16_t mfma_b(const opx8& a, const opx8& b, const f32x16_t& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+#else
+typedef bf16x8 opx8;
+__device__ __forceinline__ f32x16_t mfma_b(const opx8& a, const opx8& b, const f32x16_t& c) { return mfma32(a, b, c); }
+#endif
+__device__ __forceinline__ opx8 as_op(const bf16x8& v) { return __builtin_bit_cast(opx8, v); }
+__device__ __forceinline__ opx8 as_op(const uint4& v) { return __builtin_bit_cast(opx8, v); }
+// 8 bf16 -> 8 f16 (RNE; exact for |x| in [6.1e-5, 65504], the range of the pool's operands)
+__device__ __forceinline__ uint4 bf16x8_to_f16x8(const uint4& q) {
+  float v[8];
+  unpack8(q, v);
+  uint4 o;
+  unsigned* ow = reinterpret_cast<unsigned*>(&o);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) ow[i] = __builtin_bit_cast(unsigned, (h2_t){(_Float16)v[2 * i], (_Float16)v[2 * i + 1]});
+  return o;
+}
+__device__ __forceinline__ h2_t h2_of(unsigned u) { return __builtin_bit_cast(h2_t, u); }
+__device__ __forceinline__ unsigned u_of(h2_t v) { return __builtin_bit_cast(unsigned, v); }
+// exp2 / rcp of 4 f16 pairs: the low halves, then the high halves by SDWA into WORD_1 with the low half
+// preserved -- no v_pack per pair, and every transcendental's result is read >= 3 instructions later (the
+// trailing s_nop covers the last ones for the instruction after the block: trans-forwarding hazard)
+#define PBX_TRANS_H4(OP, x)                                                                                 \
+  do {                                                                                                      \
+    unsigned i0_ = u_of(x[0]), i1_ = u_of(x[1]), i2_ = u_of(x[2]), i3_ = u_of(x[3]), o0_, o1_, o2_, o3_;  \
+    asm volatile(OP "_e32 %0, %4\n\t" OP "_e32 %1, %5\n\t" OP "_e32 %2, %6\n\t" OP "_e32 %3, %7\n\t"           \
+                 OP "_sdwa %0, %4 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"            \
+                 OP "_sdwa %1, %5 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"            \
+                 OP "_sdwa %2, %6 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"            \
+                 OP "_sdwa %3, %7 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_1\n\t"            \
+                 "s_nop 0"                                                                                  \
+                 : "=&v"(o0_), "=&v"(o1_), "=&v"(o2_), "=&v"(o3_)                                            \
+                 : "v"(i0_), "v"(i1_), "v"(i2_), "v"(i3_));                                                 \
+    x[0] = h2_of(o0_); x[1] = h2_of(o1_); x[2] = h2_of(o2_); x[3] = h2_of(o3_);                             \
+  } while (0)
+
+__device__ __forceinline__ void pinh4(h2_t* a) {
+  asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
+}
+
 // GELU cores (measured on one box, B = 1024, L = 512, round 5; tools/ubench/pool_run3.sh):
 //   forward : A&S-erf 203-206 us | 2-term logistic (default, max |err| 2.9e-4, vpart rel 1.2e-4) 159 us |
 //             3-term logistic (2.9e-5) 177-182 us | no GELU at all (ablation) 114 us
@@ -342,7 +394,13 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
   const int TW = gridDim.x;
   int b0, b1;
   sample_range(B, b0, b1);
+#if PBX_POOL_F16
+  stage_chunks(
+      NJ * 16, [&](int idx) { return bf16x8_to_f16x8(*reinterpret_cast<const uint4*>(wv + (size_t)idx * 8)); },
+      [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(ws + swz256(idx >> 4, idx & 15)) = v; });
+#else
   stage_rows(ws, wv, NJ);
+#endif
   for (int i = tid; i < 2 * TP * 32; i += 64 * NWV) {
     const int which = i >> 10, pr = (i >> 5) & 31, unit = i & 31;
     const int p = p0 + pr;
@@ -388,12 +446,37 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned long long s1 = __builtin_amdgcn_s_memtime();
 #endif
-    bf16x8 hf[8];
+    opx8 hf[8];
     const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
+#if PBX_POOL_F16
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) hf[kk] = __builtin_bit_cast(bf16x8, ok ? hq[kk] : zq);
+    for (int kk = 0; kk < 8; ++kk) {
+      u32x4 c = __builtin_bit_cast(u32x4, bf16x8_to_f16x8(ok ? hq[kk] : zq));
+      asm volatile("" : "+v"(c));     // materialised here: sunk into the loop it would keep hq live (spills)
+      hf[kk] = __builtin_bit_cast(opx8, c);
+    }
+    // this sample's dv row as f16 pairs, scaled by 2^-ex so that max |dv| lands in [0.5, 1)
+    float dvmax = 0.f;
+#pragma unroll
+    for (int k = 0; k < NJ / 256; ++k)
+      dvmax = fmaxf(dvmax, fmaxf(fmaxf(fabsf(dvr[k].x), fabsf(dvr[k].y)), fmaxf(fabsf(dvr[k].z), fabsf(dvr[k].w))));
+    dvmax = wave_reduce_max(dvmax);
+    const int dvex = dvmax > 0.f ? __builtin_amdgcn_frexp_expf(dvmax) : 0;
+    const float dvscale = ldexpf(1.0f, -dvex), dvinv = ldexpf(1.0f, dvex);
+#pragma unroll
+    for (int k = 0; k < NJ / 256; ++k) {
+      const float4 d = dvr[k];
+      *reinterpret_cast<uint2*>(reinterpret_cast<unsigned*>(dvs) + 128 * k + 2 * lane) =
+          make_uint2(u_of(__builtin_bit_cast(h2_t, __builtin_amdgcn_cvt_pkrtz(d.x * dvscale, d.y * dvscale))),
+                     u_of(__builtin_bit_cast(h2_t, __builtin_amdgcn_cvt_pkrtz(d.z * dvscale, d.w * dvscale))));
+    }
+#else
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) hf[kk] = as_op(ok ? hq[kk] : zq);
 #pragma unroll
     for (int k = 0; k < NJ / 256; ++k) *reinterpret_cast<float4*>(dvs + 256 * k + 4 * lane) = dvr[k];
+    constexpr float dvinv = 1.0f;
+#endif
     const size_t roff = ((size_t)b * L + pc) * CH;
     f32x16_t y[4];
 #pragma unroll
@@ -405,23 +488,82 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       const unsigned char* ab = ws + jn * 32 * 256;
       const unsigned char* w0 = ws + 4096 * (2 * jt);
       const unsigned char* w1 = w0 + 4096;
+#if PBX_POOL_F16
+      // dv of this lane's rows j = 32 jt + 8 i + 4 h + (0..3), i = 0..3: f16 pairs (j, j + 1)
+      const unsigned* dvjh = reinterpret_cast<const unsigned*>(dvs) + jt * 16 + 2 * h;
+      const uint2 ddh[4] = {*reinterpret_cast<const uint2*>(dvjh), *reinterpret_cast<const uint2*>(dvjh + 4),
+                            *reinterpret_cast<const uint2*>(dvjh + 8), *reinterpret_cast<const uint2*>(dvjh + 12)};
+#else
       const float* dvj = dvs + jt * 32 + 4 * h;
       const float4 dd[4] = {*reinterpret_cast<const float4*>(dvj), *reinterpret_cast<const float4*>(dvj + 8),
                             *reinterpret_cast<const float4*>(dvj + 16), *reinterpret_cast<const float4*>(dvj + 24)};
-      bf16x8 fa[8], fb[4], fc[4];
+#endif
+      opx8 fa[8], fb[4], fc[4];
       auto tr = [&](const unsigned char* wsi, int ct) {
-        return cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct]));
+        return as_op(cat_tr(lds_tr(wsi, woff[ct]), lds_tr(wsi, woff8[ct])));
       };
       if (next) {
-        fa[0] = lds_frag(ab, swz256(r, h));
-        fa[1] = lds_frag(ab, swz256(r, 2 + h));
+        fa[0] = as_op(lds_frag(ab, swz256(r, h)));
+        fa[1] = as_op(lds_frag(ab, swz256(r, 2 + h)));
       }
       zn = zero16();
+      opx8 bu0, bu1;
+#if !PBX_POOL_F16
       float t[8], e[8], pl[8];
-      bf16x8 bu0, bu1;
+#endif
       // GELU' stages of the 8 values of 16-step s (regs 8 s .. 8 s + 7 of zo), Zelen-Severo form of
       // A&S 7.1.26: e = phi(x), Phi = 0.5 + sign(x) h, GELU' = Phi + x phi
-#if PBX_ABL_NOGELU   // ablation builds only: u = dv x (no GELU') -- the VALU-free bound
+#if PBX_POOL_F16
+      // logistic GELU' (common.h gelu_logistic_n constants) on packed f16, 4 pairs (j, j + 1) per 16-step s:
+      //   s = 1 / (1 + exp2(x (C0 + C1 t))), t = min(x^2, 64), GELU' = s + x s (1 - s) (K0 + K1 t)
+      // (t is clamped so that 0 * inf cannot occur at |x| >= 256; at |x| >= 8 s is saturated anyway)
+      h2_t xh[4], th[4], eh[4], kh[4];
+      // each stage runs one operation over the 4 independent pairs before the next (a dependent packed-f16
+      // op right after its producer costs an s_nop)
+      auto stA = [&](int s) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          xh[k] = __builtin_bit_cast(h2_t, __builtin_amdgcn_cvt_pkrtz(zo[8 * s + 2 * k], zo[8 * s + 2 * k + 1]));
+#pragma unroll
+        for (int k = 0; k < 4; ++k) th[k] = xh[k] * xh[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) th[k] = __builtin_elementwise_min(th[k], (h2_t){64.0f16, 64.0f16});
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eh[k] = th[k] * (h2_t){-0.10053117f16, -0.10053117f16} + (h2_t){-2.3073633f16, -2.3073633f16};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eh[k] = eh[k] * xh[k];
+        pinh4(xh);
+        pinh4(th);
+        pinh4(eh);
+      };
+      auto stB = [&]() { PBX_TRANS_H4("v_exp_f16", eh); };
+      auto stC = [&]() {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) eh[k] = eh[k] + (h2_t){1.0f16, 1.0f16};
+        PBX_TRANS_H4("v_rcp_f16", eh);
+      };
+      auto stD = [&]() {   // x (K0 + K1 t)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kh[k] = th[k] * (h2_t){0.20904868f16, 0.20904868f16} + (h2_t){1.5993424f16, 1.5993424f16};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kh[k] = kh[k] * xh[k];
+        pinh4(kh);
+      };
+      auto stE = [&](int s) {
+        h2_t s1[4], u[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) s1[k] = eh[k] - eh[k] * eh[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) u[k] = kh[k] * s1[k] + eh[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint2 dq2 = ddh[2 * s + (k >> 1)];
+          u[k] = u[k] * h2_of((k & 1) ? dq2.y : dq2.x);
+        }
+        pinh4(u);
+        return as_op(make_uint4(u_of(u[0]), u_of(u[1]), u_of(u[2]), u_of(u[3])));
+      };
+#elif PBX_ABL_NOGELU   // ablation builds only: u = dv x (no GELU') -- the VALU-free bound
       auto stA = [&](int) {};
       auto stB = [&]() {};
       auto stC = [&]() {};
@@ -435,7 +577,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
           u[i] = zo[8 * s + i] * dj;
         }
         pin8(u);
-        return pack8(u);
+        return as_op(pack8(u));
       };
       (void)t; (void)e; (void)pl;
 #elif PBX_POOL_GELU_TANH
@@ -478,7 +620,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
           u[i] = fmaf(x * pl[i], s1, sg) * dj;
         }
         pin8(u);
-        return pack8(u);
+        return as_op(pack8(u));
       };
 #else
       auto stA = [&](int s) {
@@ -523,14 +665,14 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
           u[i] = fmaf(x, e[i], Phi) * dj;
         }
         pin8(u);
-        return pack8(u);
+        return as_op(pack8(u));
       };
 #endif
 #define SB __builtin_amdgcn_sched_barrier(0);
 // the empty volatile asm pins each MFMA into its group (MFMA nodes carry no chain, so the DAG scheduler
 // would otherwise cluster them in front of the first sched_barrier)
 #define PIN(v) asm volatile("" : "+v"(v));
-#define G1(k) if (next) { zn = mfma32(fa[k], hf[k], zn); PIN(zn) if ((k) + 2 < 8) fa[(k) + 2] = lds_frag(ab, swz256(r, 2 * ((k) + 2) + h)); }
+#define G1(k) if (next) { zn = mfma_b(fa[k], hf[k], zn); PIN(zn) if ((k) + 2 < 8) fa[(k) + 2] = as_op(lds_frag(ab, swz256(r, 2 * ((k) + 2) + h))); }
       SB
       G1(0) stA(0); SB
       G1(1) stB(); SB
@@ -540,12 +682,12 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       G1(5) stA(1); SB
       G1(6) stB(); fb[2] = tr(w0, 2); SB
       G1(7) stC(); fb[3] = tr(w0, 3); SB
-      y[0] = mfma32(fb[0], bu0, y[0]); PIN(y[0]) fc[0] = tr(w1, 0); stD(); SB
-      y[1] = mfma32(fb[1], bu0, y[1]); PIN(y[1]) fc[1] = tr(w1, 1); SB
-      y[2] = mfma32(fb[2], bu0, y[2]); PIN(y[2]) fc[2] = tr(w1, 2); bu1 = stE(1); SB
-      y[3] = mfma32(fb[3], bu0, y[3]); PIN(y[3]) fc[3] = tr(w1, 3); SB
+      y[0] = mfma_b(fb[0], bu0, y[0]); PIN(y[0]) fc[0] = tr(w1, 0); stD(); SB
+      y[1] = mfma_b(fb[1], bu0, y[1]); PIN(y[1]) fc[1] = tr(w1, 1); SB
+      y[2] = mfma_b(fb[2], bu0, y[2]); PIN(y[2]) fc[2] = tr(w1, 2); bu1 = stE(1); SB
+      y[3] = mfma_b(fb[3], bu0, y[3]); PIN(y[3]) fc[3] = tr(w1, 3); SB
 #pragma unroll
-      for (int ct = 0; ct < 4; ++ct) y[ct] = mfma32(fc[ct], bu1, y[ct]);
+      for (int ct = 0; ct < 4; ++ct) y[ct] = mfma_b(fc[ct], bu1, y[ct]);
       SB
 #undef G1
 #undef PIN
@@ -553,7 +695,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
     };
     f32x16_t z0 = zero16(), z1;
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) z0 = mfma32(lds_frag(ws, swz256(r, kk * 2 + h)), hf[kk], z0);
+    for (int kk = 0; kk < 8; ++kk) z0 = mfma_b(as_op(lds_frag(ws, swz256(r, kk * 2 + h))), hf[kk], z0);
 #pragma unroll 1
     for (int jt = 0; jt < NJT - 2; jt += 2) {
       bstep(z1, z0, jt, jt + 1, true);
@@ -595,12 +737,25 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       const int uo = (((2 * kk + h) ^ (rh & 15)) << 3);         // 16-B unit 2 kk + h of row rh (affy layout)
       unpack4(dq[2 * kk], din);
       unpack4(dq[2 * kk + 1], din + 4);
+#if PBX_POOL_F16
+      {
+        const uint4 hb = __builtin_bit_cast(uint4, hf[kk]);     // zero past L
+        const unsigned hw[4] = {hb.x, hb.y, hb.z, hb.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const h2_t v = h2_of(hw[i]);
+          hh[2 * i] = (float)v.x;
+          hh[2 * i + 1] = (float)v.y;
+        }
+      }
+#else
       unpack8(__builtin_bit_cast(uint4, hf[kk]), hh);             // zero past L
+#endif
       unpack8(*reinterpret_cast<const uint4*>(gamh + uo), gg);
       unpack8(*reinterpret_cast<const uint4*>(beth + uo), bb);
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        o[e] = bfround(fmaf(din[e], dmask, o[e]));
+        o[e] = bfround(fmaf(din[e], dmask, o[e] * dvinv));
         sa = fmaf(o[e], gg[e], sa);
         sc = fmaf(o[e], hh[e] - bb[e], sc);
       }
