@@ -26,6 +26,9 @@ typedef unsigned short bf16_t;
 namespace {
 constexpr int CH = 128;
 constexpr int BM = 128;               // positions per workgroup
+#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/convstamps.py)
+__device__ unsigned long long pbx_conv_stamps[4096 * 8 * 4];   // [workgroup][wave][stage, loop, epilogue, t0]
+#endif
 constexpr int FRAG = 64 * 8;          // bf16 per packed fragment (64 lanes x 8)
 constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging tile
 
@@ -72,6 +75,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   unsigned char* ot = smem + XR * 256;                        // [TBM][128] bf16 staging tile
   float* bsm = reinterpret_cast<float*>(ot + TOT);            // bn | bw | gb[b] | LN scratch
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef PBX_STAMPS
+  const unsigned long long cs0 = __builtin_amdgcn_s_memtime();
+#endif
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
   // xlo / xhi: rows of the neighbouring sequence shards stored around each sample's L rows (context
@@ -100,6 +106,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       },
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
   __syncthreads();
+#ifdef PBX_STAMPS
+  const unsigned long long cs1 = __builtin_amdgcn_s_memtime();
+#endif
 
   f32x16_t acc[NPT];
 #pragma unroll
@@ -162,6 +171,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   }
 #endif
 
+#ifdef PBX_STAMPS
+  const unsigned long long cs2 = __builtin_amdgcn_s_memtime();
+#endif
   // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
   // Both pre-activation tiles are staged in LDS (narrow -> ot, wide -> over the x tile, whose 4 rows
   // per thread are read into registers first), then all 512 threads take 4 (row, 16-B chunk) units
@@ -278,6 +290,14 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     stats[((size_t)b * T + t) * 2] = m;
     stats[((size_t)b * T + t) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
   }
+#ifdef PBX_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const unsigned long long cs3 = __builtin_amdgcn_s_memtime();
+  if (lane == 0) {
+    unsigned long long* o = pbx_conv_stamps + ((size_t)(blockIdx.x & 4095) * 8 + w) * 4;
+    o[0] = cs1 - cs0; o[1] = cs2 - cs1; o[2] = cs3 - cs2; o[3] = cs0;
+  }
+#endif
 }
 
 // fp32 torch conv weight [co][ci][KS] -> bf16 fragment images: fwd[k][kb][mb][lane][8] with
@@ -360,3 +380,9 @@ PBX_EXPORT int pbx_pack_conv_frag(const float* w, void* pf, void* pt, int KS, hi
                      KS);
   return pbx_launch_status();
 }
+
+#ifdef PBX_STAMPS
+PBX_EXPORT int pbx_conv_stamps_read(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_conv_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
