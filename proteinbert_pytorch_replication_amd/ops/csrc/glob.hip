@@ -211,10 +211,10 @@ PBX_EXPORT int pbx_bias_gelu(const float* u, const float* bias, float* out, void
   return pbx_launch_status();
 }
 
-// slab (nullable): [min(M, 32)][N] fp32 -> the bias gradient is folded in a fixed order (deterministic)
+// slab (nullable): [min(M, 256)][N] fp32 -> the bias gradient is folded in a fixed order (deterministic)
 PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float* bias, void* du, float* dbias, int M,
                                  int N, float* slab, hipStream_t st) {
-  const int gy = M < 32 ? M : 32;
+  const int gy = M < 256 ? M : 256;      // (ops/global_track.py BGB_ROWS)
   hipLaunchKernelGGL(bias_gelu_bwd_kernel, dim3((N + 255) / 256, gy), dim3(256), 0, st, dout, u, bias, (bf16_t*)du,
                      dbias, M, N, slab);
   if (slab != nullptr) {

@@ -313,7 +313,7 @@ class InputLayerFn(torch.autograd.Function):
             N = ugl.shape[1]
             dugl = torch.empty((B, N), dtype=BF16, device=dev)
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
-                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, 32), N, dev)), st)
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, BGB_ROWS), N, dev)), st)
             addmm_into(dwgl, dugl.t(), g_bf)
             dg = addmm_new(dg, dugl, bf16_of(wgl))
         if ctx.sparse:
@@ -327,9 +327,14 @@ class InputLayerFn(torch.autograd.Function):
             return (None, *gr.finish())
         du = torch.empty((B, G), dtype=BF16, device=dev)
         _lib.call("pbx_bias_gelu_bwd", dg.data_ptr(), u.data_ptr(), b.data_ptr(), du.data_ptr(), db.data_ptr(), B, G,
-                  _lib.ptr(_det_slab(min(B, 32), G, dev)), st)
+                  _lib.ptr(_det_slab(min(B, BGB_ROWS), G, dev)), st)
         _gemm(du, x, dw, ta=True, tb=False, accumulate=True, pad_b=True)      # dW_in += du^T ann
         return (None, *gr.finish())
+
+
+# row groups of pbx_bias_gelu_bwd (csrc/glob.hip): a thread walks M / 256 rows (at 32 groups its 32 serial
+# row loads made the [1024, 128] input-layer backward an 80 us latency chain in the step's tail)
+BGB_ROWS = 256
 
 
 def _det_slab(rows: int, cols: int, dev) -> Optional[torch.Tensor]:
@@ -545,7 +550,7 @@ class GlobalBlockFn(torch.autograd.Function):
             N = ugl.shape[1]
             dugl = torch.empty((B, N), dtype=BF16, device=dev)
             _lib.call("pbx_bias_gelu_bwd", dgb.float().contiguous().data_ptr(), ugl.data_ptr(), bgl.data_ptr(),
-                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, 32), N, dev)), st)
+                      dugl.data_ptr(), dbgl.data_ptr(), B, N, _lib.ptr(_det_slab(min(B, BGB_ROWS), N, dev)), st)
             addmm_into(dwgl, dugl.t(), g2_bf)
             dg2 = addmm_new(dg2, dugl, bf16_of(wgl))                   # new buffer (incoming grad untouched)
         # LN2 + MLP2
