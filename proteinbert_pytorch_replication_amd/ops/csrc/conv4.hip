@@ -18,6 +18,9 @@ constexpr int BM = 128;              // positions per tile
 constexpr int KS = 9;                // taps (the launcher refuses other sizes)
 constexpr int NI = KS * 8;           // K-steps per tile (taps x 16-channel blocks)
 constexpr int NPT = BM / 32;         // 32-position MFMA tiles per wave
+#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/dgradstamps.py)
+__device__ unsigned long long pbx_dgrad_stamps[4096 * 4 * 4];   // [workgroup][wave][prologue, loop, epilogue, -]
+#endif
 
 
 // ------------------------------------------------------------------------------------------------
@@ -68,6 +71,9 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
   unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
   unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
   const int tid = threadIdx.x, lane = tid & 63, cq = __builtin_amdgcn_readfirstlane(tid >> 6);
+#ifdef PBX_STAMPS
+  const unsigned long long dst0 = __builtin_amdgcn_s_memtime();
+#endif
   const int r = lane & 31, h = lane >> 5;
   const size_t sbase = (size_t)b * L * CH;                          // outputs: [B][L][128]
   const ptrdiff_t ibase = ((ptrdiff_t)b * (L + ilo + ihi) + ilo) * CH;   // inputs: logical position 0
@@ -233,6 +239,9 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     }
   }
   __syncthreads();
+#ifdef PBX_STAMPS
+  const unsigned long long dst1 = __builtin_amdgcn_s_memtime();
+#endif
 
   f32x16_t acc[NPT];
 #pragma unroll
@@ -274,6 +283,17 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     }
   }
 
+#ifdef PBX_STAMPS
+  const unsigned long long dst2 = __builtin_amdgcn_s_memtime();
+  auto stamp_end = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned long long dst3 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) {
+      unsigned long long* o = pbx_dgrad_stamps + ((size_t)(blockIdx.x & 4095) * 4 + cq) * 4;
+      o[0] = dst1 - dst0; o[1] = dst2 - dst1; o[2] = dst3 - dst2; o[3] = 1;
+    }
+  };
+#endif
   // dx = ds1 + acc: the fp32 tile goes through LDS (over the dpre tiles) for row-contiguous 16-B accesses
   const int vrows = min(BM, L - pos0);
   float* ft = reinterpret_cast<float*>(smem);
@@ -320,6 +340,9 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
       for (int e = 0; e < 8; ++e) o[e] = gv[e] + fv[e];
       *reinterpret_cast<uint4*>(dx + sbase + (size_t)(pos0 + row) * CH + cc * 8) = packq8(o);
     }
+#ifdef PBX_STAMPS
+    stamp_end();
+#endif
     return;
   }
 #pragma unroll
@@ -395,3 +418,9 @@ PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw
                                void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
   return pbx_conv_dgrad4x(ds1, gdn, gdw, ftn, ftw, dx, dpre_n, dpre_w, B, L, KS_, dil, 0, 0, st);
 }
+
+#ifdef PBX_STAMPS
+PBX_EXPORT int pbx_dgrad_stamps_read(unsigned long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_dgrad_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
+}
+#endif
