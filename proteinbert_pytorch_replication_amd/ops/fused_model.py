@@ -57,8 +57,6 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
     if cp is None:
         model.check_length(tokens.shape[1])   # the kernels index the [L, C] LayerNorm affine by position
     else:
-        if model.semantics != "reference":
-            raise NotImplementedError("context parallelism on the fused executor: reference semantics only")
         model.check_length(cp.L)
         if tokens.shape[1] != cp.shard_len:
             raise ValueError(f"expected a {cp.shard_len}-residue shard, got {tokens.shape[1]}")
@@ -107,8 +105,9 @@ def fused_encode(model, tokens: torch.Tensor, annotations: torch.Tensor,
         if paper:
             # per-position LayerNorm local track, then attention over positions (split-L HIP core);
             # its [B, G] output enters the global track unscaled (W_parameter unused, as in the oracle)
-            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i], tok=tok_c if i == 0 else None,
-                               emb=emb_w if i == 0 else None, emb_grad=fold and i == 0)
+            first = i == 0 and cp is None
+            h, o = paper_block(h, gb, g, blk, mask, conv_imgs[i], tok=tok_c if first else None,
+                               emb=emb_w if first else None, emb_grad=fold and i == 0, cp=cp)
             vpart = o.unsqueeze(1)
             wp = unit_attention_weight(att.key_dim, h.device)
         else:

@@ -51,8 +51,6 @@ _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
 _lib.register("pbx_conv_fwd3t", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4f", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I,
                                     _F, _P])
-_lib.register("pbx_conv_dgrad5f", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
-                                    _I, _F, _P])
 _lib.register("pbx_embed_dpre", [_P, _P, _P, _P, _P, _P, _P, _L, _I, _P, _P])
 _lib.register("pbx_embed_bwd_groups", [_L])
 
@@ -186,11 +184,6 @@ EMBED_FOLD = True
 # ... and (reference semantics) its conv gathers emb[tok] in the staging pass: the [B, L, 128] embedding
 # output is never written (False: embed_fwd + conv_fwd3)
 EMBED_GATHER = True
-
-
-# the LN1-finalize data gradient as the wave-specialised persistent kernel (csrc/conv5.hip: 4 MFMA waves + 4
-# staging waves per CU, two LDS buffers; False: conv_dgrad4<FIN>, three phases per tile)
-DGRAD5 = False
 
 
 def wgrad_tok_ok(tok: Optional[torch.Tensor], emb: Optional[torch.Tensor], L: int, KS: int) -> bool:
@@ -415,8 +408,7 @@ class LocalBlockFn(torch.autograd.Function):
             dgb_ready()
         demb = None
         if fin:
-            _lib.call("pbx_conv_dgrad5f" if DGRAD5 and dil <= 5 else "pbx_conv_dgrad4f", dh1.data_ptr(),
-                      s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+            _lib.call("pbx_conv_dgrad4f", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
                       TS1, g1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
                       dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), dgb.data_ptr(), B, L, KS, dil, LN_EPS, stream)
             dgb_ready()

@@ -74,7 +74,7 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, gb, g, wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv, mask, dil: int, packed=None,
-                tok=None, emb=None, emb_grad: bool = False):
+                tok=None, emb=None, emb_grad: bool = False, cp=None):
         from .paper_attention import KEY_DIM, VALUE_DIM, _nsplit
         params = (wn, bn, ww, bw, g1, be1, wl, bl, g2, be2, Wq, Wk, Wv)
         B, L, C = x.shape
@@ -97,7 +97,12 @@ class PaperBlockFn(torch.autograd.Function):
         gb = gb.detach().float().contiguous()
         pre_n, pre_w, s1 = torch.empty_like(x), torch.empty_like(x), torch.empty_like(x)
         st1 = torch.empty((B, T1, 2), dtype=F32, device=dev)       # whole-sequence partials (unused here)
-        conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream)
+        # cp (parallel/cp_fused.py CPShard): x is this rank's slice; the convs read the neighbours' halo
+        # rows (P2P), LayerNorm is per position (nothing else to exchange in the local track)
+        x_ext, hlo = (x, 0) if cp is None else (cp.halo_rows(x), cp.halo)
+        if cp is not None and (tok is not None or emb_grad):
+            raise ValueError("context parallelism: the token-embedding first-block forms are single-shard only")
+        conv_fwd(x_ext, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, st1, B, L, KS, dil, stream, hlo, hlo)
         h2 = torch.empty_like(x)
         stats = torch.empty((B * L, 4), dtype=F32, device=dev)
         _lib.call("pbx_pc_ln_linear_fwd", s1.data_ptr(), g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(),
@@ -131,6 +136,8 @@ class PaperBlockFn(torch.autograd.Function):
             _lib.call("pbx_paper_attn_fwd", pre.data_ptr(), qs.data_ptr(), _lib.ptr(mk), part.data_ptr(),
                       o.data_ptr(), lse.data_ptr(), B, L, H, K, VD, ns, stream)
             wsave = wcat
+        if cp is not None:
+            o, lse = _cp_softmax_combine(o, lse, B, H, VD, cp)
         ctx.fused = fused
         ctx.g32 = gf                          # fp32 (detached) g for the dWq product
         # the first block: x = bf16(emb[tok]), the conv weight gradient goes through the token one-hot
@@ -140,8 +147,9 @@ class PaperBlockFn(torch.autograd.Function):
         ctx.emb_grad = bool(emb_grad)
         if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
             raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
-        ctx.save_for_backward(x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
-                              wq_cat)
+        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse,
+                              h2, wq_cat)
+        ctx.cp, ctx.hlo = cp, hlo
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
         ctx.set_materialize_grads(False)
@@ -149,9 +157,11 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, do):
-        (x, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
+        (x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
          wq_cat) = ctx.saved_tensors
         B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
+        cp, hlo = ctx.cp, ctx.hlo
+        x = x_ext if cp is None else x_ext[:, hlo:hlo + L]     # this shard's rows (shape / dtype only)
         dev = x.device
         stream = _lib.stream_ptr(dev)
         params = ctx.params
@@ -184,6 +194,8 @@ class PaperBlockFn(torch.autograd.Function):
                           stream)
                 dh2_att = [mm32(dpre, wsave.t()).to(BF16), None]                          # [R, C] bf16
             dqs = dq_part.sum(dim=1).view(B, H, K)
+            if cp is not None:
+                cp.all_reduce_(dqs)             # q is replicated: its gradient sums every shard's positions
             dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K)        # [B, H*K] fp32
             dg = mm_x3(dqpre, wq_cat.t())                                                  # [B, G]
             gf32 = ctx.g32
@@ -215,20 +227,27 @@ class PaperBlockFn(torch.autograd.Function):
                   dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
                   dbl.data_ptr(), *dwl_slab(dev), B, L, stream)
         dgb = dgbp.sum(dim=1)
+        if cp is not None:
+            cp.all_reduce_(dgb)                 # gb is replicated: its gradient sums every shard's positions
         dpn, dpw = torch.empty_like(x), torch.empty_like(x)
         demb, dE_direct, dx = None, True, None
         if ctx.emb_grad:
             demb, dE_direct = embed_fold_bwd(*ctx.tok, ds1, pre_n, pre_w, dpn, dpw, wn, ww, stream)
-        else:
+        elif cp is None:
             dx = torch.empty_like(x)
             conv_dgrad(ds1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream)
+        else:
+            dx = torch.empty_like(x)
+            conv_dgrad(*cp.halo_rows_many(ds1, pre_n, pre_w), wtn, wtw, dx, dpn, dpw, B, L, KS, dil, stream,
+                       hlo, hlo)
         if ctx.tok is not None:
             tok, emb = ctx.tok
             wg = lambda: _wgrad_tok(dpn, dpw, tok, emb, dil, B, L, [(dwn, dbn), (dww, dbw)], demb)   # noqa: E731
         else:
-            wg = lambda: _wgrad(dpn, dpw, x, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)])      # noqa: E731
+            wg = lambda: _wgrad(dpn, dpw, x_ext, KS, dil, 2, B, L, [(dwn, dbn), (dww, dbw)],   # noqa: E731
+                                xlo=hlo, xhi=hlo)
         if all(dsts[i][1] for i in (0, 1, 2, 3)) and dE_direct and streams.ENABLED:
-            streams.launch(dev, wg, keep=[dpn, dpw, x] + ([demb[2]] if demb is not None else []), name="wgrad")
+            streams.launch(dev, wg, keep=[dpn, dpw, x_ext] + ([demb[2]] if demb is not None else []), name="wgrad")
         else:
             wg()
         direct = [p for p, (_, d) in zip(params, dsts) if d]
@@ -238,11 +257,34 @@ class PaperBlockFn(torch.autograd.Function):
             notify_grads_ready(direct)
         pgrads = [None if d else gr for (gr, d) in dsts]
         gemb = demb[2] if demb is not None and not dE_direct else None
-        return (dx, dgb, dg, *pgrads, None, None, None, None, gemb, None)
+        return (dx, dgb, dg, *pgrads, None, None, None, None, gemb, None, None)
+
+
+def _cp_softmax_combine(o: torch.Tensor, lse: torch.Tensor, B: int, H: int, VD: int, cp):
+    """Merge the shards' softmax-over-positions results: each rank's ``(o_r, lse_r)`` covers its own
+    positions; the group's is ``lse = logsumexp_r lse_r`` and ``o = sum_r exp(lse_r - lse) o_r`` (one MAX
+    and one SUM all-reduce of ``B H (1 + VD)`` floats).  With the group's ``(o, lse)`` the backward kernel
+    is exact on each shard's positions.  A shard whose positions of a sample are all padding carries
+    ``lse = +inf`` (the kernels' "no mass" value: p = exp(s - lse) = 0) and adds nothing."""
+    import torch.distributed as dist
+    empty = torch.isposinf(lse)
+    lr = torch.where(empty, torch.full_like(lse, -float("inf")), lse)
+    m = lr.clone()
+    dist.all_reduce(m, op=dist.ReduceOp.MAX, group=cp.group)
+    mz = torch.where(torch.isfinite(m), m, torch.zeros_like(m))
+    w = torch.exp(lr - mz)                                                  # 0 for an all-padding shard
+    ow = torch.where(w[:, None] > 0, o.view(B * H, VD) * w[:, None], torch.zeros_like(o.view(B * H, VD)))
+    s = torch.cat([w, ow.reshape(-1)])
+    dist.all_reduce(s, group=cp.group)
+    sw = s[:B * H]
+    has = sw > 0
+    o_g = torch.where(has[:, None], s[B * H:].view(B * H, VD) / sw.clamp_min(1e-30)[:, None], 0.0)
+    lse_g = torch.where(has, mz + torch.log(sw.clamp_min(1e-30)), torch.full_like(sw, float("inf")))
+    return o_g.reshape(B, H * VD).contiguous(), lse_g.contiguous()
 
 
 def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, packed=None, tok=None, emb=None,
-                emb_grad: bool = False):
+                emb_grad: bool = False, cp=None):
     """``(h2, o)`` of one paper-semantics block's local track + attention (fused HIP path); ``tok`` /
     ``emb``: ``x`` is the token embedding bf16(emb[tok]) (the first block); ``emb_grad``: the backward
     returns ``emb``'s gradient (``x`` without autograd history, local_track.EMBED_FOLD)."""
@@ -252,7 +294,7 @@ def paper_block(x: torch.Tensor, gb: torch.Tensor, g: torch.Tensor, blk, mask, p
     return PaperBlockFn.apply(x, gb, g, nc.weight, nc.bias, wc.weight, wc.bias, blk.local_norm_1.weight,
                               blk.local_norm_1.bias, blk.local_linear_layer[0].weight,
                               blk.local_linear_layer[0].bias, blk.local_norm_2.weight, blk.local_norm_2.bias,
-                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed, tok, emb, emb_grad)
+                              att.Wq, att.Wk, att.Wv, mask, blk.wide_conv_dilation, packed, tok, emb, emb_grad, cp)
 
 
 def paper_local_block(x: torch.Tensor, gb: torch.Tensor, blk, packed=None) -> torch.Tensor:

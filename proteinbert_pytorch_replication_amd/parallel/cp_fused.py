@@ -5,8 +5,9 @@ CDNA4 local-track kernels on its slice ``[r L/P, (r+1) L/P)`` and the tiny globa
 What couples the slices (reference ``ProteinBERT/modules.py:124-151,201-231``) and where it is
 exchanged:
 
-* the narrow / wide dilated convolutions need ``4 d`` = 20 neighbour rows on each side: the halo is
-  gathered once per block (``halo_rows``) and the conv kernels read it in place (``pbx_conv_fwd3x`` /
+* the narrow / wide dilated convolutions need ``4 d`` = 20 neighbour rows on each side: the halo comes
+  from the two ring neighbours by ``isend`` / ``irecv`` once per block and direction (``halo_rows`` /
+  ``halo_rows_many``) and the conv kernels read it in place (``pbx_conv_fwd3x`` /
   ``pbx_wgrad2x`` take ``xlo`` / ``xhi`` halo rows; the data gradient ``pbx_conv_dgrad4x`` reads the
   neighbours' ``ds1`` and GELU' rows the same way, so no gradient is sent back);
 * ``LayerNorm((L, C))`` statistics are per sample over the WHOLE sequence: the kernels' per-tile
@@ -27,9 +28,14 @@ local-track parameters (convs, [L, C] affine rows, local MLP, embedding, local h
 partial gradients that :func:`cp_reduce_grads` SUMs over the group, while the replicated parameters
 (global track, GO input / output layers) already hold the full gradient on every rank.
 
+Paper semantics (per-position LayerNorm, attention softmax over positions; ``ops/paper_track.py``) shards
+the same way with less to exchange: no LayerNorm statistics, the conv halos as above, and the attention
+over positions as a split softmax -- every rank's fused attention kernel covers its positions and the
+group merges ``(o, logsumexp)`` (one MAX + one SUM all-reduce), after which the backward kernel is exact on
+each shard; the query gradient and the broadcast vector's gradient are all-reduced.
+
 Collectives are plain ``torch.distributed`` calls on the CP group (RCCL over xGMI on a node; gloo for
-CPU rehearsal of the bookkeeping).  Reference semantics only: paper semantics keeps the PyTorch-op CP
-path (:mod:`.context_parallel`).
+CPU rehearsal of the bookkeeping).
 """
 from __future__ import annotations
 
@@ -69,19 +75,40 @@ class CPShard:
         return t
 
     # ---- halo ----------------------------------------------------------------------------------
-    def halo_rows(self, x: torch.Tensor) -> torch.Tensor:
-        """``[B, Ls, C]`` -> ``[B, H + Ls + H, C]`` with the neighbours' edge rows (zeros beyond the
-        sequence ends = the convs' ``padding="same"``).  One all-gather of every rank's two edge strips
-        (2 x B x 20 x 128 bf16 per rank)."""
+    def _peer(self, r: int) -> int:
+        return r if self.group is None else dist.get_global_rank(self.group, r)
+
+    def halo_rows_many(self, *xs: torch.Tensor) -> List[torch.Tensor]:
+        """Each ``[B, Ls, C]`` -> ``[B, H + Ls + H, C]`` with the neighbours' edge rows (zeros beyond the
+        sequence ends = the convs' ``padding="same"``).  Neighbour point-to-point only: one
+        ``isend`` / ``irecv`` pair per neighbour carries the edge strips of every tensor (2 x B x H x C
+        per tensor and direction, the same on every rank whatever the CP degree; on a node these are
+        single-link xGMI transfers between ring neighbours)."""
         H = self.halo
-        B, Ls, C = x.shape
-        edges = torch.stack([x[:, :H], x[:, Ls - H:]]).contiguous()            # [2, B, H, C]
-        allg = [torch.empty_like(edges) for _ in range(self.world)]
-        dist.all_gather(allg, edges, group=self.group)
-        zero = torch.zeros((B, H, C), dtype=x.dtype, device=x.device)
-        left = allg[self.rank - 1][1] if self.rank > 0 else zero
-        right = allg[self.rank + 1][0] if self.rank < self.world - 1 else zero
-        return torch.cat([left, x, right], dim=1).contiguous()
+        B, Ls, C = xs[0].shape
+        for x in xs:
+            if x.shape != (B, Ls, C) or x.dtype != xs[0].dtype:
+                raise ValueError("halo_rows_many: tensors must share shape and dtype")
+        n = len(xs)
+        lo = torch.stack([x[:, :H] for x in xs]).contiguous()            # [n, B, H, C] -> left neighbour
+        hi = torch.stack([x[:, Ls - H:] for x in xs]).contiguous()       # -> right neighbour
+        left = torch.zeros_like(lo)
+        right = torch.zeros_like(hi)
+        ops = []
+        if self.rank > 0:
+            peer = self._peer(self.rank - 1)
+            ops += [dist.P2POp(dist.isend, lo, peer, self.group), dist.P2POp(dist.irecv, left, peer, self.group)]
+        if self.rank < self.world - 1:
+            peer = self._peer(self.rank + 1)
+            ops += [dist.P2POp(dist.isend, hi, peer, self.group), dist.P2POp(dist.irecv, right, peer, self.group)]
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return [torch.cat([left[i], xs[i], right[i]], dim=1).contiguous() for i in range(n)]
+
+    def halo_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """One tensor's halo exchange (:meth:`halo_rows_many`)."""
+        return self.halo_rows_many(x)[0]
 
     # ---- LayerNorm((L, C)) statistics ----------------------------------------------------------
     def fix_stats(self, st: torch.Tensor, BM: int, C: int = 128) -> None:
@@ -134,11 +161,16 @@ class _PoolSum(torch.autograd.Function):
 
 
 def local_track_params(model) -> List[torch.nn.Parameter]:
-    """Parameters whose gradients are per-shard partials under CP (summed over the group)."""
+    """Parameters whose gradients are per-shard partials under CP (summed over the group).  In paper
+    semantics the attention's key / value projections are too (h2^T dpre over this shard's positions);
+    the query projection's gradient comes from the all-reduced query gradient, i.e. already complete."""
     out = [model.local_embedding.weight, *model.pretraining_local_output.parameters()]
     for blk in model.proteinBERT_blocks:
         out += [*blk.local_narrow_conv_layer.parameters(), *blk.local_wide_conv_layer.parameters(),
                 *blk.local_norm_1.parameters(), *blk.local_norm_2.parameters(), *blk.local_linear_layer.parameters()]
+        if getattr(model, "semantics", "reference") == "paper":
+            att = blk.global_attention_layer
+            out += [p for p in (att.Wk, att.Wv) if isinstance(p, torch.nn.Parameter)]
     return out
 
 

@@ -3,7 +3,9 @@
 group-wide LayerNorm((L, C)) statistics and backward partials, the attention-pool sum and the broadcast
 gradient exchanged over the group; gloo here -- RCCL refuses two ranks on one device -- RCCL on a node).
 The group's loss and (CP-reduced) parameter gradients must match the single-GPU fused step on the whole
-sequence within the fused path's bf16 tolerances."""
+sequence within the fused path's bf16 tolerances.  Both semantics: paper semantics (per-position
+LayerNorm, attention softmax over positions) merges the shards' attention as a split softmax and sums the
+key / value projections' partial gradients (parallel/cp_fused.py)."""
 import os
 import socket
 
@@ -24,21 +26,28 @@ def _port():
     return p
 
 
-def _setup():
+def _setup(semantics):
     from proteinbert_pytorch_replication_amd.data import SyntheticUniRefGO
     from proteinbert_pytorch_replication_amd.models import ProteinBERT
     torch.manual_seed(0)
     m = ProteinBERT(sequences_length=L, num_annotations=8943, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
-                    num_blocks=2, device="cuda", backend="hip")
+                    num_blocks=2, device="cuda", backend="hip", semantics=semantics)
     with torch.no_grad():   # non-trivial [L, C] affines: a wrong slice or statistic shows up
         for blk in m.proteinBERT_blocks:
             for ln in (blk.local_norm_1, blk.local_norm_2):
                 ln.weight.normal_(1.0, 0.2)
                 ln.bias.normal_(0.0, 0.2)
-    return m, SyntheticUniRefGO(L, 8943, B, "cuda", seed=11).next_batch()
+    X, Y, W = SyntheticUniRefGO(L, 8943, B, "cuda", seed=11).next_batch()
+    if semantics == "paper":
+        # no padding: every position takes part in the attention softmax, so both shards carry mass and
+        # the split-softmax merge is exercised (with the synthetic lengths the second half would be all pad)
+        g = torch.Generator(device="cuda").manual_seed(5)
+        fill = torch.randint(1, 24, X["local"].shape, device="cuda", generator=g, dtype=X["local"].dtype)
+        X = dict(X, local=torch.where(X["local"] == 0, fill, X["local"]))
+    return m, (X, Y, W)
 
 
-def _worker(rank, world, port, out):
+def _worker(rank, world, port, out, semantics):
     import datetime
     import torch.distributed as dist
     from proteinbert_pytorch_replication_amd.ops import streams
@@ -47,7 +56,7 @@ def _worker(rank, world, port, out):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
                             timeout=datetime.timedelta(seconds=300))
     try:
-        m, (X, Y, W) = _setup()
+        m, (X, Y, W) = _setup(semantics)
         cp = CPShard(L)
         sh = lambda d: {"local": cp.shard(d["local"]), "global": d["global"]}   # noqa: E731
         loss, full = cp_loss(m, cp, sh(X), sh(Y), sh(W))
@@ -61,12 +70,14 @@ def _worker(rank, world, port, out):
         dist.destroy_process_group()
 
 
-def test_cp_fused_matches_single_gpu(tmp_path):
+@pytest.mark.parametrize("semantics", ["reference", "paper"])
+def test_cp_fused_matches_single_gpu(tmp_path, semantics):
     from proteinbert_pytorch_replication_amd.ops import streams
     from proteinbert_pytorch_replication_amd.ops.fused_model import fused_pretrain_loss
     world = 2
-    mp.start_processes(_worker, args=(world, _port(), str(tmp_path)), nprocs=world, start_method="spawn", join=True)
-    m, (X, Y, W) = _setup()
+    mp.start_processes(_worker, args=(world, _port(), str(tmp_path), semantics), nprocs=world, start_method="spawn",
+                       join=True)
+    m, (X, Y, W) = _setup(semantics)
     loss = fused_pretrain_loss(m, X, Y, W)
     loss.backward()
     streams.join()

@@ -22,7 +22,7 @@ ap.add_argument("--dp", action="store_true",
                 help="attach the bucketed all-reduce (forced on a 1-rank RCCL group): the DP step's hooks")
 ap.add_argument("--graph", action="store_true", help="time hipGraph replays (GraphedStep) instead of eager steps")
 a = ap.parse_args()
-dev = torch.device("cuda")
+dev = torch.device("cuda", 0)     # an indexed device: init_process_group(device_id=...) requires one
 torch.manual_seed(0)
 m = ProteinBERT(sequences_length=512, num_annotations=8943, local_dim=128, global_dim=512, key_dim=64, num_heads=4,
                 num_blocks=6, device=dev, backend="hip")
