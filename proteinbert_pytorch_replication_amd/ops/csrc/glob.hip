@@ -258,6 +258,46 @@ PBX_EXPORT int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
   return pbx_launch_status();
 }
 
+// two folds with the same row count in one launch (a weight slab and its bias slab): blocks < ceil(cols0 / 32)
+// fold (src0, cols0) into dst0, the rest (src1, cols1) into dst1; same fixed order as colsum_add_kernel
+__global__ void __launch_bounds__(256) colsum_add2_kernel(const float* __restrict__ src0, int cols0,
+                                                          float* __restrict__ dst0, const float* __restrict__ src1,
+                                                          int cols1, float* __restrict__ dst1, int rows) {
+  __shared__ float part[8][33];
+  const int nb0 = (cols0 + 31) / 32;
+  const bool second = (int)blockIdx.x >= nb0;
+  const float* src = second ? src1 : src0;
+  float* dst = second ? dst1 : dst0;
+  const int cols = second ? cols1 : cols0;
+  const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int c = ((int)blockIdx.x - (second ? nb0 : 0)) * 32 + cl;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < cols) {
+    int r = rl;
+    for (; r + 8 < rows; r += 16) {
+      a0 += src[(size_t)r * cols + c];
+      a1 += src[(size_t)(r + 8) * cols + c];
+    }
+    for (; r < rows; r += 8) a0 += src[(size_t)r * cols + c];
+  }
+  part[rl][cl] = a0 + a1;
+  __syncthreads();
+  if (rl == 0 && c < cols) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += part[k][cl];
+    dst[c] += s;
+  }
+}
+
+PBX_EXPORT int pbx_colsum_add2(const float* src0, int cols0, float* dst0, const float* src1, int cols1, float* dst1,
+                               int rows, hipStream_t st) {
+  if (cols0 <= 0 || cols1 <= 0 || rows <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_add2_kernel, dim3((cols0 + 31) / 32 + (cols1 + 31) / 32), dim3(256), 0, st, src0, cols0,
+                     dst0, src1, cols1, dst1, rows);
+  return pbx_launch_status();
+}
+
 // the same over column block [0, cols) of rows `ld` floats apart
 PBX_EXPORT int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, float* dst, const float* scale,
                                  hipStream_t st) {

@@ -45,6 +45,7 @@ _lib.register("pbx_ln2_linear_bwd", [_P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I,
                                      _P, _P, _P, _P, _P, _I, _I, _F, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_ln2_bwd_slab_rows", [_I, _I, _I])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
+_lib.register("pbx_colsum_add2", [_P, _I, _P, _P, _I, _P, _I, _P])
 _lib.register("pbx_ln1_finalize", [_P, _P, _P, _I, _I, _P, _I, _P, _P, _P, _I, _I, _F, _I, _P])
 _lib.register("pbx_embed_fwd", [_P, _P, _P, _L, _P])
 _lib.register("pbx_embed_bwd", [_P, _P, _P, _L, _I, _P, _P])
@@ -377,8 +378,8 @@ class LocalBlockFn(torch.autograd.Function):
         if late_fold:
             def fold(slab=fslab, rows=rows, dwl=dwl, dbl=dbl):
                 st = _lib.stream_ptr(dev)
-                _lib.call("pbx_colsum_add", slab.data_ptr(), rows, CH * CH, dwl.data_ptr(), None, st)
-                _lib.call("pbx_colsum_add", slab[rows * CH * CH:].data_ptr(), rows, CH, dbl.data_ptr(), None, st)
+                _lib.call("pbx_colsum_add2", slab.data_ptr(), CH * CH, dwl.data_ptr(), slab[rows * CH * CH:].data_ptr(),
+                          CH, dbl.data_ptr(), rows, st)
             streams.launch(dev, fold, keep=[fslab], name="wgrad")
         dx = None if ctx.emb_grad else torch.empty_like(x)
         dpn = torch.empty_like(x)
