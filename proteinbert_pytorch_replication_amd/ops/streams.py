@@ -23,8 +23,8 @@ Protocol (eager and under hipGraph capture, where fork/join become graph edges):
   stream keeps overlapping).
 * :func:`join` makes the main stream wait for every aux stream (queued as an autograd
   end-of-backward callback and called by :class:`..train.step.PretrainStep`), and
-  :func:`collective_stream` orders a DP all-reduce behind the main stream and every aux stream on a
-  dedicated communication stream.
+  :func:`collective_stream` orders a DP all-reduce behind the main stream and every aux stream, on the
+  weight-gradient stream.
 """
 from __future__ import annotations
 
@@ -207,27 +207,40 @@ def join() -> None:
 
 @contextmanager
 def collective_stream(device: torch.device):
-    """Context for a collective over gradients that may include aux-stream results: it is enqueued
-    on a communication stream behind the current stream and every aux stream in use, without making
-    any of them wait."""
+    """Context for a collective over gradients that may include aux-stream results, without making the
+    main stream wait.  It is enqueued on the conv weight-gradient stream (``wgrad``, which produces the
+    bucket's last gradients) behind the main stream and every other aux stream in use.
+
+    Why not a dedicated communication stream: HIP multiplexes streams onto GPU_MAX_HW_QUEUES hardware
+    queues (4 on the pool), and a stream's wait on another stream's event is a barrier packet that stalls
+    its whole hardware queue.  The communication stream shared the main stream's queue, so every bucket's
+    wait for the weight-gradient stream stalled the critical path (~0.3 ms per bucket, -30 % on a forced
+    1-rank RCCL step, profiles/r5/dp_host_and_flags.txt).  The weight-gradient stream lags the main stream,
+    so its wait for the main stream is normally already satisfied, and its own queue is the one that
+    would wait anyway."""
     idx = _idx(device)
     names = _used.get(idx)
     if not names:
         yield
         return
-    comm = _aux(device, "comm")
-    comm.wait_stream(torch.cuda.current_stream(idx))
+    host = _aux(device, "wgrad") if "wgrad" in names else _aux(device, "comm")
+    _wait(host, torch.cuda.current_stream(idx))
     for name in names:
-        comm.wait_stream(_streams[(idx, name)])
-    with torch.cuda.stream(comm):
+        other = _streams[(idx, name)]
+        if other is not host:
+            _wait(host, other)
+    with torch.cuda.stream(host):
         yield
 
 
 def join_collectives(device: torch.device) -> None:
-    """Current stream waits for the communication stream of :func:`collective_stream` (its non-finite flag
+    """Current stream waits for the streams :func:`collective_stream` enqueued on (the non-finite flag
     kernels; the collectives themselves are joined by ``work.wait()``).  Under hipGraph capture every stream
     forked into the capture must rejoin the capturing stream before the capture ends."""
-    s = _streams.get((_idx(device), "comm"))
-    if s is not None:
-        _wait(torch.cuda.current_stream(_idx(device)), s)
+    cur = torch.cuda.current_stream(_idx(device))
+    for name in ("comm", "wgrad"):
+        s = _streams.get((_idx(device), name))
+        if s is not None:
+            _wait(cur, s)
+
 

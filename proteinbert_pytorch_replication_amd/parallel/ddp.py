@@ -22,12 +22,15 @@ collectives per step.
   behind the exposed tail: the buckets whose gradients are final only after backward (the global input
   layer + block 0, ~20 MB) are still on the wire when the Adam update of every other bucket runs on the
   compute stream; only the tail buckets' update trails their all-reduce.  The group-wide non-finite
-  decision is taken BEFORE any update: each bucket's local gradients are tested as it is launched, and
-  one 4-byte MAX all-reduce of the OR of those flags is queued ahead of the tail buckets, so every rank
-  skips or commits every bucket together.  The reduced gradients are tested as well (identical on every
-  rank, so no extra collective): a sum of finite per-rank gradients that overflows fp32 skips the whole
-  step when it is in the head buckets, and the tail update (with the head already committed) when it
-  appears only in the tail -- no Inf / NaN ever reaches the parameters.
+  decision is taken BEFORE any update: the tail buckets' local gradients are tested when they are
+  launched and one 4-byte MAX all-reduce of those flags is queued ahead of them; the head buckets are
+  tested after their all-reduce (a NaN / Inf on any rank survives the sum, and the reduced values are
+  identical on every rank, so no extra collective), so every rank skips or commits every bucket
+  together.  (Testing each head bucket's local gradients as it was launched put a kernel and two
+  cross-stream waits per bucket on the communication stream during backward: -48 % on a forced 1-rank
+  RCCL step, profiles/r5/dp_host_and_flags.txt.)  A sum of finite per-rank gradients that overflows fp32
+  skips the whole step when it is in the head buckets, and the tail update (with the head already
+  committed) when it appears only in the tail -- no Inf / NaN ever reaches the parameters.
 * ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
   bf16-rounded gradient sums); the default is fp32.  (A bf16 reduction of only the last, exposed
   bucket -- the 18 MB global input layer -- was an unmeasured option and has been removed: no
@@ -151,8 +154,9 @@ class BucketedAllReduce:
         # (ops/streams.py): enqueue the collective behind both streams without stalling this one
         ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()
         with ctx:
-            if self.track_nonfinite and not flag_done:
-                self._local_flag(b, view)
+            # no local non-finite flag for a bucket launched during backward: finish_and_step checks the
+            # REDUCED head gradients (a NaN / Inf on any rank survives the sum), so only the buckets held
+            # for the end need local flags (their update must be decided before their all-reduce lands)
             if dt != torch.float32:
                 tmp = view.to(dt)
                 self._tmp[b] = tmp
@@ -181,6 +185,7 @@ class BucketedAllReduce:
         dev = self.arena.grad.device
         ctx = streams.collective_stream(dev) if self.arena.grad.is_cuda else contextlib.nullcontext()
         with ctx:
+            self._flags.zero_()
             for b in rest:
                 s, e = self.buckets[b]
                 self._local_flag(b, self.arena.grad[s:e])

@@ -21,6 +21,9 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--dp", action="store_true",
                 help="attach the bucketed all-reduce (forced on a 1-rank RCCL group): the DP step's hooks")
 ap.add_argument("--graph", action="store_true", help="time hipGraph replays (GraphedStep) instead of eager steps")
+ap.add_argument("--dp-variant", default="full", choices=["full", "nocomm", "nooverlap"],
+                help="--dp diagnosis: nocomm = hooks and flags but no all-reduce; nooverlap = finish() + "
+                     "whole-arena Adam")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)     # an indexed device: init_process_group(device_id=...) requires one
 torch.manual_seed(0)
@@ -36,6 +39,13 @@ if a.dp:
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29517", rank=0, world_size=1,
                             timeout=datetime.timedelta(seconds=60), device_id=dev, pg_options=nccl_pg_options())
     ddp = BucketedAllReduce(opt.arena, force=True)
+    if a.dp_variant == "nocomm":
+        class _Done:
+            def wait(self):
+                pass
+        dist.all_reduce = lambda *args, **kw: _Done()     # noqa: E731
+    elif a.dp_variant == "nooverlap":
+        ddp.overlap_optimizer = False
 step = PretrainStep(m, opt, ddp)
 gen = SyntheticUniRefGO(512, 8943, a.batch, dev, seed=1)
 one = lambda: step(*gen.next_batch())  # noqa: E731
@@ -51,7 +61,8 @@ for _ in range(a.steps):
 t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
-mode = ("graph" if a.graph else "eager") + (f" + DP buckets ({len(ddp.buckets)}, 1-rank RCCL)" if ddp else "")
+mode = ("graph" if a.graph else "eager") + (f" + DP buckets ({len(ddp.buckets)}, 1-rank RCCL, {a.dp_variant})"
+                                            if ddp else "")
 print(f"B={a.batch} {mode}: issue {1000 * (t1 - t0) / a.steps:.3f} ms/step   complete {1000 * (t2 - t0) / a.steps:.3f} "
       "ms/step", flush=True)
 if os.environ.get("PBX_CPROFILE"):
