@@ -25,17 +25,6 @@ import torch
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
 from .gemm import gemm as _gemm
-
-
-def mm_x3(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """fp32 a [M, K] x b [K, N] at ~fp32 accuracy on the bf16 MFMA GEMM: a = ah + al, b = bh + bl (bf16
-    hi / lo parts), a b ~ ah bh + ah bl + al bh as ONE GEMM over the concatenated K (relative error
-    ~2^-16 instead of bf16's 2^-8).  For the small [B, G] x [G, H*K] query products of paper semantics."""
-    ah = a.to(BF16)
-    al = (a - ah.float()).to(BF16)
-    bh = b.to(BF16)
-    bl = (b - bh.float()).to(BF16)
-    return mm32(torch.cat([ah, ah, al], dim=1).contiguous(), torch.cat([bh, bl, bh], dim=0).contiguous())
 from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
                            addmm_into)
 from .local_track import (CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad,
@@ -49,6 +38,16 @@ _lib.register("pbx_pa_fused_fwd", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_paper_head", [_P, _P, _P, _P, _P, _P, _P, _P, _P, ctypes.c_long, _I, _F, _P])
 _lib.register("pbx_paper_head_parts", [ctypes.c_long])
 _lib.register("pbx_pa_fused_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+# fp32 query-path GEMMs with fused layouts / epilogues (csrc/sgemm.hip)
+_lib.register("pbx_sg_query_fwd", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_sg_query_dg", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_sg_query_dwq", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
+_lib.register("pbx_sg_query_ws", [_I, _I, _I, _I])
+
+
+def _sg_ws(B: int, G: int, H: int, K: int, dev) -> torch.Tensor:
+    """Split-K partial-sum workspace of the query-path GEMMs (csrc/sgemm.hip)."""
+    return torch.empty(_lib.lib().pbx_sg_query_ws(B, G, H, K), dtype=torch.float32, device=dev)
 
 # paper attention form: "fused" (csrc/paper_fused.hip: K/V projections on MFMA inside the attention
 # kernels, no [B*L, H*(K+VD)] pre-activation tensor; H in {2, 4}); other head counts take "split" (in-tree
@@ -108,13 +107,15 @@ class PaperBlockFn(torch.autograd.Function):
         _lib.call("pbx_pc_ln_linear_fwd", s1.data_ptr(), g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(),
                   bl.data_ptr(), g2.data_ptr(), be2.data_ptr(), h2.data_ptr(), stats.data_ptr(), B, L, LN_EPS, stream)
         # attention: q from the global track, K/V projection as one library GEMM, split-L core
-        gf = g.detach().float()
-        # q = tanh(g Wq): [B, G] x [G, H*K] at ~fp32 accuracy (three bf16 MFMA terms in one in-tree GEMM:
-        # the query feeds the softmax over L, so the bf16 rounding of g and Wq is kept out of it)
-        wq_cat = Wq.detach().permute(1, 0, 2).reshape(gf.shape[1], -1).float().contiguous()   # [G, H*K] fp32
-        g_bf = gf.to(BF16)
-        q = torch.tanh(mm_x3(gf, wq_cat)).view(B, H, K)                                  # [B, H, K]
-        qs = (q * (1.0 / math.sqrt(K))).contiguous()
+        gf = g.detach().float().contiguous()
+        # q = tanh(g Wq) at fp32 (the query feeds the softmax over L, so bf16 rounding is kept out of it):
+        # one fp32 GEMM reading Wq [H, G, K] in place, tanh and the 1/sqrt(K) scale in its epilogue
+        wq32 = Wq.detach().float().contiguous()                                         # [H, G, K]
+        G = gf.shape[1]
+        q = torch.empty((B, H, K), dtype=F32, device=dev)
+        qs = torch.empty((B, H, K), dtype=F32, device=dev)
+        _lib.call("pbx_sg_query_fwd", gf.data_ptr(), wq32.data_ptr(), q.data_ptr(), qs.data_ptr(),
+                  _sg_ws(B, G, H, K, dev).data_ptr(), B, G, H, K, 1.0 / math.sqrt(K), stream)
         o = torch.empty(B, H * VD, device=dev, dtype=F32)
         lse = torch.empty(B * H, device=dev, dtype=F32)
         mk = None if mask is None else mask.contiguous()
@@ -147,8 +148,8 @@ class PaperBlockFn(torch.autograd.Function):
         ctx.emb_grad = bool(emb_grad)
         if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
             raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
-        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse,
-                              h2, wq_cat)
+        ctx.save_for_backward(x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, q, qs, wsave, pre, mk, o, lse,
+                              h2, wq32)
         ctx.cp, ctx.hlo = cp, hlo
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
@@ -157,8 +158,8 @@ class PaperBlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dh2, do):
-        (x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, g_bf, q, qs, wsave, pre, mk, o, lse, h2,
-         wq_cat) = ctx.saved_tensors
+        (x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, q, qs, wsave, pre, mk, o, lse, h2,
+         wq32) = ctx.saved_tensors
         B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
         cp, hlo = ctx.cp, ctx.hlo
         x = x_ext if cp is None else x_ext[:, hlo:hlo + L]     # this shard's rows (shape / dtype only)
@@ -196,26 +197,30 @@ class PaperBlockFn(torch.autograd.Function):
             dqs = dq_part.sum(dim=1).view(B, H, K)
             if cp is not None:
                 cp.all_reduce_(dqs)             # q is replicated: its gradient sums every shard's positions
-            dqpre = (dqs * (1.0 / math.sqrt(K)) * (1.0 - q * q)).reshape(B, H * K)        # [B, H*K] fp32
-            dg = mm_x3(dqpre, wq_cat.t())                                                  # [B, G]
             gf32 = ctx.g32
+            G = gf32.shape[1]
+            # dg = dqpre Wq^T with dqpre = dqs (1 - q^2) / sqrt(K) formed while the operand is staged
+            dg = torch.empty((B, G), dtype=F32, device=dev)
+            _lib.call("pbx_sg_query_dg", dqs.data_ptr(), q.data_ptr(), wq32.data_ptr(), dg.data_ptr(),
+                      _sg_ws(B, G, H, K, dev).data_ptr(), B, G, H, K, 1.0 / math.sqrt(K), stream)
 
-            def att_wgrad(dpre=dpre, h2=h2, dqpre=dqpre, g_bf=g_bf, gf32=gf32):
+            def att_wgrad(dpre=dpre, h2=h2, dqs=dqs, q=q, gf32=gf32):
                 # attention projection weight gradients: dWk | dWv = h2^T dpre (K = B*L), dWq = g^T dqpre
                 # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
                 dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
                 _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)                   # [C, N] fp32
                 dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
                 dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
-                G = g_bf.shape[1]
-                dwq = mm_x3(gf32.t(), dqpre)                                               # [G, H*K], K = B
-                dWq.add_(dwq.view(G, H, K).permute(1, 0, 2))
-                return [dwcat, dwq]
+                # dWq += g^T dqpre, accumulated into the [H, G, K] gradient (fp32, fixed-order split-K)
+                ws = _sg_ws(B, G, H, K, dev)
+                _lib.call("pbx_sg_query_dwq", gf32.data_ptr(), dqs.data_ptr(), q.data_ptr(), dWq.data_ptr(),
+                          ws.data_ptr(), B, G, H, K, 1.0 / math.sqrt(K), _lib.stream_ptr(dev))
+                return [dwcat, ws]
 
             if streams.ENABLED and dev.type == "cuda" and all(d for _, d in dsts[10:]):
                 # only the optimizer and the DP all-reduce read them: beside the critical path, on the
                 # weight-gradient stream (the split-K GEMM over B*L rows was ~60 us per block on it)
-                streams.launch(dev, att_wgrad, keep=[dpre, h2, dqpre, g_bf, gf32], name="wgrad")
+                streams.launch(dev, att_wgrad, keep=[dpre, h2, dqs, q, gf32], name="wgrad")
             else:
                 att_wgrad()
         ds1 = torch.empty_like(x)

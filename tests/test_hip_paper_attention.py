@@ -73,21 +73,40 @@ def test_paper_model_step_uses_kernel_and_matches_oracle():
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize("M,K,N", [(1024, 512, 256), (7, 512, 256), (512, 6, 256)])
-def test_query_products_fp32_accurate(M, K, N):
-    """the paper-semantics query products q = tanh(g Wq), dg = dqpre Wq^T and dWq = g^T dqpre run
-    as three-term bf16 hi/lo GEMMs (ops/paper_track.py mm_x3), so their error vs fp64 stays at fp32 level
-    (~1e-5 relative) instead of bf16's ~4e-3."""
-    from proteinbert_pytorch_replication_amd.ops.global_track import mm32
-    from proteinbert_pytorch_replication_amd.ops.paper_track import mm_x3
-    torch.manual_seed(M + K)
-    a = torch.randn(M, K, device="cuda")
-    b = torch.randn(K, N, device="cuda") * 0.05
-    ref = a.double() @ b.double()
-    err3 = ((mm_x3(a, b).double() - ref).norm() / ref.norm()).item()
-    err1 = ((mm32(a.bfloat16(), b.bfloat16()).double() - ref).norm() / ref.norm()).item()
-    print(f"M={M} K={K} N={N}: hi/lo rel err {err3:.2e}  plain bf16 {err1:.2e}")
-    assert err3 < 2e-5 and err3 < 0.02 * err1
-    # non-contiguous operands, as the backward passes them (g^T, Wq^T)
-    ref_t = b.t().double() @ a.t().double()
-    assert ((mm_x3(b.t(), a.t()).double() - ref_t).norm() / ref_t.norm()).item() < 2e-5
+@pytest.mark.parametrize("B,G,H,Kd", [(1024, 512, 4, 64), (7, 512, 4, 64), (130, 384, 2, 64), (33, 40, 3, 24)])
+def test_query_products_fp32(B, G, H, Kd):
+    """the paper-semantics query products q = tanh(g Wq), dg = dqpre Wq^T and dWq += g^T dqpre
+    (csrc/sgemm.hip: fp32 FMA, fixed-order split-K, Wq read in place as [H, G, Kd], dqpre = dqs (1 - q^2) /
+    sqrt(Kd) formed while staging) stay at fp32 accuracy against fp64 -- bf16 operands would give ~4e-3."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
+    from proteinbert_pytorch_replication_amd.ops import paper_track  # noqa: F401  (registers the launchers)
+    torch.manual_seed(B + G)
+    dev = torch.device("cuda")
+    st = _lib.stream_ptr(dev)
+    g = torch.randn(B, G, device=dev)
+    wq = torch.randn(H, G, Kd, device=dev) * 0.05
+    s = 1.0 / Kd ** 0.5
+    q = torch.empty(B, H * Kd, device=dev)
+    qs = torch.empty(B, H * Kd, device=dev)
+    ws = torch.empty(_lib.lib().pbx_sg_query_ws(B, G, H, Kd), device=dev)
+    _lib.call("pbx_sg_query_fwd", g.data_ptr(), wq.data_ptr(), q.data_ptr(), qs.data_ptr(), ws.data_ptr(), B, G, H, Kd,
+              s, st)
+    wcat = wq.double().permute(1, 0, 2).reshape(G, H * Kd)
+    q_ref = torch.tanh(g.double() @ wcat)
+    dqs = torch.randn(B, H * Kd, device=dev)
+    dg = torch.empty(B, G, device=dev)
+    _lib.call("pbx_sg_query_dg", dqs.data_ptr(), q.data_ptr(), wq.data_ptr(), dg.data_ptr(), ws.data_ptr(), B, G, H,
+              Kd, s, st)
+    dwq = torch.randn(H, G, Kd, device=dev)
+    dwq0 = dwq.clone()
+    _lib.call("pbx_sg_query_dwq", g.data_ptr(), dqs.data_ptr(), q.data_ptr(), dwq.data_ptr(), ws.data_ptr(), B, G, H,
+              Kd, s, st)
+    torch.cuda.synchronize()
+    dqpre = dqs.double() * s * (1 - q.double() ** 2)
+    dg_ref = dqpre @ wcat.t()
+    dwq_ref = dwq0.double() + (g.double().t() @ dqpre).view(G, H, Kd).permute(1, 0, 2)
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()   # noqa: E731
+    e_q, e_qs = rel(q, q_ref), rel(qs, q_ref * s)
+    e_dg, e_dw = rel(dg, dg_ref), rel(dwq - dwq0, dwq_ref - dwq0.double())
+    print(f"B={B} G={G} H={H} Kd={Kd}: q {e_q:.2e} qs {e_qs:.2e} dg {e_dg:.2e} dWq {e_dw:.2e}")
+    assert max(e_q, e_qs, e_dg, e_dw) < 2e-6
