@@ -167,7 +167,13 @@ class GraphedStep:
         torch.cuda.synchronize()
         opt.prepare()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # with a process group attached, the RCCL watchdog thread polls its work events while this thread
+        # captures: under the default "global" mode such a call from another thread invalidates the capture
+        # (seen as a rare hipErrorStreamCaptureInvalidated in the DP capture test), so only this thread's
+        # calls are checked
+        ddp = getattr(step, "ddp", None)
+        mode = "thread_local" if ddp is not None and getattr(ddp, "enabled", False) else "global"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):
             X, Y, W = batch_fn()
             self.loss = step(X, Y, W)
         # capture recorded the optimizer step without executing it: undo the host-side increment
