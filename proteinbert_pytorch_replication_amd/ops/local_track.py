@@ -147,6 +147,10 @@ DGRAD_FIN = True
 INPUT_BWD_EARLY = True
 
 
+# eighths of the CUs the aux-stream conv weight gradient takes (R = 56 chunks at 7 on 256 CUs)
+WGRAD_CU_EIGHTHS = 7
+
+
 def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: int, dil: int, nconv: int,
            B: int, L: int, outs, full_chip: bool = False, xlo: int = 0, xhi: int = 0):
     """outs: [(dw, db)] destinations (accumulated into).  Returns the scratch tensors (the caller keeps
@@ -156,7 +160,7 @@ def _wgrad(dy0: torch.Tensor, dy1: Optional[torch.Tensor], x: torch.Tensor, KS: 
     # csrc/wgrad.hip: one workgroup per CU, R chunks x (nconv x 2) channel halves = 7/8 of the CUs
     # (R = 56 on 256 CUs): the aux-stream weight gradient runs beside the main-stream backward, and
     # leaving it a few CUs measured +2.4 % on the step over R = 64 (R = 48: +1.3 %, 32: -0.4 %)
-    R = max(8, (7 * _num_cus(dev) // (16 * nconv)) // 8 * 8)
+    R = max(8, (WGRAD_CU_EIGHTHS * _num_cus(dev) // (16 * nconv)) // 8 * 8)
     if full_chip:
         R = max(8, (_num_cus(dev) // (2 * nconv)) // 8 * 8)
     R = min(R, ntiles)
