@@ -123,11 +123,10 @@ PRESETS: Dict[str, RunConfig] = {
                           num_heads=4, num_blocks=2),
         kernel=KernelConfig(backend="torch", dtype="fp32"),
         train=TrainConfig(batch_size=4)),
-    # Per-GPU batches are sized for throughput on a 288 GB MI355X (~9 MiB of activations per L=512
-    # sequence, 9.0 GiB peak at 1024): at 256 sequences many fused kernels still run only 1-2 work items per wave
-    # (latency-bound); 512 fills the chip, and 1024 amortises the step's fixed part (weight-gradient
-    # reductions, the optimizer, launch tails; ~0.9 ms of a 6.3 ms B=512 step).  Round-4 same-box
-    # sweep: B=512 81.3k, 1024 87.1-87.5k, 1536 88.9k, 2048 90.0k seq/s (profiles/r4_batch_sweep.txt).
+    # Per-GPU batches are sized for throughput on a 288 GB MI355X (5.9 GiB peak at 1024 in round 5): at 256
+    # sequences many fused kernels still run only 1-2 work items per wave (latency-bound); 512 fills the chip,
+    # and 1024 amortises the step's fixed part (weight-gradient reductions, the optimizer, launch tails).
+    # Round-5 same-box sweep: B=1024 102.4k, 1536 103.8k, 2048 104.4k seq/s (profiles/r5/batch_sweep.txt).
     "cfg2_paper_l512": RunConfig(
         name="cfg2_paper_l512", model=_paper_model(512),
         train=TrainConfig(batch_size=1024)),
