@@ -166,3 +166,59 @@ PBX_EXPORT int pbx_sg_query_dwq(const float* g, const float* dqs, const float* q
   SgArgs p{g, nullptr, dqs, q, G, G, Kd, s, ws, G, H * Kd, B};
   return run<A_COL, B_DQPRE>(p, 2, dwq, nullptr, st);
 }
+
+// ------------------------------------------------------------------------------------------------
+// The fused attention kernels' K/V weight image and the K/V weight-gradient scatter, one launch each
+// (replacing a permute-cat-cast chain of three PyTorch launches and two strided adds per block).
+namespace {
+__global__ void __launch_bounds__(256) pa_wimg_kernel(const float* __restrict__ wk, const float* __restrict__ wv,
+                                                      unsigned short* __restrict__ img, int H, int C, int K, int VD) {
+  // img [H][K + VD][C] bf16: row j < K is Wk[h][:, j], row K + j is Wv[h][:, j]
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long n = (long)H * (K + VD) * C;
+  if (idx >= n) return;
+  const int c = (int)(idx % C);
+  const long hr = idx / C;
+  const int r = (int)(hr % (K + VD)), h = (int)(hr / (K + VD));
+  const float v = r < K ? wk[((size_t)h * C + c) * K + r] : wv[((size_t)h * C + c) * VD + (r - K)];
+  img[idx] = f2bf(v);
+}
+
+__global__ void __launch_bounds__(256) pa_dwkv_add_kernel(const float* __restrict__ dwcat, float* __restrict__ dwk,
+                                                          float* __restrict__ dwv, int H, int C, int K, int VD) {
+  // dwcat [C][H K + H VD]: dWk[h][c][k] += dwcat[c][h K + k], dWv[h][c][v] += dwcat[c][H K + h VD + v]
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long nk = (long)H * C * K, n = nk + (long)H * C * VD;
+  if (idx >= n) return;
+  const int N = H * (K + VD);
+  if (idx < nk) {
+    const int k = (int)(idx % K);
+    const long hc = idx / K;
+    const int c = (int)(hc % C), h = (int)(hc / C);
+    dwk[idx] += dwcat[(size_t)c * N + h * K + k];
+  } else {
+    const long j = idx - nk;
+    const int v = (int)(j % VD);
+    const long hc = j / VD;
+    const int c = (int)(hc % C), h = (int)(hc / C);
+    dwv[j] += dwcat[(size_t)c * N + H * K + h * VD + v];
+  }
+}
+}  // namespace
+
+PBX_EXPORT int pbx_pa_wimg(const float* wk, const float* wv, void* img, int H, int C, int K, int VD, hipStream_t st) {
+  const long n = (long)H * (K + VD) * C;
+  if (n <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pa_wimg_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, wk, wv,
+                     (unsigned short*)img, H, C, K, VD);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_pa_dwkv_add(const float* dwcat, float* dwk, float* dwv, int H, int C, int K, int VD,
+                               hipStream_t st) {
+  const long n = (long)H * C * (K + VD);
+  if (n <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pa_dwkv_add_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dwcat, dwk, dwv, H, C,
+                     K, VD);
+  return pbx_launch_status();
+}

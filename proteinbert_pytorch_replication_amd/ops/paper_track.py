@@ -43,6 +43,8 @@ _lib.register("pbx_sg_query_fwd", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_sg_query_dg", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_sg_query_dwq", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_sg_query_ws", [_I, _I, _I, _I])
+_lib.register("pbx_pa_wimg", [_P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_pa_dwkv_add", [_P, _P, _P, _I, _I, _I, _I, _P])
 
 
 def _sg_ws(B: int, G: int, H: int, K: int, dev) -> torch.Tensor:
@@ -122,7 +124,9 @@ class PaperBlockFn(torch.autograd.Function):
         fused = PAPER_ATTN == "fused" and H in (2, 4)
         if fused:
             # [H][Wk_h^T (64 rows) | Wv_h^T (128 rows)][C] bf16: the MFMA A/B rows of the fused kernels
-            wimg = torch.cat([Wk.detach().permute(0, 2, 1), Wv.detach().permute(0, 2, 1)], dim=1).to(BF16).contiguous()
+            wimg = torch.empty((H, K + VD, C), dtype=BF16, device=dev)
+            _lib.call("pbx_pa_wimg", Wk.detach().float().contiguous().data_ptr(),
+                      Wv.detach().float().contiguous().data_ptr(), wimg.data_ptr(), H, C, K, VD, stream)
             ns = -(-L // FUSED_CHUNK_F)
             part = torch.empty(B * H, ns, 2 + VD, device=dev, dtype=F32)
             _lib.call("pbx_pa_fused_fwd", h2.data_ptr(), wimg.data_ptr(), qs.data_ptr(), _lib.ptr(mk),
@@ -209,8 +213,12 @@ class PaperBlockFn(torch.autograd.Function):
                 # in-tree MFMA GEMM, deterministic split-K over the K = B*L rows (csrc/gemm.hip)
                 dwcat = torch.empty((C, dpre.shape[1]), dtype=F32, device=dev)
                 _gemm(h2.reshape(R, C), dpre, dwcat, ta=True, tb=False)                   # [C, N] fp32
-                dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
-                dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
+                if dWk.is_contiguous() and dWv.is_contiguous():
+                    _lib.call("pbx_pa_dwkv_add", dwcat.data_ptr(), dWk.data_ptr(), dWv.data_ptr(), H, C, K, VD,
+                              _lib.stream_ptr(dev))
+                else:
+                    dWk.add_(dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2))
+                    dWv.add_(dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2))
                 # dWq += g^T dqpre, accumulated into the [H, G, K] gradient (fp32, fixed-order split-K)
                 ws = _sg_ws(B, G, H, K, dev)
                 _lib.call("pbx_sg_query_dwq", gf32.data_ptr(), dqs.data_ptr(), q.data_ptr(), dWq.data_ptr(),

@@ -110,3 +110,28 @@ def test_query_products_fp32(B, G, H, Kd):
     e_dg, e_dw = rel(dg, dg_ref), rel(dwq - dwq0, dwq_ref - dwq0.double())
     print(f"B={B} G={G} H={H} Kd={Kd}: q {e_q:.2e} qs {e_qs:.2e} dg {e_dg:.2e} dWq {e_dw:.2e}")
     assert max(e_q, e_qs, e_dg, e_dw) < 2e-6
+
+
+def test_kv_weight_image_and_gradient_scatter():
+    """csrc/sgemm.hip: the fused attention's K/V weight image (bf16 [H][K + VD][C] from Wk [H][C][K] and
+    Wv [H][C][VD]) and the dWk / dWv scatter-add from the [C][H K + H VD] GEMM output, vs torch."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
+    from proteinbert_pytorch_replication_amd.ops import paper_track  # noqa: F401  (registers the launchers)
+    torch.manual_seed(7)
+    dev = torch.device("cuda")
+    st = _lib.stream_ptr(dev)
+    H, C, K, VD = 4, 128, 64, 128
+    wk = torch.randn(H, C, K, device=dev)
+    wv = torch.randn(H, C, VD, device=dev)
+    img = torch.empty(H, K + VD, C, dtype=torch.bfloat16, device=dev)
+    _lib.call("pbx_pa_wimg", wk.data_ptr(), wv.data_ptr(), img.data_ptr(), H, C, K, VD, st)
+    ref = torch.cat([wk.permute(0, 2, 1), wv.permute(0, 2, 1)], dim=1).to(torch.bfloat16)
+    dwcat = torch.randn(C, H * (K + VD), device=dev)
+    dwk = torch.randn(H, C, K, device=dev)
+    dwv = torch.randn(H, C, VD, device=dev)
+    rk = dwk + dwcat[:, :H * K].view(C, H, K).permute(1, 0, 2)
+    rv = dwv + dwcat[:, H * K:].view(C, H, VD).permute(1, 0, 2)
+    _lib.call("pbx_pa_dwkv_add", dwcat.data_ptr(), dwk.data_ptr(), dwv.data_ptr(), H, C, K, VD, st)
+    torch.cuda.synchronize()
+    assert torch.equal(img, ref)
+    assert torch.equal(dwk, rk) and torch.equal(dwv, rv)

@@ -1,10 +1,15 @@
-"""Raw per-kernel counter means from rocprofv3 --pmc csv output: python tools/ubench/pmc_raw.py <dir>..."""
+"""Raw per-kernel counter means from rocprofv3 --pmc csv output:
+    python tools/ubench/pmc_raw.py [--match SUBSTRING] <dir>..."""
 import collections
 import csv
 import glob
 import sys
 
-for d in sys.argv[1:]:
+args = sys.argv[1:]
+match = ""
+if args[:1] == ["--match"]:
+    match, args = args[1], args[2:]
+for d in args:
     fs = glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)
     if not fs:
         print("missing", d)
@@ -19,6 +24,6 @@ for d in sys.argv[1:]:
         for c, x in v.items():
             per[names[k][:40]][c].append(x)
     for n, v in sorted(per.items()):
-        if "conv_dgrad" not in n:
+        if match not in n:
             continue
         print(d, n, " ".join(f"{c}={sum(x) / len(x):.4g}" for c, x in sorted(v.items())))
