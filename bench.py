@@ -64,6 +64,9 @@ def parse():
                     help="capture the whole step in a hipGraph (auto: only with PBX_GRAPH=1; eager launches "
                          "measure faster since the conv weight gradients overlap on a second stream)")
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--gelu", default=None, choices=["fitted", "exact"],
+                    help="GELU core of the fused kernels (default: PBX_GELU or fitted): fitted = logistic fit "
+                         "(max |err| 2.9e-4); exact = the erf form of the reference's nn.GELU()")
     ap.add_argument("--semantics", default="reference", choices=["reference", "paper"],
                     help="paper: published attention/LN/softmax (per-position LayerNorm, softmax over positions)")
     return ap.parse_args()
@@ -99,6 +102,9 @@ def main():
         print(f"error: --gpus {a.gpus} but WORLD_SIZE={world}: refusing to measure a different world size",
               file=sys.stderr)
         sys.exit(2)
+    if a.gelu is not None:
+        from proteinbert_pytorch_replication_amd.ops import _lib as hiplib
+        hiplib.set_gelu(a.gelu)
     info = pdist.init_distributed()
     dev = info.device
     cfg = get_preset(a.preset or ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else "cfg2_paper_l512"))
@@ -172,6 +178,8 @@ def main():
                           "impl": a.impl, "hip_graph": graphed},
                "world_size": n, "backend": info.backend if n > 1 else "single",
                "rccl_env": getattr(info, "rccl_env", None),
+               "dp_transport": ddp.transport if ddp is not None else "none",
+               "gelu": _gelu_label(a.impl),
                "device": _device_label(dev), "final_loss": round(final_loss, 5),
                # the reference reduces its loss in float64 (float64 weights, utils.py:293-294); the fused
                # heads reduce in fp32: < 1e-6 relative at this shape (tests/test_loss_precision.py)
@@ -183,7 +191,17 @@ def main():
             out["vs_baseline"] = round(value / REFERENCE_CFG1_CPU_SEQ_PER_S, 2)
             out["baseline"] = "reference modules.py cfg 1 step on an 8-core CPU (BASELINE.md)"
         print(json.dumps(out), flush=True)
+    if ddp is not None:
+        ddp.close()
     pdist.destroy()
+
+
+def _gelu_label(impl: str) -> str:
+    if impl != "hip":
+        return "exact (torch nn.GELU)"
+    from proteinbert_pytorch_replication_amd.ops import _lib as hiplib
+    return {"fitted": "fitted logistic core in the fused kernels (max |err| 2.9e-4 vs erf; --gelu exact for erf)",
+            "exact": "exact erf form (A&S 7.1.26, |err| <= 1.5e-7)"}.get(hiplib.gelu_mode(), hiplib.HIP_LIB)
 
 
 def _device_label(dev) -> str:
@@ -262,6 +280,8 @@ def finetune_bench(a, info, encoder, L, B, mcfg):
                           "global_batch": B * n, "per_gpu_batch": B, "seq_len": L, "parallelism": f"dp{n}",
                           "impl": a.impl}, "final_loss": round(float(loss.item()), 5)}
         print(json.dumps(out), flush=True)
+    if ddp is not None:
+        ddp.close()
     pdist.destroy()
 
 

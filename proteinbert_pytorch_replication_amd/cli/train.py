@@ -75,6 +75,9 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
     dev = info.device
     if cfg.kernel.deterministic:
         determinism.enable()
+    if cfg.kernel.gelu != "fitted":
+        from ..ops import _lib as _hiplib
+        _hiplib.set_gelu(cfg.kernel.gelu)
     torch.manual_seed(cfg.train.seed)
     if cfg.data.lengths:
         # multi-length schedule: the LayerNorm affine is stored at the longest L and sliced per batch
@@ -158,6 +161,9 @@ def finetune_main(argv: Optional[List[str]] = None) -> dict:
     info = pdist.init_distributed(backend=cfg.dist.backend)
     if cfg.kernel.deterministic:
         determinism.enable()
+    if cfg.kernel.gelu != "fitted":
+        from ..ops import _lib as _hiplib
+        _hiplib.set_gelu(cfg.kernel.gelu)
     dev = info.device
     torch.manual_seed(cfg.train.seed)
     if a.pretrained:

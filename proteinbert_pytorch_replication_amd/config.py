@@ -84,6 +84,7 @@ class KernelConfig:
     dtype: str = "bf16"                 # compute dtype on GPU
     hip_graph: bool = False             # capture the whole train step
     deterministic: bool = False         # bitwise-reproducible run (fixed-order HIP forms; paper semantics -> PyTorch path)
+    gelu: str = "fitted"                # fused kernels' GELU core: fitted (logistic fit, |err| 2.9e-4) | exact (erf)
 
 
 @dataclass

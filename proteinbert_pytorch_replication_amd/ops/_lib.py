@@ -13,11 +13,41 @@ from typing import Optional
 
 import torch
 
-from .build import HIP_LIB as _BUILT_HIP_LIB, HOST_LIB
+from .build import HIP_LIB as _BUILT_HIP_LIB, HIP_LIB_EXACT as _BUILT_HIP_LIB_EXACT, HOST_LIB
 
-# PBX_HIP_LIB: load an alternative build of the kernel library (A/B comparisons of kernel variants
-# inside one process launch on the same GPU); the in-tree build otherwise
-HIP_LIB = os.environ.get("PBX_HIP_LIB") or _BUILT_HIP_LIB
+GELU_MODES = ("fitted", "exact")
+
+
+def _default_lib() -> str:
+    mode = os.environ.get("PBX_GELU", "fitted")
+    if mode not in GELU_MODES:
+        raise ValueError(f"PBX_GELU={mode!r}: expected one of {GELU_MODES}")
+    return _BUILT_HIP_LIB_EXACT if mode == "exact" else _BUILT_HIP_LIB
+
+
+# The GELU core of the fused kernels: "fitted" (libpbx_hip.so, the default) or "exact" (libpbx_hip_exact.so,
+# the erf form of the reference's nn.GELU()), chosen by PBX_GELU / set_gelu() before the first kernel launch.
+# PBX_HIP_LIB: load any other build of the kernel library (A/B comparisons of kernel variants).
+HIP_LIB = os.environ.get("PBX_HIP_LIB") or _default_lib()
+
+
+def gelu_mode() -> str:
+    return "exact" if HIP_LIB == _BUILT_HIP_LIB_EXACT else ("fitted" if HIP_LIB == _BUILT_HIP_LIB else "custom")
+
+
+def set_gelu(mode: str) -> None:
+    """Select the fused kernels' GELU core ("fitted" | "exact") for this process.  Must precede the first
+    kernel launch (the library is loaded once); a later call with another mode raises."""
+    global HIP_LIB
+    if mode not in GELU_MODES:
+        raise ValueError(f"gelu mode {mode!r}: expected one of {GELU_MODES}")
+    want = _BUILT_HIP_LIB_EXACT if mode == "exact" else _BUILT_HIP_LIB
+    if want == HIP_LIB:
+        return
+    if _lib is not None:
+        raise HipError(f"set_gelu({mode!r}): the kernel library ({HIP_LIB}) is already loaded")
+    HIP_LIB = want
+    os.environ["PBX_GELU"] = mode     # child processes (DP ranks spawned later) inherit the choice
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64
@@ -29,7 +59,7 @@ _SIGS = {
     "pbx_adam_flat": [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P],
     "pbx_sumsq_flat": [_P, _I64, _P, _P, _P],
     "pbx_clip_scale_flat": [_P, _I64, _P, _F32, _P],
-    "pbx_nonfinite_flag": [_P, _I64, _P, _P, _P],
+    "pbx_nonfinite_flag": [_P, _I64, _P, _P, _F32, _I32, _P],
 }
 
 _lib: Optional[ctypes.CDLL] = None

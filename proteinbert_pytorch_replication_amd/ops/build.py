@@ -6,6 +6,10 @@
   each file is plain HIP C++ exposing ``extern "C"`` launchers that take raw
   device pointers and a ``hipStream_t`` (torch's current stream), so every
   launch is capturable in a hipGraph.
+* ``libpbx_hip_exact.so`` - the same sources with ``-DPBX_GELU_EXACT=1``: every fused
+  GELU / GELU' evaluates the erf form (A&S 7.1.26, |err| <= 1.5e-7) instead of the
+  fitted logistic core.  :mod:`._lib` loads it when ``PBX_GELU=exact`` (or the
+  ``kernel.gelu=exact`` config key) selects reference-exact activations.
 * ``libpbx_host.so``  - host-only C++ runtime pieces (``csrc/*.cpp``: the
   threaded batch builder), compiled with g++.
 
@@ -26,6 +30,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 BUILD_DIR = os.path.join(HERE, "_build")
 HIP_LIB = os.path.join(HERE, "libpbx_hip.so")
+HIP_LIB_EXACT = os.path.join(HERE, "libpbx_hip_exact.so")
+# variant -> (extra hipcc flags, library path)
+VARIANTS = {"fitted": ([], HIP_LIB), "exact": (["-DPBX_GELU_EXACT=1"], HIP_LIB_EXACT)}
 HOST_LIB = os.path.join(HERE, "libpbx_host.so")
 ARCH = "gfx950"
 
@@ -63,26 +70,28 @@ def hip_flags() -> List[str]:
             "-ffp-contract=fast", "-fno-slp-vectorize", "-Wno-unused-result", "-I", CSRC]
 
 
-def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
+def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8, variant: str = "fitted") -> str:
     hipcc = _hipcc()
-    os.makedirs(BUILD_DIR, exist_ok=True)
+    extra, lib = VARIANTS[variant]
+    bdir = BUILD_DIR if variant == "fitted" else os.path.join(BUILD_DIR, variant)
+    os.makedirs(bdir, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     objs = []
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(BUILD_DIR, os.path.basename(src) + ".o")
+        obj = os.path.join(bdir, os.path.basename(src) + ".o")
         if force or not _newer(obj, [src] + headers):
-            _run([hipcc, *hip_flags(), "-c", src, "-o", obj], verbose)
+            _run([hipcc, *hip_flags(), *extra, "-c", src, "-o", obj], verbose)
         return obj
 
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         objs = list(ex.map(compile_one, srcs))
-    if force or not _newer(HIP_LIB, objs):
-        tmp = HIP_LIB + ".tmp"
+    if force or not _newer(lib, objs):
+        tmp = lib + ".tmp"
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp, *objs], verbose)
-        os.replace(tmp, HIP_LIB)
-    return HIP_LIB
+        os.replace(tmp, lib)
+    return lib
 
 
 def build_host(verbose: bool = False, force: bool = False) -> str:
@@ -99,7 +108,8 @@ def build_host(verbose: bool = False, force: bool = False) -> str:
 
 
 def build_all(verbose: bool = False, force: bool = False, jobs: int = 8) -> None:
-    build_hip(verbose, force, jobs)
+    for v in VARIANTS:
+        build_hip(verbose, force, jobs, v)
     build_host(verbose, force)
 
 

@@ -44,53 +44,22 @@ __device__ __forceinline__ float gelu_grad_f(float x) {
   return fmaf(x, p, c);
 }
 
-// Packed (2-wide) versions on v_pk_fma_f32 / v_pk_mul_f32: the polynomial, the squares and the
-// final products run two lanes' values per instruction; rcp / exp2 stay scalar (transcendental).
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void gelu_parts2(f32x2 x, f32x2& cdf, f32x2& pdf) {
-  const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
-  const f32x2 den = z * 0.3275911f + 1.0f;
-  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
-  f32x2 pl = __builtin_elementwise_fma(t, (f32x2){1.061405429f, 1.061405429f}, (f32x2){-1.453152027f, -1.453152027f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){1.421413741f, 1.421413741f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){-0.284496736f, -0.284496736f});
-  pl = __builtin_elementwise_fma(t, pl, (f32x2){0.254829592f, 0.254829592f});
-  pl = pl * t;
-  const f32x2 q = (z * z) * -1.4426950408889634f;          // -z^2 log2(e)
-  const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-  const f32x2 erfz = __builtin_elementwise_fma(-pl, e, (f32x2){1.0f, 1.0f});
-  const f32x2 se = {copysignf(erfz.x, x.x), copysignf(erfz.y, x.y)};
-  cdf = __builtin_elementwise_fma(se, (f32x2){0.5f, 0.5f}, (f32x2){0.5f, 0.5f});
-  pdf = e * 0.3989422804014327f;
-}
-#ifndef PBX_PACKED_GELU
-// Beside MFMAs packed f32 VALU is an anti-lever on gfx950 (a v_pk_fma_f32 costs ~22 cycles more per
-// MFMA gap than two v_fma_f32, MI355X_MICROARCH.md): the 2-wide entry points run scalar code.
-__device__ __forceinline__ f32x2 gelu2(f32x2 x) { return (f32x2){gelu_f(x.x), gelu_f(x.y)}; }
-__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) { return (f32x2){gelu_grad_f(x.x), gelu_grad_f(x.y)}; }
-#else
-__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
-  f32x2 c, p;
-  gelu_parts2(x, c, p);
-  return x * c;
-}
-__device__ __forceinline__ f32x2 gelu_grad2(f32x2 x) {
-  f32x2 c, p;
-  gelu_parts2(x, c, p);
-  return __builtin_elementwise_fma(x, p, c);
-}
+
+// The fused kernels' GELU cores come in two builds of the same sources (ops/build.py):
+//   libpbx_hip.so        the fitted logistic core below (max |err| 2.9e-4 in GELU, 7.8e-4 in GELU', below the
+//                        bf16 rounding of every stored value; 7 / 11 VALU per GELU / GELU + GELU')
+//   libpbx_hip_exact.so  -DPBX_GELU_EXACT: the A&S 7.1.26 erf core (|err| <= 1.5e-7, the reference's exact
+//                        nn.GELU() up to fp32 rounding; 14 / 15 VALU), selected at run time by PBX_GELU=exact
+//                        or the `kernel.gelu=exact` config key
+#ifndef PBX_GELU_EXACT
+#define PBX_GELU_EXACT 0
 #endif
 
-// Packed GELU / GELU' for VALU-bound epilogues (the attention pool: one GELU per element of a
-// [rows, 512] GEMM output, ~13 VALU + 2 transcendentals each, 3-4x the MFMA time of the GEMM).
-// A&S 7.1.26 erf, arranged so every non-transcendental step is one v_pk_* instruction for two
-// values:  gelu(x) = 0.5 x + |x| * h,  h = 0.5 erf(|x|/sqrt2) = 0.5 - 0.5 t P(t) e  (the -0.5 is
-// folded into the polynomial coefficients), e = exp(-x^2 / 2), t = 1 / (1 + p |x| / sqrt2).
-
-// Scalar form of the interleaved cores below: the same A&S stages on 2N independent scalars, one
-// v_fma_f32 per value per stage.  Beside in-flight MFMAs a v_pk_*_f32 costs far more than its two
-// scalar halves (MI355X_MICROARCH.md constants table), and these cores run in the shadow of the MFMAs
-// of the next tile.  (Needs -fno-slp-vectorize, or the SLP vectoriser packs the halves again.)
+// A&S 7.1.26 erf core on 2N independent scalars, stage by stage (every stage of all values before the
+// next, so the transcendental latencies and dependent-op slots are filled).  Scalar on purpose: beside
+// in-flight MFMAs a v_pk_*_f32 costs far more than its two scalar halves (MI355X_MICROARCH.md constants
+// table), and the build passes -fno-slp-vectorize so the halves stay scalar.
 template <int N, int MODE>   // MODE 0: GELU, 1: GELU', 2: both (g and gd)
 __device__ __forceinline__ void gelu_scalar_n(const f32x2* x, f32x2* g, f32x2* gd) {
   constexpr int M = 2 * N;
@@ -179,127 +148,20 @@ __device__ __forceinline__ void gelu_logistic_n(const f32x2* x, f32x2* g, f32x2*
   }
 }
 
-// N independent pairs evaluated stage by stage (every stage of all N before the next): the
-// one-pair forms above compile to a serial dependency chain with an s_nop between dependent packed
-// ops; N interleaved chains fill those slots and the transcendental latencies.
+// The build's GELU core on N independent pairs (MODE 0: GELU, 1: GELU', 2: both)
+template <int N, int MODE>
+__device__ __forceinline__ void gelu_n(const f32x2* x, f32x2* g, f32x2* gd) {
+  if constexpr (PBX_GELU_EXACT) gelu_scalar_n<N, MODE>(x, g, gd);
+  else gelu_logistic_n<N, MODE>(x, g, gd);
+}
 template <int N, bool GRAD>
 __device__ __forceinline__ void gelu2_fast_n(const f32x2* x, f32x2* out) {
-#ifdef PBX_ABL_NOGELU   // ablation builds only (tools/ubench/build_flags.sh): the cost of the GELU chains
-#pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = x[i] * 0.5f;
-  return;
-#endif
-#ifndef PBX_GELU_ERF   // default: the fitted logistic core (A/B builds with -DPBX_GELU_ERF keep the erf forms)
-  if (GRAD) gelu_logistic_n<N, 1>(x, nullptr, out);
-  else gelu_logistic_n<N, 0>(x, out, nullptr);
-  return;
-#endif
-#ifdef PBX_SCALAR_GELU
-  if (GRAD) gelu_scalar_n<N, 1>(x, nullptr, out);
-  else gelu_scalar_n<N, 0>(x, out, nullptr);
-  return;
-#endif
-  // GRAD: e = phi(x) with the Zelen-Severo coefficients (see gelu2_both_n), GELU' = Phi + x e
-  constexpr float q1 = GRAD ? -1.3257480647361592f : 0.0f;
-  constexpr float c5 = GRAD ? -1.3302744295891233f : -0.5307027145f;
-  constexpr float c4 = GRAD ? 1.8212559791077754f : 0.7265760135f;
-  constexpr float c3 = GRAD ? -1.7814779365698128f : -0.7107068705f;
-  constexpr float c2 = GRAD ? 0.3565637812489156f : 0.142248368f;
-  constexpr float c1 = GRAD ? -0.31938153025994087f : -0.127414796f;
-  f32x2 ax[N], t[N], e[N], pl[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    ax[i] = __builtin_elementwise_abs(x[i]);
-    t[i] = __builtin_elementwise_fma(ax[i], (f32x2){0.23164190f, 0.23164190f}, (f32x2){1.0f, 1.0f});
-    if (GRAD)
-      e[i] = __builtin_elementwise_fma(x[i] * x[i], (f32x2){-0.72134752044448170f, -0.72134752044448170f},
-                                       (f32x2){q1, q1});
-    else
-      e[i] = (x[i] * -0.72134752044448170f) * x[i];
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    t[i] = (f32x2){__builtin_amdgcn_rcpf(t[i].x), __builtin_amdgcn_rcpf(t[i].y)};
-    e[i] = (f32x2){__builtin_amdgcn_exp2f(e[i].x), __builtin_amdgcn_exp2f(e[i].y)};
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], (f32x2){c5, c5}, (f32x2){c4, c4});
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c3, c3});
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c2, c2});
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){c1, c1});
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(pl[i] * t[i], e[i], (f32x2){0.5f, 0.5f});   // h
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    if (GRAD) {
-      const f32x2 Phi = (f32x2){copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)} + 0.5f;
-      out[i] = __builtin_elementwise_fma(x[i], e[i], Phi);
-    } else {
-      out[i] = __builtin_elementwise_fma(ax[i], pl[i], x[i] * 0.5f);
-    }
-  }
+  if (GRAD) gelu_n<N, 1>(x, nullptr, out);
+  else gelu_n<N, 0>(x, out, nullptr);
 }
-
-// GELU AND GELU' of N independent pairs from one shared erf / exp evaluation (same stages as
-// gelu2_fast_n): a producer that needs the activation now and its derivative later (stored for the
-// backward) pays ~5 extra packed ops per pair instead of a second core.
 template <int N>
 __device__ __forceinline__ void gelu2_both_n(const f32x2* x, f32x2* g, f32x2* gd) {
-#ifdef PBX_ABL_NOGELU
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    g[i] = x[i] * 0.5f;
-    gd[i] = x[i] * 0.25f;
-  }
-  return;
-#endif
-#ifndef PBX_GELU_ERF
-  gelu_logistic_n<N, 2>(x, g, gd);
-  return;
-#endif
-#ifdef PBX_SCALAR_GELU
-  gelu_scalar_n<N, 2>(x, g, gd);
-  return;
-#endif
-  // e = phi(x) (the 1/sqrt(2 pi) folded into the exponent and the polynomial: Zelen-Severo form of
-  // the same A&S 7.1.26 erf), Phi = 0.5 + sign(x) h, GELU = x Phi, GELU' = Phi + x phi: 13 VALU + 2 T
-  f32x2 t[N], e[N], pl[N];
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    t[i] = __builtin_elementwise_fma(__builtin_elementwise_abs(x[i]), (f32x2){0.23164190f, 0.23164190f},
-                                     (f32x2){1.0f, 1.0f});
-    e[i] = __builtin_elementwise_fma(x[i] * x[i], (f32x2){-0.72134752044448170f, -0.72134752044448170f},
-                                     (f32x2){-1.3257480647361592f, -1.3257480647361592f});
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    t[i] = (f32x2){__builtin_amdgcn_rcpf(t[i].x), __builtin_amdgcn_rcpf(t[i].y)};
-    e[i] = (f32x2){__builtin_amdgcn_exp2f(e[i].x), __builtin_amdgcn_exp2f(e[i].y)};
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], (f32x2){-1.3302744295891233f, -1.3302744295891233f},
-                                      (f32x2){1.8212559791077754f, 1.8212559791077754f});
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-1.7814779365698128f, -1.7814779365698128f});
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){0.3565637812489156f, 0.3565637812489156f});
-#pragma unroll
-  for (int i = 0; i < N; ++i)
-    pl[i] = __builtin_elementwise_fma(t[i], pl[i], (f32x2){-0.31938153025994087f, -0.31938153025994087f});
-#pragma unroll
-  for (int i = 0; i < N; ++i) pl[i] = __builtin_elementwise_fma(pl[i] * t[i], e[i], (f32x2){0.5f, 0.5f});   // h
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const f32x2 Phi = (f32x2){copysignf(pl[i].x, x[i].x), copysignf(pl[i].y, x[i].y)} + 0.5f;
-    g[i] = x[i] * Phi;
-    gd[i] = __builtin_elementwise_fma(x[i], e[i], Phi);
-  }
+  gelu_n<N, 2>(x, g, gd);
 }
 
 __device__ __forceinline__ float wave_reduce_sum(float v) {

@@ -26,9 +26,6 @@ typedef unsigned short bf16_t;
 namespace {
 constexpr int CH = 128;
 constexpr int BM = 128;               // positions per workgroup
-#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/convstamps.py)
-__device__ unsigned long long pbx_conv_stamps[4096 * 8 * 4];   // [workgroup][wave][stage, loop, epilogue, t0]
-#endif
 constexpr int FRAG = 64 * 8;          // bf16 per packed fragment (64 lanes x 8)
 constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging tile
 
@@ -36,14 +33,10 @@ constexpr int OT = BM * 256;          // bytes of one [BM][128] bf16 staging til
 // (blockIdx % 8 labels the blocks that share an XCD's L2), so the bijective remap
 // (cdna_hip_programming.md T1) gives each XCD a contiguous run of tiles: neighbouring tiles of one
 // sample, whose +-20-row halos overlap, then read those rows through the same L2.  +0.5 % on the step,
-// 6/6 same-box rounds (profiles/r2_v8_xcd_remap_ab.txt); -DPBX_NO_XCD_REMAP builds the identity map.
+// 6/6 same-box rounds against the identity map (profiles/r2_v8_xcd_remap_ab.txt).
 __device__ __forceinline__ int tile_id() {
-#ifndef PBX_NO_XCD_REMAP
   const int n = gridDim.x, orig = blockIdx.x, xcd = orig & 7, q = n >> 3, r = n & 7;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
-#else
-  return blockIdx.x;
-#endif
 }
 
 // Packed fragment index (in fragments) of (tap k, K-block kb of 16, M-block mb of 32); lane offset
@@ -75,9 +68,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   unsigned char* ot = smem + XR * 256;                        // [TBM][128] bf16 staging tile
   float* bsm = reinterpret_cast<float*>(ot + TOT);            // bn | bw | gb[b] | LN scratch
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
-#ifdef PBX_STAMPS
-  const unsigned long long cs0 = __builtin_amdgcn_s_memtime();
-#endif
   const int r = lane & 31, h = lane >> 5;
   const int cv = w >> 2, cq = w & 3;
   // xlo / xhi: rows of the neighbouring sequence shards stored around each sample's L rows (context
@@ -106,9 +96,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
       },
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(xs + swz256(idx >> 4, idx & 15)) = v; });
   __syncthreads();
-#ifdef PBX_STAMPS
-  const unsigned long long cs1 = __builtin_amdgcn_s_memtime();
-#endif
 
   f32x16_t acc[NPT];
 #pragma unroll
@@ -118,22 +105,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
   // chunk 2 kb + h) is rowb + 8192 pt + ((32 kb) ^ gs) with rowb / gs fixed per tap, so a step costs one
   // v_xad_u32 instead of the ~7 VALU of the general swizzle; the weight fragment address is a scalar
   // base + the lane offset (no per-step 64-bit vector add)
-#ifdef PBX_CONV_BPF0   // ablation: B fragments read right before their MFMAs (round-3 form)
-  for (int k = 0; k < KS; ++k) {
-    const int rb = halo + r + (k - half) * d;
-    const int rowb = rb << 8, gs = (h ^ (((rb & 3) << 2) | ((rb >> 2) & 3))) << 4;
-#pragma unroll
-    for (int kb = 0; kb < 8; ++kb) {
-      const int it = k * 8 + kb;
-      const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;
-      fr[(kb + 3) & 3] = fwk[lane];
-      __builtin_amdgcn_sched_barrier(0);
-      const int off = ((32 * kb) ^ gs) + rowb;
-#pragma unroll
-      for (int pt = 0; pt < NPT; ++pt) acc[pt] = mfma32(fr[kb & 3], lds_frag(xs, off + pt * 8192), acc[pt]);
-    }
-  }
-#else
   // B fragments (the x rows) are read one K-step ahead into a 2-deep register ring, so an MFMA never
   // waits on the LDS read issued right before it (the previous form read them in front of their own
   // MFMAs: an s_waitcnt lgkmcnt per MFMA pair, the LDS latency exposed on every step)
@@ -153,11 +124,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
 #pragma unroll
     for (int kb = 0; kb < 8; ++kb) {
       const int it = k * 8 + kb;
-#ifdef PBX_ABL_AFIX   // ablation builds only: 4 weight fragments reused (L1-resident) -- the L2 weight stream's cost
-      const bf16x8* fwk = fw + ((it + 3) & 3) * 256;
-#else
       const bf16x8* fwk = fw + min(it + 3, NI - 1) * 256;   // scalar base
-#endif
       fr[(kb + 3) & 3] = fwk[lane];
       const int noff = kb < 7 ? ((32 * (kb + 1)) ^ gs) + rowb : (0 ^ gsn) + rowbn;
 #pragma unroll
@@ -169,11 +136,7 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     rowb = rowbn;
     gs = gsn;
   }
-#endif
 
-#ifdef PBX_STAMPS
-  const unsigned long long cs2 = __builtin_amdgcn_s_memtime();
-#endif
   // ---- epilogue: acc[pt][4g + e] = (co = cq*32 + 8g + 4h + e, pos = pt*32 + r) ------------------
   // Both pre-activation tiles are staged in LDS (narrow -> ot, wide -> over the x tile, whose 4 rows
   // per thread are read into registers first), then all 512 threads take 4 (row, 16-B chunk) units
@@ -231,15 +194,11 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     // scalar GELU stages: this epilogue runs beside the other waves' MFMAs, where packed-fp32 forms measured
     // slower.  Training: GELU AND GELU' from one shared core; GELU' is what the data gradient multiplies by,
     // so it is stored instead of the pre-activation and the data gradient evaluates no GELU' core
-#ifdef PBX_GELU_ERF   // A/B builds only: the A&S erf core (15 VALU per GELU + GELU', 14 per GELU)
-#define CONV_GELU gelu_scalar_n
-#else                       // fitted logistic core (common.h: 11 / 7 VALU, |err| <= 7.8e-4 / 2.9e-4)
-#define CONV_GELU gelu_logistic_n
-#endif
+    // (gelu_n: the fitted logistic core, or the A&S erf core in the exact-GELU library -- common.h)
     if constexpr (STORE) {
       f32x2 gd[8];
-      CONV_GELU<4, 2>(gi, go, gd);
-      CONV_GELU<4, 2>(gi + 4, go + 4, gd + 4);
+      gelu_n<4, 2>(gi, go, gd);
+      gelu_n<4, 2>(gi + 4, go + 4, gd + 4);
       float dn[8], dw[8];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -253,10 +212,9 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
         *reinterpret_cast<uint4*>(pre_w + off) = packq8(dw);
       }
     } else {
-      CONV_GELU<4, 0>(gi, go, nullptr);
-      CONV_GELU<4, 0>(gi + 4, go + 4, nullptr);
+      gelu_n<4, 0>(gi, go, nullptr);
+      gelu_n<4, 0>(gi + 4, go + 4, nullptr);
     }
-#undef CONV_GELU
     float o[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -290,14 +248,6 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     stats[((size_t)b * T + t) * 2] = m;
     stats[((size_t)b * T + t) * 2 + 1] = fmaxf(sq - sa * m, 0.f);
   }
-#ifdef PBX_STAMPS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const unsigned long long cs3 = __builtin_amdgcn_s_memtime();
-  if (lane == 0) {
-    unsigned long long* o = pbx_conv_stamps + ((size_t)(blockIdx.x & 4095) * 8 + w) * 4;
-    o[0] = cs1 - cs0; o[1] = cs2 - cs1; o[2] = cs3 - cs2; o[3] = cs0;
-  }
-#endif
 }
 
 // fp32 torch conv weight [co][ci][KS] -> bf16 fragment images: fwd[k][kb][mb][lane][8] with
@@ -350,12 +300,6 @@ static int conv_fwd3_launch(const void* x, const long long* tok, const void* emb
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_conv_fwd3(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
-                             const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
-                             int dil, hipStream_t st) {
-  return conv_fwd3_launch(x, nullptr, nullptr, fwn, fww, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, 0, 0, st);
-}
-
 // context-parallel form: x holds xlo / xhi halo rows of the neighbouring shards around each sample's L rows
 PBX_EXPORT int pbx_conv_fwd3x(const void* x, const void* fwn, const void* fww, const float* bn, const float* bw,
                               const float* gb, void* pre_n, void* pre_w, void* s1, float* stats, int B, int L, int KS,
@@ -365,7 +309,7 @@ PBX_EXPORT int pbx_conv_fwd3x(const void* x, const void* fwn, const void* fww, c
 }
 
 // The first block (reference modules.py:249-253,300 feeding :185-212): x = emb[tok] gathered in the
-// staging pass (tok [B][L] int64 < V, emb [V][128] bf16); otherwise pbx_conv_fwd3.
+// staging pass (tok [B][L] int64 < V, emb [V][128] bf16); otherwise pbx_conv_fwd3x.
 PBX_EXPORT int pbx_conv_fwd3t(const long long* tok, const void* emb, const void* fwn, const void* fww, const float* bn,
                               const float* bw, const float* gb, void* pre_n, void* pre_w, void* s1, float* stats,
                               int B, int L, int KS, int dil, hipStream_t st) {
@@ -381,8 +325,3 @@ PBX_EXPORT int pbx_pack_conv_frag(const float* w, void* pf, void* pt, int KS, hi
   return pbx_launch_status();
 }
 
-#ifdef PBX_STAMPS
-PBX_EXPORT int pbx_conv_stamps_read(unsigned long long* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_conv_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-#endif

@@ -18,9 +18,6 @@ constexpr int BM = 128;              // positions per tile
 constexpr int KS = 9;                // taps (the launcher refuses other sizes)
 constexpr int NI = KS * 8;           // K-steps per tile (taps x 16-channel blocks)
 constexpr int NPT = BM / 32;         // 32-position MFMA tiles per wave
-#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/dgradstamps.py)
-__device__ unsigned long long pbx_dgrad_stamps[4096 * 4 * 4];   // [workgroup][wave][prologue, loop, epilogue, -]
-#endif
 
 
 // ------------------------------------------------------------------------------------------------
@@ -71,9 +68,6 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
   unsigned char* an = smem;                       // RN x 256 B: dpre of the narrow conv (swz256)
   unsigned char* aw = smem + RN * 256;            // (BM + 2 halo_w) x 256 B: wide conv
   const int tid = threadIdx.x, lane = tid & 63, cq = __builtin_amdgcn_readfirstlane(tid >> 6);
-#ifdef PBX_STAMPS
-  const unsigned long long dst0 = __builtin_amdgcn_s_memtime();
-#endif
   const int r = lane & 31, h = lane >> 5;
   const size_t sbase = (size_t)b * L * CH;                          // outputs: [B][L][128]
   const ptrdiff_t ibase = ((ptrdiff_t)b * (L + ilo + ihi) + ilo) * CH;   // inputs: logical position 0
@@ -83,11 +77,7 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
       const_cast<bf16x8*>(ftw + cq * 64), (short)0, (NI * 4 - cq) * 1024, 0x00020000);
   auto wfrag = [&](int it) {      // K-step it of 2 NI: narrow image for it < NI, then the wide one
     typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-#ifdef PBX_ABL_AFIX   // ablation builds only: 4 weight fragments reused (L1-resident) -- the L2 weight stream's cost
-    const int li = it & 3;
-#else
     const int li = it < NI ? it : it - NI;
-#endif
     const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(it < NI ? rn : rw, lane * 16, li * 4096, 0);
     return __builtin_bit_cast(bf16x8, v);
   };
@@ -239,9 +229,6 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     }
   }
   __syncthreads();
-#ifdef PBX_STAMPS
-  const unsigned long long dst1 = __builtin_amdgcn_s_memtime();
-#endif
 
   f32x16_t acc[NPT];
 #pragma unroll
@@ -283,17 +270,6 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     }
   }
 
-#ifdef PBX_STAMPS
-  const unsigned long long dst2 = __builtin_amdgcn_s_memtime();
-  auto stamp_end = [&]() {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long dst3 = __builtin_amdgcn_s_memtime();
-    if (lane == 0) {
-      unsigned long long* o = pbx_dgrad_stamps + ((size_t)(blockIdx.x & 4095) * 4 + cq) * 4;
-      o[0] = dst1 - dst0; o[1] = dst2 - dst1; o[2] = dst3 - dst2; o[3] = 1;
-    }
-  };
-#endif
   // dx = ds1 + acc: the fp32 tile goes through LDS (over the dpre tiles) for row-contiguous 16-B accesses
   const int vrows = min(BM, L - pos0);
   float* ft = reinterpret_cast<float*>(smem);
@@ -340,9 +316,6 @@ __global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
       for (int e = 0; e < 8; ++e) o[e] = gv[e] + fv[e];
       *reinterpret_cast<uint4*>(dx + sbase + (size_t)(pos0 + row) * CH + cc * 8) = packq8(o);
     }
-#ifdef PBX_STAMPS
-    stamp_end();
-#endif
     return;
   }
 #pragma unroll
@@ -371,7 +344,7 @@ int conv_dgrad4_lds(int dil) {
   return a > e ? a : e;
 }
 
-// KS = 9: gdn / gdw are the GELU'(pre) images the forward (pbx_conv_fwd3) stored.
+// KS = 9: gdn / gdw are the GELU'(pre) images the forward (pbx_conv_fwd3x / pbx_conv_fwd3t) stored.
 // ilo / ihi: halo rows of ds1 and GELU' from the neighbouring shards (context parallelism; both inputs
 // [B][ilo + L + ihi][128]); outputs dx, dpre_n, dpre_w are [B][L][128].  0 / 0 for a whole sequence.
 PBX_EXPORT int pbx_conv_dgrad4x(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
@@ -391,7 +364,7 @@ PBX_EXPORT int pbx_conv_dgrad4x(const void* ds1, const void* gdn, const void* gd
   return pbx_launch_status();
 }
 
-// pbx_conv_dgrad4 with the LayerNorm-1 backward finalize fused in (see FinArgs): dh1 / s1 [B][L][128]
+// pbx_conv_dgrad4x with the LayerNorm-1 backward finalize fused in (see FinArgs): dh1 / s1 [B][L][128]
 // bf16, st1 [B][T1][2] / sums1 [B][TS1][2] the LN1 statistics and backward partials (as
 // pbx_ln1_finalize), g1 [L][128]; dgb [B][128] accumulated.  dS1 itself is not written.
 PBX_EXPORT int pbx_conv_dgrad4f(const void* dh1, const void* s1, const float* st1, int T1, int BM1, const float* sums1,
@@ -414,13 +387,3 @@ PBX_EXPORT int pbx_conv_dgrad4f(const void* dh1, const void* s1, const float* st
   return pbx_launch_status();
 }
 
-PBX_EXPORT int pbx_conv_dgrad4(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
-                               void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, hipStream_t st) {
-  return pbx_conv_dgrad4x(ds1, gdn, gdw, ftn, ftw, dx, dpre_n, dpre_w, B, L, KS_, dil, 0, 0, st);
-}
-
-#ifdef PBX_STAMPS
-PBX_EXPORT int pbx_dgrad_stamps_read(unsigned long long* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_dgrad_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-#endif

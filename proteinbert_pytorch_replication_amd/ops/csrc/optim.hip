@@ -123,42 +123,50 @@ PBX_EXPORT int pbx_sumsq_flat(const float* x, int64_t n, float* workspace, float
 // ---- non-finite gradient flag (the fused Adam kernel skips the update when it is set) ----------
 // One partial pass (per-block "any NaN / Inf", v - v != 0 exactly for those) and a one-block OR:
 // replaces torch.isfinite(grad.sum()) (a 70 MB reduction plus five one-element kernels per step).
-__global__ void __launch_bounds__(256) nonfinite_partial_kernel(const float* __restrict__ x, int64_t n,
+// Non-finite test: an element is bad when it is NaN / Inf or |x| >= bound (!(|x| < bound) is true for NaN).
+// The DP step passes bound = FLT_MAX / world, so no sum of accepted per-rank values can overflow fp32.
+__global__ void __launch_bounds__(256) nonfinite_partial_kernel(const float* __restrict__ x, int64_t n, float bound,
                                                                 int* __restrict__ partial) {
   __shared__ int red[4];
-  float acc = 0.f;                                  // stays 0 unless some element is NaN / Inf
+  bool bad = false;
   const int64_t n4 = n >> 2;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const float4 a = reinterpret_cast<const float4*>(x)[i];
-    acc += ((a.x - a.x) + (a.y - a.y)) + ((a.z - a.z) + (a.w - a.w));
+    const float m = fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w)));   // NaN-free max
+    bad |= !(m < bound) || (a.x != a.x) || (a.y != a.y) || (a.z != a.z) || (a.w != a.w);
   }
   const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t < n && blockIdx.x * blockDim.x + threadIdx.x < 4) acc += x[t] - x[t];
-  const int bad = __any(acc != 0.f) ? 1 : 0;
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bad;
+  if (t < n && blockIdx.x * blockDim.x + threadIdx.x < 4) bad |= !(fabsf(x[t]) < bound);
+  const int wb = __any(bad) ? 1 : 0;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = wb;
   __syncthreads();
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] | red[1] | red[2] | red[3];
 }
 
 __global__ void __launch_bounds__(256) nonfinite_final_kernel(const int* __restrict__ partial, int nb,
-                                                              int* __restrict__ flag) {
+                                                              int* __restrict__ flag, int accumulate) {
   __shared__ int red[4];
   int acc = 0;
   for (int i = threadIdx.x; i < nb; i += 256) acc |= partial[i];
   const int bad = __any(acc != 0) ? 1 : 0;
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = bad;
   __syncthreads();
-  if (threadIdx.x == 0) flag[0] = red[0] | red[1] | red[2] | red[3];
+  if (threadIdx.x == 0) {
+    const int v = red[0] | red[1] | red[2] | red[3];
+    flag[0] = accumulate ? (flag[0] | v) : v;
+  }
 }
 
-// workspace must hold 1024 ints; flag: one int32 (1 when any element of x is NaN or Inf)
-PBX_EXPORT int pbx_nonfinite_flag(const float* x, int64_t n, int* workspace, int* flag, hipStream_t stream) {
+// workspace must hold 1024 ints; flag: one int32, set to (accumulate: OR-ed with) 1 when any element of x
+// is NaN / Inf or has |x| >= bound (bound = FLT_MAX: exactly the non-finite test)
+PBX_EXPORT int pbx_nonfinite_flag(const float* x, int64_t n, int* workspace, int* flag, float bound, int accumulate,
+                                  hipStream_t stream) {
   int64_t blocks = ((n >> 2) + 255) / 256;
   if (blocks > 1024) blocks = 1024;
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(nonfinite_partial_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, workspace);
-  hipLaunchKernelGGL(nonfinite_final_kernel, dim3(1), dim3(256), 0, stream, workspace, (int)blocks, flag);
+  hipLaunchKernelGGL(nonfinite_partial_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, bound, workspace);
+  hipLaunchKernelGGL(nonfinite_final_kernel, dim3(1), dim3(256), 0, stream, workspace, (int)blocks, flag, accumulate);
   return pbx_launch_status();
 }
 

@@ -13,7 +13,7 @@
 //     into a swizzled LDS image; a workgroup owns ONE 32-position tile and walks a group of samples, so
 //     the tile's [L, C] LayerNorm affine rows are staged into the remaining LDS once as well;
 //   * forward: s2 rows -> LN2 apply (fp32 affine from LDS) -> h2 (stored: block output) -> MFMA against
-//     Wv -> GELU (logistic form fitted to the erf GELU, see PBX_POOL_GELU_FAST) -> column sums, all in
+//     Wv -> GELU (logistic form fitted to the erf GELU; the A&S erf form in the exact-GELU build) -> column sums, all in
 //     registers (no ln2_apply pass, no GELU' store);
 //   * backward: h2 rows -> zT = Wv h2^T (MFMA) -> u = dv * GELU'(zT) on the VALU -> dh2^T += Wv^T u (MFMA).
 //     The D layout of zT (lane = position, rows 8 g + 4 h + e of a 32-row block) IS the B operand of the
@@ -64,15 +64,16 @@ __device__ __forceinline__ void pin8(float* a) {
   asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]), "+v"(a[7]));
 }
 
-// Backward operand type: PBX_POOL_F16 (default) runs both backward GEMMs on v_mfma_f32_32x32x16_f16 with an f16
+// Backward operand type.  Fitted-GELU build: both backward GEMMs run on v_mfma_f32_32x32x16_f16 with an f16
 // Wv image, so GELU' is evaluated on packed-f16 VALU (v_pk_* f16: two values per ~4-cycle issue slot instead of
 // one per fp32 instruction) and u = dv GELU' is the f16 B operand as it stands.  dv is scaled per sample by a
 // power of two (max |dv| -> [0.5, 1)) so u stays in the f16 normal range; the epilogue undoes it exactly.
-#ifndef PBX_POOL_F16
-#define PBX_POOL_F16 1
-#endif
+// Entries of u more than 2^14 below the sample's max |dv| lose precision as f16 subnormals and 2^24 below it
+// flush to zero: an absolute error <= 2^-24 max |dv| per term, far below the bf16 rounding of dh2
+// (tests/test_hip_pool.py, dv spanning 1e-6 .. 1).  Exact-GELU build (PBX_GELU_EXACT): bf16 operands and the
+// A&S erf GELU' in fp32.
 typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
 typedef __attribute__((ext_vector_type(8))) _Float16 opx8;
 __device__ __forceinline__ f32x16_t mfma_b(const opx8& a, const opx8& b, const f32x16_t& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -116,23 +117,10 @@ __device__ __forceinline__ void pinh4(h2_t* a) {
   asm volatile("" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]));
 }
 
-// GELU cores (measured on one box, B = 1024, L = 512, round 5; tools/ubench/pool_run3.sh):
-//   forward : A&S-erf 203-206 us | 2-term logistic (default, max |err| 2.9e-4, vpart rel 1.2e-4) 159 us |
-//             3-term logistic (2.9e-5) 177-182 us | no GELU at all (ablation) 114 us
-//   backward: A&S-erf GELU' 294-296 us | tanh-form GELU' (default, max |err| 8.7e-4, below the bf16 rounding
-//             of u = dv GELU') 275-279 us | no GELU' (ablation) 232 us
-#ifndef PBX_POOL_GELU_TANH
-#define PBX_POOL_GELU_TANH 1
-#endif
-#ifndef PBX_POOL_GELU_FAST
-#define PBX_POOL_GELU_FAST 1
-#endif
-#ifndef PBX_ABL_NOGELU   // ablation builds only
-#define PBX_ABL_NOGELU 0
-#endif
-#ifdef PBX_STAMPS       // instrumented builds only (-DPBX_STAMPS)
-__device__ unsigned long long pbx_pool_stamps[256 * 64 * 8 * 4];   // [workgroup][wave][wait, loop, epi, n]
-#endif
+// GELU cores (measured on one box, B = 1024, L = 512, round 5, profiles/r5/pool_gelu_cores_ab.txt):
+//   forward : A&S-erf 203-206 us (exact build) | 2-term logistic (max |err| 2.9e-4, vpart rel 1.2e-4) 159 us |
+//             no GELU at all (ablation, removed) 114 us
+//   backward: A&S-erf GELU' 294-296 us (exact build) | f16 logistic GELU' 245 us alone
 
 // sample range of workgroup row blockIdx.y
 __device__ __forceinline__ void sample_range(int B, int& b0, int& b1) {
@@ -266,32 +254,16 @@ __global__ void __launch_bounds__(64 * NWV) pool_fwd_kernel(
       asm volatile("" : "+v"(cn));                                      \
       wf[kk] = lds_frag(nb, swz256(r, (kk) * 2 + h));                   \
       __builtin_amdgcn_sched_barrier(0);
-#if PBX_ABL_NOGELU   // ablation builds only: the column sums of x (no GELU) -- the VALU-free bound
-      float sm = 0.f;
-      POOL_MF(0) POOL_MF(1) POOL_MF(2) POOL_MF(3) POOL_MF(4) POOL_MF(5)
-#pragma unroll
-      for (int i = 0; i < 16; ++i) sm += x[i];
-      __builtin_amdgcn_sched_barrier(0);
-      POOL_MF(6)
-#elif PBX_POOL_GELU_FAST
-      // logistic form: GELU(x) ~ x sigma(x k(t)), t = x^2, fitted (minimax on [-14, 14]) to the exact erf GELU:
-      //   1: k = 1.59934 + 0.0696829 t                          max |err| 2.9e-4, 7 VALU per value
-      //   2: k = 1.59497 + 0.0739707 t - 6.93343e-4 t^2, t <= 49  max |err| 2.9e-5, 9 VALU per value
-      // evaluated as x / (1 + exp2(-log2(e) x k(t)))
+#if !PBX_GELU_EXACT
+      // logistic form: GELU(x) ~ x sigma(x k(t)), t = x^2, k = 1.59934 + 0.0696829 t, fitted (minimax on
+      // [-14, 14]) to the exact erf GELU: max |err| 2.9e-4, 7 VALU per value; x / (1 + exp2(-log2(e) x k(t)))
       POOL_MF(0)
 #pragma unroll
       for (int i = 0; i < 16; ++i) t[i] = x[i] * x[i];
       __builtin_amdgcn_sched_barrier(0);
       POOL_MF(1)
 #pragma unroll
-#if PBX_POOL_GELU_FAST == 2
-      for (int i = 0; i < 16; ++i) {
-        const float tt = fminf(t[i], 49.0f);
-        t[i] = fmaf(tt, fmaf(tt, 0.0010002823f, -0.10671716f), -2.3010488f) * x[i];
-      }
-#else
       for (int i = 0; i < 16; ++i) t[i] = fmaf(t[i], -0.10053117f, -2.3073633f) * x[i];
-#endif
       __builtin_amdgcn_sched_barrier(0);
       POOL_MF(2)
 #pragma unroll
@@ -394,7 +366,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
   const int TW = gridDim.x;
   int b0, b1;
   sample_range(B, b0, b1);
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
   stage_chunks(
       NJ * 16, [&](int idx) { return bf16x8_to_f16x8(*reinterpret_cast<const uint4*>(wv + (size_t)idx * 8)); },
       [&](int idx, uint4 v) { *reinterpret_cast<uint4*>(ws + swz256(idx >> 4, idx & 15)) = v; });
@@ -437,18 +409,10 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       dvr[k] = *reinterpret_cast<const float4*>(dv + ((size_t)bb * dv_tiles + dv_tile) * NJ + 256 * k + 4 * lane);
   };
   load_item(b);
-#ifdef PBX_STAMPS   // instrumented builds only (tools/ubench/poolstamps.py): per-wave phase cycle totals
-  unsigned long long st_wait = 0, st_loop = 0, st_epi = 0, st_n = 0;
-#endif
   for (; b < b1; b += NWV) {
-#ifdef PBX_STAMPS
-    const unsigned long long s0 = __builtin_amdgcn_s_memtime();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long s1 = __builtin_amdgcn_s_memtime();
-#endif
     opx8 hf[8];
     const uint4 zq = make_uint4(0u, 0u, 0u, 0u);
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
 #pragma unroll
     for (int kk = 0; kk < 8; ++kk) {
       u32x4 c = __builtin_bit_cast(u32x4, bf16x8_to_f16x8(ok ? hq[kk] : zq));
@@ -488,7 +452,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       const unsigned char* ab = ws + jn * 32 * 256;
       const unsigned char* w0 = ws + 4096 * (2 * jt);
       const unsigned char* w1 = w0 + 4096;
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
       // dv of this lane's rows j = 32 jt + 8 i + 4 h + (0..3), i = 0..3: f16 pairs (j, j + 1)
       const unsigned* dvjh = reinterpret_cast<const unsigned*>(dvs) + jt * 16 + 2 * h;
       const uint2 ddh[4] = {*reinterpret_cast<const uint2*>(dvjh), *reinterpret_cast<const uint2*>(dvjh + 4),
@@ -508,15 +472,16 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       }
       zn = zero16();
       opx8 bu0, bu1;
-#if !PBX_POOL_F16
+#if PBX_GELU_EXACT
       float t[8], e[8], pl[8];
 #endif
       // GELU' stages of the 8 values of 16-step s (regs 8 s .. 8 s + 7 of zo), Zelen-Severo form of
       // A&S 7.1.26: e = phi(x), Phi = 0.5 + sign(x) h, GELU' = Phi + x phi
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
       // logistic GELU' (common.h gelu_logistic_n constants) on packed f16, 4 pairs (j, j + 1) per 16-step s:
-      //   s = 1 / (1 + exp2(x (C0 + C1 t))), t = min(x^2, 64), GELU' = s + x s (1 - s) (K0 + K1 t)
-      // (t is clamped so that 0 * inf cannot occur at |x| >= 256; at |x| >= 8 s is saturated anyway)
+      //   s = 1 / (1 + exp2(x (C0 + C1 t))), t = x^2, GELU' = s + x s (1 - s) (K0 + K1 t)
+      // x is clamped to [-8, 8] first (GELU' is saturated there: s is exactly 0 or 1 in f16), so t <= 64 and
+      // x (K0 + K1 t) stays finite: no 0 * inf, whatever the pre-activation
       h2_t xh[4], th[4], eh[4], kh[4];
       // each stage runs one operation over the 4 independent pairs before the next (a dependent packed-f16
       // op right after its producer costs an s_nop)
@@ -525,9 +490,11 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
         for (int k = 0; k < 4; ++k)
           xh[k] = __builtin_bit_cast(h2_t, __builtin_amdgcn_cvt_pkrtz(zo[8 * s + 2 * k], zo[8 * s + 2 * k + 1]));
 #pragma unroll
-        for (int k = 0; k < 4; ++k) th[k] = xh[k] * xh[k];
+        for (int k = 0; k < 4; ++k)
+          xh[k] = __builtin_elementwise_max(__builtin_elementwise_min(xh[k], (h2_t){8.0f16, 8.0f16}),
+                                            (h2_t){-8.0f16, -8.0f16});
 #pragma unroll
-        for (int k = 0; k < 4; ++k) th[k] = __builtin_elementwise_min(th[k], (h2_t){64.0f16, 64.0f16});
+        for (int k = 0; k < 4; ++k) th[k] = xh[k] * xh[k];
 #pragma unroll
         for (int k = 0; k < 4; ++k) eh[k] = th[k] * (h2_t){-0.10053117f16, -0.10053117f16} + (h2_t){-2.3073633f16, -2.3073633f16};
 #pragma unroll
@@ -562,65 +529,6 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
         }
         pinh4(u);
         return as_op(make_uint4(u_of(u[0]), u_of(u[1]), u_of(u[2]), u_of(u[3])));
-      };
-#elif PBX_ABL_NOGELU   // ablation builds only: u = dv x (no GELU') -- the VALU-free bound
-      auto stA = [&](int) {};
-      auto stB = [&]() {};
-      auto stC = [&]() {};
-      auto stD = [&]() {};
-      auto stE = [&](int s) {
-        float u[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float4 d = dd[2 * s + (i >> 2)];
-          const float dj = (i & 3) == 0 ? d.x : (i & 3) == 1 ? d.y : (i & 3) == 2 ? d.z : d.w;
-          u[i] = zo[8 * s + i] * dj;
-        }
-        pin8(u);
-        return as_op(pack8(u));
-      };
-      (void)t; (void)e; (void)pl;
-#elif PBX_POOL_GELU_TANH
-      // tanh-form GELU' (max |err| 8.7e-4 vs the erf form, below the bf16 rounding of u): sigma = 1 / (1 + e),
-      // e = exp(-2 k(x)), k(x) = c (x + 0.044715 x^3); GELU' = sigma + x k'(x) 2 sigma (1 - sigma)
-      auto stA = [&](int s) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float x = zo[8 * s + i];
-          t[i] = x * x;
-          e[i] = x * fmaf(t[i], -0.10294324f, -2.3022082f);   // -2 k(x) log2(e)
-        }
-        pin8(t);
-        pin8(e);
-      };
-      auto stB = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_exp2f(e[i]);
-        pin8(e);
-      };
-      auto stC = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) e[i] = __builtin_amdgcn_rcpf(e[i] + 1.0f);   // sigma
-        pin8(e);
-      };
-      auto stD = [&]() {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) pl[i] = fmaf(t[i], 0.21406445f, 1.5957691f);   // 2 k'(x)
-        pin8(pl);
-      };
-      auto stE = [&](int s) {
-        float u[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const float x = zo[8 * s + i];
-          const float sg = e[i];
-          const float s1 = fmaf(-sg, sg, sg);
-          const float4 d = dd[2 * s + (i >> 2)];
-          const float dj = (i & 3) == 0 ? d.x : (i & 3) == 1 ? d.y : (i & 3) == 2 ? d.z : d.w;
-          u[i] = fmaf(x * pl[i], s1, sg) * dj;
-        }
-        pin8(u);
-        return as_op(pack8(u));
       };
 #else
       auto stA = [&](int s) {
@@ -708,9 +616,6 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
     for (int q = 0; q < 16; ++q) dq[q] = *reinterpret_cast<const uint2*>(dsrc + roff + 16 * (q >> 1) + 8 * h + 4 * (q & 1));
     bstep(z1, z0, NJT - 2, NJT - 1, true);
     bstep(z0, z1, NJT - 1, NJT - 1, false);
-#ifdef PBX_STAMPS
-    const unsigned long long s2 = __builtin_amdgcn_s_memtime();
-#endif
     load_item(min(b + NWV, b1 - 1));                 // next item: in flight during the epilogue
     // dh2^T in the B-fragment layout too: y[ct][4 g + e] is channel ct*32 + 8 g + 4 h + e; a permlane32 swap
     // of the (g, g + 1) registers leaves lane half h with g = 2 m + h of both halves, i.e. channels
@@ -737,7 +642,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
       const int uo = (((2 * kk + h) ^ (rh & 15)) << 3);         // 16-B unit 2 kk + h of row rh (affy layout)
       unpack4(dq[2 * kk], din);
       unpack4(dq[2 * kk + 1], din + 4);
-#if PBX_POOL_F16
+#if !PBX_GELU_EXACT
       {
         const uint4 hb = __builtin_bit_cast(uint4, hf[kk]);     // zero past L
         const unsigned hw[4] = {hb.x, hb.y, hb.z, hb.w};
@@ -766,21 +671,7 @@ __global__ void __launch_bounds__(64 * NWV) pool_bwd_kernel(
     sa = wave_reduce_sum(ok ? sa : 0.f);
     sc = wave_reduce_sum(ok ? sc : 0.f);
     if (lane == 0) *reinterpret_cast<float2*>(sums2 + ((size_t)b * TW + tp) * 2) = make_float2(sa, sc);
-#ifdef PBX_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned long long s3 = __builtin_amdgcn_s_memtime();
-    st_wait += s1 - s0;
-    st_loop += s2 - s1;
-    st_epi += s3 - s2;
-    ++st_n;
-#endif
   }
-#ifdef PBX_STAMPS
-  if (lane == 0) {
-    unsigned long long* o = pbx_pool_stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NWV + w) * 4;
-    o[0] = st_wait; o[1] = st_loop; o[2] = st_epi; o[3] = st_n;
-  }
-#endif
 }
 
 bool pool_attrs_set = false;
@@ -841,8 +732,3 @@ PBX_EXPORT int pbx_pool_bwd(const void* h2, const float* g2, const float* be2, c
   return pbx_launch_status();
 }
 
-#ifdef PBX_STAMPS
-PBX_EXPORT int pbx_pool_stamps_read(unsigned long long* host, int n) {
-  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(pbx_pool_stamps), (size_t)n * 8, 0, hipMemcpyDeviceToHost);
-}
-#endif

@@ -376,9 +376,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
     unsigned char* nxt = smem + (((tile - t0) & 1) ^ 1) * buf_bytes;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMA of `cur` landed
     __syncthreads();                                   // ... every wave's; `nxt` no longer read
-#ifndef PBX_TOK_NOSTAGE   // ablation builds only (tools/ubench/build_flags.sh)
     if (tile + 1 < t1) stage(tile + 1, nxt);
-#endif
     // (k-step kb, tap k) steps s = kb * 9 + k: the B fragment of step s + 2 is read while the MFMA of
     // step s runs (3-slot ring); the one-hot A operand of k-step kb + 1 (A[i = v][k = src] = [tok == v],
     // lane's v = r; positions >= L were staged as token -1) is built during taps 3..7 of k-step kb
@@ -387,11 +385,7 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
     unsigned tk[8];
     auto read_b = [&](int st) {
       const unsigned char* c = cur + (st / KS) * 4096;
-#ifdef PBX_TOK_NOLDS      // ablation builds only (tools/ubench/build_flags.sh): B fragments without LDS reads
-      fb[st % 3] = __builtin_bit_cast(bf16x8, make_uint4(st, lane, 0u, 0u));
-#else
       fb[st % 3] = cat_tr(lds_tr(c, boff[st % KS]), lds_tr(c, boff4[st % KS]));
-#endif
     };
     auto read_tok = [&](int kb) {
       const unsigned* tp = reinterpret_cast<const unsigned*>(cur + toff + kb * 128);
@@ -404,9 +398,6 @@ __global__ void __launch_bounds__(512, 1) wgrad_tok_kernel(const long long* __re
 #pragma unroll
       for (int e = 0; e < 4; ++e)
         o[e] = (tk[2 * e] == (unsigned)r ? 0x3F80u : 0u) | (tk[2 * e + 1] == (unsigned)r ? 0x3F800000u : 0u);
-#ifdef PBX_TOK_NOONEHOT   // ablation builds only: a constant A operand
-      o = u32x4{0x3F80u * (unsigned)(r == kb), 0u, 0u, 0u};
-#endif
       fa[kb & 1] = __builtin_bit_cast(bf16x8, o);
     };
     read_tok(0);

@@ -31,8 +31,6 @@ from .global_track import bf16_of
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd3x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_fwd3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
-_lib.register("pbx_conv_dgrad4", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4x", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])

@@ -144,7 +144,6 @@ class PaperBlockFn(torch.autograd.Function):
         if cp is not None:
             o, lse = _cp_softmax_combine(o, lse, B, H, VD, cp)
         ctx.fused = fused
-        ctx.g32 = gf                          # fp32 (detached) g for the dWq product
         # the first block: x = bf16(emb[tok]), the conv weight gradient goes through the token one-hot
         ctx.tok = (tok, emb) if wgrad_tok_ok(tok, emb, L, KS) else None
         # emb_grad: x has no autograd history; the backward folds the conv data gradient into emb's
@@ -152,8 +151,10 @@ class PaperBlockFn(torch.autograd.Function):
         ctx.emb_grad = bool(emb_grad)
         if ctx.emb_grad and (ctx.tok is None or x.requires_grad):
             raise ValueError("emb_grad needs a token-embedding input without autograd history (wgrad_tok_ok)")
+        # gf (the fp32 g of the dWq product) is saved through autograd: when g is already fp32 it is an alias
+        # of g, and the version check then catches an in-place change of g before backward
         ctx.save_for_backward(x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, q, qs, wsave, pre, mk, o, lse,
-                              h2, wq32)
+                              h2, wq32, gf)
         ctx.cp, ctx.hlo = cp, hlo
         ctx.meta = (B, L, KS, dil, BM1, H, K, VD, ns)
         ctx.params = params
@@ -163,7 +164,7 @@ class PaperBlockFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dh2, do):
         (x_ext, pre_n, pre_w, s1, stats, wtn, wtw, wl_b, q, qs, wsave, pre, mk, o, lse, h2,
-         wq32) = ctx.saved_tensors
+         wq32, gf32) = ctx.saved_tensors
         B, L, KS, dil, BM1, H, K, VD, ns = ctx.meta
         cp, hlo = ctx.cp, ctx.hlo
         x = x_ext if cp is None else x_ext[:, hlo:hlo + L]     # this shard's rows (shape / dtype only)
@@ -201,7 +202,6 @@ class PaperBlockFn(torch.autograd.Function):
             dqs = dq_part.sum(dim=1).view(B, H, K)
             if cp is not None:
                 cp.all_reduce_(dqs)             # q is replicated: its gradient sums every shard's positions
-            gf32 = ctx.g32
             G = gf32.shape[1]
             # dg = dqpre Wq^T with dqpre = dqs (1 - q^2) / sqrt(K) formed while the operand is staged
             dg = torch.empty((B, G), dtype=F32, device=dev)

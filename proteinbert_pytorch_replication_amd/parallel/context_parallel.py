@@ -51,18 +51,24 @@ def _exchange(send_left: Optional[torch.Tensor], send_right: Optional[torch.Tens
               recv_shape, dtype, device, group) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """Send ``send_left`` to rank-1 / ``send_right`` to rank+1; receive the matching strips."""
     rank, world = _group_rank_world(group)
+    # gloo point-to-point does not order against the device stream: device strips go through host memory
+    staged = torch.device(device).type == "cuda" and dist.get_backend(group) == "gloo"
+    buf_dev = "cpu" if staged else device
     ops, from_left, from_right = [], None, None
     if rank > 0:
-        from_left = torch.empty(recv_shape, dtype=dtype, device=device)
-        ops.append(dist.P2POp(dist.isend, send_left.contiguous(), _peer(group, rank - 1), group))
+        from_left = torch.empty(recv_shape, dtype=dtype, device=buf_dev)
+        ops.append(dist.P2POp(dist.isend, send_left.contiguous().to(buf_dev), _peer(group, rank - 1), group))
         ops.append(dist.P2POp(dist.irecv, from_left, _peer(group, rank - 1), group))
     if rank < world - 1:
-        from_right = torch.empty(recv_shape, dtype=dtype, device=device)
-        ops.append(dist.P2POp(dist.isend, send_right.contiguous(), _peer(group, rank + 1), group))
+        from_right = torch.empty(recv_shape, dtype=dtype, device=buf_dev)
+        ops.append(dist.P2POp(dist.isend, send_right.contiguous().to(buf_dev), _peer(group, rank + 1), group))
         ops.append(dist.P2POp(dist.irecv, from_right, _peer(group, rank + 1), group))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+    if staged:
+        from_left = None if from_left is None else from_left.to(device)
+        from_right = None if from_right is None else from_right.to(device)
     return from_left, from_right
 
 

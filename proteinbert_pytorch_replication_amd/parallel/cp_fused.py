@@ -90,8 +90,15 @@ class CPShard:
             if x.shape != (B, Ls, C) or x.dtype != xs[0].dtype:
                 raise ValueError("halo_rows_many: tensors must share shape and dtype")
         n = len(xs)
+        dev = xs[0].device
         lo = torch.stack([x[:, :H] for x in xs]).contiguous()            # [n, B, H, C] -> left neighbour
         hi = torch.stack([x[:, Ls - H:] for x in xs]).contiguous()       # -> right neighbour
+        # gloo's point-to-point ops take the raw pointer and do not order against the device stream: a device
+        # tensor could be read before the kernel producing it (or written before its zero-fill) ran, so gloo
+        # groups (the one-GPU tests) stage the strips through host memory; RCCL orders them on its stream
+        staged = dev.type == "cuda" and dist.get_backend(self.group) == "gloo"
+        if staged:
+            lo, hi = lo.cpu(), hi.cpu()
         left = torch.zeros_like(lo)
         right = torch.zeros_like(hi)
         ops = []
@@ -104,6 +111,8 @@ class CPShard:
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
+        if staged:
+            left, right = left.to(dev), right.to(dev)
         return [torch.cat([left[i], xs[i], right[i]], dim=1).contiguous() for i in range(n)]
 
     def halo_rows(self, x: torch.Tensor) -> torch.Tensor:

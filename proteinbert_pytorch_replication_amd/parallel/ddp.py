@@ -14,39 +14,43 @@ collectives per step.
   buckets complete front-to-back; each parameter's
   ``post_accumulate_grad_hook`` counts down its bucket, and buckets are
   launched strictly in index order (every rank issues the same collective
-  sequence) as soon as they are complete — overlapping with the rest of
-  backward on RCCL's own stream.
+  sequence) as soon as they are complete, during the rest of backward.
+* Transport: on the nccl (RCCL) backend the buckets go through a direct RCCL communicator
+  (:mod:`.rccl`) whose ``ncclAllReduce`` is enqueued on the conv weight-gradient stream that produces
+  each bucket's last gradients -- no process-group stream and no event pair per bucket (the process
+  group's extra stream shared a hardware queue with the step's streams: +3.7 ms on a forced 1-rank step,
+  ``profiles/r5/dp_host_and_flags.txt``).  gloo groups (CPU tests) and ``PBX_DP_COMM=torch`` use
+  ``torch.distributed.all_reduce``.
 * ``SUM`` reduction; the 1/world factor is folded into the fused Adam
   (``FusedAdam.grad_scale``) instead of an extra pass.
 * :meth:`finish_and_step` (the training step's default with the fused Adam) hides the optimizer
   behind the exposed tail: the buckets whose gradients are final only after backward (the global input
   layer + block 0, ~20 MB) are still on the wire when the Adam update of every other bucket runs on the
-  compute stream; only the tail buckets' update trails their all-reduce.  The group-wide non-finite
-  decision is taken BEFORE any update: the tail buckets' local gradients are tested when they are
-  launched and one 4-byte MAX all-reduce of those flags is queued ahead of them; the head buckets are
-  tested after their all-reduce (a NaN / Inf on any rank survives the sum, and the reduced values are
-  identical on every rank, so no extra collective), so every rank skips or commits every bucket
-  together.  (Testing each head bucket's local gradients as it was launched put a kernel and two
-  cross-stream waits per bucket on the communication stream during backward: -48 % on a forced 1-rank
-  RCCL step, profiles/r5/dp_host_and_flags.txt.)  A sum of finite per-rank gradients that overflows fp32
-  skips the whole step when it is in the head buckets, and the tail update (with the head already
-  committed) when it appears only in the tail -- no Inf / NaN ever reaches the parameters.
+  compute stream; only the tail buckets' update trails their all-reduce.
+* Non-finite steps are skipped group-wide, decided BEFORE any update: every bucket's LOCAL gradients
+  are tested on the collective stream right before its all-reduce (one small kernel pair beside the
+  backward), with a conservative bound -- an element counts as bad when it is NaN / Inf or
+  ``|g| >= FLT_MAX / world``, so no sum of the ranks' accepted values can overflow fp32 -- and the
+  per-rank flag goes through one 4-byte MAX all-reduce queued ahead of the tail buckets.  Every rank
+  then skips or commits the whole step together (no partially applied step).
 * ``comm_dtype=torch.bfloat16`` reduces every bucket through a bf16 copy (half the xGMI bytes,
-  bf16-rounded gradient sums); the default is fp32.  (A bf16 reduction of only the last, exposed
-  bucket -- the 18 MB global input layer -- was an unmeasured option and has been removed: no
-  multi-rank run on this pool could show whether its saving beats the two conversion passes.)
+  bf16-rounded gradient sums); the default is fp32.
 """
 from __future__ import annotations
 
 import contextlib
 import os
+import warnings
 from typing import List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..ops import streams
+from . import rccl
 from ..train.arena import FlatArena, add_grad_ready_listener, remove_grad_ready_listener
+
+FLT_MAX = 3.4028234663852886e38
 
 
 class BucketedAllReduce:
@@ -92,12 +96,14 @@ class BucketedAllReduce:
         # both launched buckets before their last gradient was written
         self._ready = [False] * len(arena.params)
         self._works: List[Optional[object]] = [None] * len(self.buckets)
-        # overlapped optimizer (finish_and_step): per-bucket local non-finite flags, group-wide OR.
-        # PBX_DP_OVERLAP_OPT=0: finish() + one whole-arena update after every all-reduce (A/B knob)
+        # overlapped optimizer (finish_and_step).  PBX_DP_OVERLAP_OPT=0: finish() + one whole-arena update
+        # after every all-reduce (A/B knob)
         self.overlap_optimizer = os.environ.get("PBX_DP_OVERLAP_OPT", "1") != "0"
         self.track_nonfinite = False
-        self._flags: Optional[torch.Tensor] = None
-        self._gflag: Optional[torch.Tensor] = None
+        # bad element: NaN / Inf, or so large that the sum over the ranks could overflow fp32
+        self.nonfinite_bound = FLT_MAX / max(1, self.world)
+        self._flag: Optional[torch.Tensor] = None       # int32 [1]: this rank's flag, then the group MAX
+        self._flag_fresh = True
         self._flag_work = None
         self._nf_ws: Optional[torch.Tensor] = None
         self._tmp: List[Optional[torch.Tensor]] = [None] * len(self.buckets)
@@ -105,10 +111,24 @@ class BucketedAllReduce:
         self._hooks = []
         self.enabled = self.world > 1 or (force and dist.is_initialized())
         self._index = {id(p): i for i, p in enumerate(arena.params)}
+        self.comm: Optional[rccl.Communicator] = None
+        self._ev_head: Optional[torch.cuda.Event] = None
+        self._ev_tail: Optional[torch.cuda.Event] = None
+        self._evs = None
         if self.enabled:
+            if arena.grad.is_cuda and rccl.wanted(process_group):
+                try:
+                    self.comm = rccl.Communicator(process_group, device=arena.grad.device)
+                except Exception as e:       # noqa: BLE001 - keep training on the process-group path
+                    warnings.warn(f"direct RCCL communicator unavailable ({e}); using torch.distributed")
+                    self.comm = None
             for i, p in enumerate(arena.params):
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
             add_grad_ready_listener(self._on_direct_grads)
+
+    @property
+    def transport(self) -> str:
+        return "rccl-direct" if self.comm is not None else ("torch.distributed" if self.enabled else "none")
 
     # --------------------------------------------------------------------------------
     def _mark(self, i: int) -> None:
@@ -131,22 +151,44 @@ class BucketedAllReduce:
                 self._mark(i)
         self._launch_ready()
 
-    def _local_flag(self, b: int, view: torch.Tensor) -> None:
-        """flags[b] = 1 when this rank's gradients of bucket b hold a NaN / Inf (before the in-place
-        all-reduce overwrites them), on the stream the collective is ordered on."""
-        if self._flags is None or self._flags.device != view.device:
-            self._flags = torch.zeros(len(self.buckets), dtype=torch.int32, device=view.device)
+    def _local_flag(self, view: torch.Tensor) -> None:
+        """flag |= 1 when this rank's gradients in ``view`` hold a NaN / Inf or an element at or above
+        :attr:`nonfinite_bound` (before the in-place all-reduce overwrites them), on the current stream
+        (the one the collective is ordered on).  The first test of a step overwrites the flag."""
+        if self._flag is None or self._flag.device != view.device:
+            self._flag = torch.zeros(1, dtype=torch.int32, device=view.device)
+        acc = 0 if self._flag_fresh else 1
+        self._flag_fresh = False
         if view.is_cuda:
             from ..ops import _lib
             if self._nf_ws is None:
                 self._nf_ws = torch.empty(1024, dtype=torch.int32, device=view.device)
             _lib.call("pbx_nonfinite_flag", view.data_ptr(), view.numel(), self._nf_ws.data_ptr(),
-                      self._flags[b:].data_ptr(), _lib.stream_ptr(view.device))
+                      self._flag.data_ptr(), self.nonfinite_bound, acc, _lib.stream_ptr(view.device))
         else:
-            bad = not bool(torch.isfinite(torch.dot(view, torch.zeros_like(view))))
-            self._flags[b] = 1 if bad else 0
+            bad = 1 if view.numel() and not bool((view.abs() < self.nonfinite_bound).all()) else 0
+            self._flag[0] = bad if acc == 0 else max(int(self._flag[0]), bad)
 
-    def _launch(self, b: int, flag_done: bool = False) -> None:
+    def _all_reduce(self, t: torch.Tensor, op: str = "sum"):
+        """Enqueue an in-place all-reduce of ``t`` behind the current stream's work; returns the work
+        handle to wait for (None for the direct communicator: stream-ordered, see :meth:`_record`)."""
+        if self.comm is not None:
+            self.comm.all_reduce_(t, op)
+            return None
+        rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+        return dist.all_reduce(t, op=rop, group=self.pg, async_op=True)
+
+    def _record(self, i: int) -> Optional[torch.cuda.Event]:
+        """Event ``i`` (0: head, 1: tail; cached, re-recorded every step) after the work enqueued so far
+        on the current (collective) stream."""
+        if self.comm is None:
+            return None
+        if self._evs is None:
+            self._evs = (torch.cuda.Event(), torch.cuda.Event())
+        self._evs[i].record()
+        return self._evs[i]
+
+    def _launch(self, b: int, flag: bool = True) -> None:
         s, e = self.buckets[b]
         view = self.arena.grad[s:e]
         dt = self.comm_dtype
@@ -154,45 +196,32 @@ class BucketedAllReduce:
         # (ops/streams.py): enqueue the collective behind both streams without stalling this one
         ctx = streams.collective_stream(view.device) if view.is_cuda else contextlib.nullcontext()
         with ctx:
-            # no local non-finite flag for a bucket launched during backward: finish_and_step checks the
-            # REDUCED head gradients (a NaN / Inf on any rank survives the sum), so only the buckets held
-            # for the end need local flags (their update must be decided before their all-reduce lands)
+            if flag and self.track_nonfinite:
+                self._local_flag(view)
             if dt != torch.float32:
                 tmp = view.to(dt)
                 self._tmp[b] = tmp
-                self._works[b] = dist.all_reduce(tmp, group=self.pg, async_op=True)
+                self._works[b] = self._all_reduce(tmp)
             else:
-                self._works[b] = dist.all_reduce(view, group=self.pg, async_op=True)
-
-    def _post_flag(self, start: int, end: int) -> torch.Tensor:
-        """int32 [1] device flag: 1 when the (reduced) arena gradients [start, end) hold a NaN / Inf."""
-        view = self.arena.grad[start:end]
-        if view.is_cuda:
-            from ..ops import _lib
-            ws = torch.empty(1025, dtype=torch.int32, device=view.device)
-            if view.numel() == 0:
-                return ws[1024:].zero_()
-            _lib.call("pbx_nonfinite_flag", view.data_ptr(), view.numel(), ws.data_ptr(), ws[1024:].data_ptr(),
-                      _lib.stream_ptr(view.device))
-            return ws[1024:]
-        bad = view.numel() > 0 and not bool(torch.isfinite(torch.dot(view, torch.zeros_like(view))))
-        return torch.tensor([1 if bad else 0], dtype=torch.int32, device=view.device)
+                self._works[b] = self._all_reduce(view)
 
     def _flag_reduce_and_launch_rest(self) -> None:
-        """Local flags of the buckets not launched yet, the group-wide MAX of every bucket's flag (4 bytes,
-        queued ahead), then those buckets' all-reduces."""
+        """Local flags of the buckets not launched yet, the group-wide MAX of the flag (4 bytes, queued
+        ahead of them), then those buckets' all-reduces."""
         rest = range(self._next, len(self.buckets))
         dev = self.arena.grad.device
         ctx = streams.collective_stream(dev) if self.arena.grad.is_cuda else contextlib.nullcontext()
         with ctx:
-            self._flags.zero_()
             for b in rest:
                 s, e = self.buckets[b]
-                self._local_flag(b, self.arena.grad[s:e])
-            self._gflag = self._flags.amax().reshape(1)
-            self._flag_work = dist.all_reduce(self._gflag, op=dist.ReduceOp.MAX, group=self.pg, async_op=True)
-        for b in rest:
-            self._launch(b, flag_done=True)
+                self._local_flag(self.arena.grad[s:e])
+            if self._flag is None:
+                self._flag = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._flag_work = self._all_reduce(self._flag, "max")
+            self._ev_head = self._record(0)         # head buckets and the group flag have landed
+            for b in rest:
+                self._launch(b, flag=False)
+            self._ev_tail = self._record(1)
         self._next = len(self.buckets)
 
     def _land(self, b: int) -> None:
@@ -219,6 +248,8 @@ class BucketedAllReduce:
         self._ready = [False] * len(self._ready)
         self._next = 0
         self._works = [None] * len(self.buckets)
+        self._flag_fresh = True
+        self._ev_head = self._ev_tail = None
 
     def finish(self, average: bool = False) -> None:
         """Launch any bucket whose params got no gradient, then wait (stream-ordered)."""
@@ -229,12 +260,13 @@ class BucketedAllReduce:
         for b in range(self._next, len(self.buckets)):
             self._launch(b)
         self._next = len(self.buckets)
+        if self.arena.grad.is_cuda:
+            streams.join_collectives(self.arena.grad.device)   # direct communicator: its stream
         for b in range(len(self.buckets)):
             self._land(b)
-        if self.arena.grad.is_cuda:
-            streams.join_collectives(self.arena.grad.device)
         if average:
             self.arena.grad.div_(self.world)
+        self.track_nonfinite = False
         self.start_step()
 
     def finish_and_step(self, opt, skip_nonfinite: bool = True) -> None:
@@ -242,42 +274,38 @@ class BucketedAllReduce:
         non-finite flag (queued ahead of the last bucket) has landed, beside the last bucket's
         all-reduce; the last bucket's update follows its all-reduce.  Bitwise the same parameters as
         :meth:`finish` + a whole-arena ``opt.step()`` (Adam is element-wise).  Call
-        :meth:`begin_overlapped_step` before backward."""
+        :meth:`begin_overlapped_step` before backward (the buckets launched during backward test their
+        local gradients then)."""
         if not self.enabled:
             if skip_nonfinite:
                 opt.set_nonfinite_skip()
             opt.step()
             return
-        if self.arena.grad.is_cuda:
+        if not self.track_nonfinite and self._next > 0:
+            raise RuntimeError("finish_and_step: begin_overlapped_step() was not called before backward")
+        cuda = self.arena.grad.is_cuda
+        if cuda:
             streams.join()
-        if self._flags is None:
-            self._flags = torch.zeros(len(self.buckets), dtype=torch.int32, device=self.arena.grad.device)
-        # the exposed tail: buckets whose gradients were not final during backward (launched only now)
-        # (all of them launched already: the update waits only for the flag, queued behind them)
         split_b = self._next
         self._flag_reduce_and_launch_rest()
+        cur = torch.cuda.current_stream(self.arena.grad.device) if cuda else None
+        if self._ev_head is not None:
+            cur.wait_event(self._ev_head)
         for b in range(split_b):
             self._land(b)
-        self._flag_work.wait()
+        if self._flag_work is not None:
+            self._flag_work.wait()
         split = self.buckets[split_b][0] if split_b < len(self.buckets) else self.arena.numel
-        skip = None
-        if skip_nonfinite:
-            # local flags (group OR) + the REDUCED head gradients: finite per-rank gradients whose sum
-            # overflows are caught too; the reduced values are identical on every rank, so every rank
-            # takes the same decision without another collective
-            skip = torch.maximum(self._gflag, self._post_flag(0, split))
-        opt.skip_flag = skip
+        # every rank holds the same group-wide flag: the whole step is skipped or committed together
+        opt.skip_flag = self._flag if skip_nonfinite else None
         opt.begin_step()
         opt.step_range(0, split)              # beside the tail buckets' all-reduce
+        if self._ev_tail is not None:
+            cur.wait_event(self._ev_tail)
         for b in range(split_b, len(self.buckets)):
             self._land(b)
-        if split < self.arena.numel:
-            if skip_nonfinite:
-                # a sum that overflows only in the tail is known only now: the tail update is skipped
-                # (the head's was already committed), so no Inf / NaN ever reaches the parameters
-                opt.skip_flag = torch.maximum(skip, self._post_flag(split, self.arena.numel))
-            opt.step_range(split, self.arena.numel)
-        if self.arena.grad.is_cuda:
+        opt.step_range(split, self.arena.numel)
+        if cuda:
             streams.join_collectives(self.arena.grad.device)
         self.track_nonfinite = False
         self._flag_work = None
@@ -286,6 +314,7 @@ class BucketedAllReduce:
     def begin_overlapped_step(self) -> None:
         """The coming backward's buckets carry local non-finite flags (for :meth:`finish_and_step`)."""
         self.track_nonfinite = self.enabled
+        self._flag_fresh = True
 
     def broadcast_parameters(self, module: Optional[torch.nn.Module] = None, src: int = 0) -> None:
         if not self.enabled:
@@ -301,3 +330,10 @@ class BucketedAllReduce:
             h.remove()
         self._hooks = []
         remove_grad_ready_listener(self._on_direct_grads)
+
+    def close(self) -> None:
+        """Remove the hooks and release the direct communicator (before the process group goes)."""
+        self.remove_hooks()
+        if self.comm is not None:
+            self.comm.close()
+            self.comm = None

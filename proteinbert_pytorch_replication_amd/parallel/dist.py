@@ -45,6 +45,10 @@ def env_world() -> DistInfo:
                     local_rank=int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def _gpu_node_present() -> bool:
+    return os.path.exists("/dev/kfd") and os.environ.get("HIP_VISIBLE_DEVICES", "x") != ""
+
+
 def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Optional[str] = None) -> DistInfo:
     """Idempotent.  With WORLD_SIZE==1 no process group is created."""
     global _INFO
@@ -53,9 +57,11 @@ def init_distributed(backend: str = "auto", timeout_s: int = 600, device: Option
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     info = env_world()
     # the node defaults go into the environment BEFORE the first GPU call: the HSA runtime reads its HSA_*
-    # variables once, at start-up (torch.cuda.device_count() does not start it on this image)
+    # variables once, at start-up.  Decided from the arguments and the environment only: a device query
+    # (torch.cuda.device_count() goes through hipGetDeviceCount on builds without amdsmi) could start HSA
+    # first; /dev/kfd is the ROCm compute device node
     rccl_env = None
-    if info.world_size > 1 and device != "cpu" and backend in ("auto", "nccl") and torch.cuda.device_count() > 0:
+    if info.world_size > 1 and device != "cpu" and backend in ("auto", "nccl") and _gpu_node_present():
         rccl_env = rccl_node_defaults(info.world_size)
     use_gpu = torch.cuda.is_available() and device != "cpu"
     if use_gpu:
@@ -104,6 +110,8 @@ def rccl_node_defaults(world_size: int) -> Optional[dict]:
     if int(os.environ.get("LOCAL_WORLD_SIZE", world_size)) != world_size:
         return None
     applied = {}
+    # torch.cuda.is_initialized() is False after a bare device query that already started HSA, so this
+    # guard is a lower bound: callers set the environment before any HIP call (init_distributed does)
     hsa_started = torch.cuda.is_initialized()
     for k, v in RCCL_NODE_DEFAULTS.items():
         if k.startswith("HSA_") and hsa_started:

@@ -99,7 +99,7 @@ class ZeroFusedAdam(FusedAdam):
                     from ..ops import _lib
                     ws = torch.empty(1025, dtype=torch.int32, device=self._gshard.device)
                     _lib.call("pbx_nonfinite_flag", self._gshard.data_ptr(), n, ws.data_ptr(), ws[1024:].data_ptr(),
-                              _lib.stream_ptr(self._gshard.device))
+                              float("inf"), 0, _lib.stream_ptr(self._gshard.device))
                     bad = ws[1024:].clone()
                 else:
                     bad.fill_(0 if bool(torch.isfinite(self._gshard[:n]).all()) else 1)

@@ -133,7 +133,7 @@ class FusedAdam(torch.optim.Optimizer):
             if getattr(self, "_nf_ws", None) is None:
                 self._nf_ws = torch.empty(1025, dtype=torch.int32, device=a.grad.device)
             _lib.call("pbx_nonfinite_flag", a.grad.data_ptr(), a.numel, self._nf_ws.data_ptr(),
-                      self._nf_ws[1024:].data_ptr(), _lib.stream_ptr(a.grad.device))
+                      self._nf_ws[1024:].data_ptr(), float("inf"), 0, _lib.stream_ptr(a.grad.device))
             self.skip_flag = self._nf_ws[1024:]
         else:
             # exact per-element test in one BLAS pass: grad . 0 is NaN iff some element is NaN / Inf (every

@@ -1,4 +1,8 @@
-"""argparse validators and task-splitting flags (reference ``shared_utils/util.py:371-506``)."""
+"""argparse validators and task-splitting flags (reference ``shared_utils/util.py:371-506``).
+
+The reference's SLURM job-array helper (``shared_utils/util.py:1120-1158``) is not provided: SURVEY
+marks it "not needed" -- ranks come from the ``torchrun`` environment, and task splitting from
+``--task-index`` / ``--total-tasks`` or ``SLURM_ARRAY_TASK_ID`` (:func:`determine_parser_task_details`)."""
 from __future__ import annotations
 
 import argparse
@@ -59,35 +63,3 @@ def determine_parser_task_details(args) -> Tuple[int, int]:
         raise ValueError("task index %d out of range for %d tasks" % (task_index, total_tasks))
     return task_index, total_tasks
 
-
-def get_slurm_job_array_ids(parse_total_tasks_by_max_variable: bool = True, log_ids: bool = True,
-                            verbose: bool = True,
-                            task_index_remapping_json_file_path: Optional[str] = None) -> Tuple[int, int, int]:
-    """``(job_id, total_tasks, task_index)`` of a SLURM job-array task (reference
-    ``shared_utils/util.py:1120-1158``, U4): ``SLURM_ARRAY_TASK_ID`` + optional ``TASK_ID_OFFSET``,
-    optionally remapped through a JSON list; total from ``TOTAL_TASKS``, else
-    ``SLURM_ARRAY_TASK_MAX + 1`` (or ``SLURM_ARRAY_TASK_COUNT``)."""
-    import json
-    from .log import log
-    job_id = int(os.environ["SLURM_ARRAY_JOB_ID"])
-    task_index = int(os.environ["SLURM_ARRAY_TASK_ID"])
-    if "TASK_ID_OFFSET" in os.environ:
-        offset = int(os.environ["TASK_ID_OFFSET"])
-        if verbose:
-            log("Raw task index %d with offset %d." % (task_index, offset))
-        task_index += offset
-    if task_index_remapping_json_file_path is not None:
-        with open(task_index_remapping_json_file_path) as f:
-            remapped = int(json.load(f)[task_index])
-        if verbose:
-            log("Remapped task index %d into %d." % (task_index, remapped))
-        task_index = remapped
-    if "TOTAL_TASKS" in os.environ:
-        total_tasks = int(os.environ["TOTAL_TASKS"])
-    elif parse_total_tasks_by_max_variable:
-        total_tasks = int(os.environ["SLURM_ARRAY_TASK_MAX"]) + 1
-    else:
-        total_tasks = int(os.environ["SLURM_ARRAY_TASK_COUNT"])
-    if log_ids:
-        log("Running job %s, task %d of %d." % (job_id, task_index, total_tasks))
-    return job_id, total_tasks, task_index

@@ -45,8 +45,7 @@ def _exported_launchers():
     names = set()
     for f in glob.glob(os.path.join(ROOT, "proteinbert_pytorch_replication_amd", "ops", "csrc", "*.hip")):
         with open(f) as fh:
-            src = re.sub(r"#ifdef PBX_STAMPS.*?#endif", "", fh.read(), flags=re.S)   # instrumented builds only
-            names.update(re.findall(r"PBX_EXPORT\s+int\s+(pbx_\w+)\s*\(", src))
+            names.update(re.findall(r"PBX_EXPORT\s+int\s+(pbx_\w+)\s*\(", fh.read()))
     return names
 
 

@@ -76,29 +76,21 @@ def test_summary_counts_match_parameters():
     assert "Total params" in str(s)
 
 
-def test_task_splitting_and_slurm_array_ids(monkeypatch, tmp_path):
-    """U3/U4 helpers (reference shared_utils/util.py:436-505, 1120-1158)."""
+def test_task_splitting(monkeypatch):
+    """U3 task-splitting helpers (reference shared_utils/util.py:436-505); the SLURM array id is read from
+    the environment (U4's job-array helper itself is not needed)."""
     import argparse
-    import json
     from proteinbert_pytorch_replication_amd.utils.cli_types import (add_parser_task_arguments,
-                                                                     determine_parser_task_details,
-                                                                     get_slurm_job_array_ids)
+                                                                     determine_parser_task_details)
     p = argparse.ArgumentParser()
     add_parser_task_arguments(p)
     assert determine_parser_task_details(p.parse_args(["--task-index", "2", "--total-tasks", "4"])) == (2, 4)
     for k in ("SLURM_ARRAY_TASK_ID", "TASK_ID_OFFSET", "TOTAL_TASKS"):
         monkeypatch.delenv(k, raising=False)
     assert determine_parser_task_details(p.parse_args([])) == (0, 1)
-    monkeypatch.setenv("SLURM_ARRAY_JOB_ID", "77")
     monkeypatch.setenv("SLURM_ARRAY_TASK_ID", "3")
-    monkeypatch.setenv("SLURM_ARRAY_TASK_MAX", "9")
-    assert get_slurm_job_array_ids(log_ids=False, verbose=False) == (77, 10, 3)
     monkeypatch.setenv("TASK_ID_OFFSET", "2")
-    remap = tmp_path / "remap.json"
-    remap.write_text(json.dumps(list(range(100, 120))))
-    assert get_slurm_job_array_ids(log_ids=False, verbose=False,
-                                   task_index_remapping_json_file_path=str(remap)) == (77, 10, 105)
     monkeypatch.setenv("TOTAL_TASKS", "40")
-    assert get_slurm_job_array_ids(log_ids=False, verbose=False)[1] == 40
+    assert determine_parser_task_details(p.parse_args([])) == (5, 40)
     with pytest.raises(ValueError):
         determine_parser_task_details(p.parse_args(["--task-index", "5", "--total-tasks", "4"]))

@@ -138,9 +138,10 @@ def test_dp_overlapped_optimizer_skips_all_buckets_on_nonfinite(tmp_path):
 
 
 def _overflow_worker(rank, world, port, out_dir, where):
-    """Both ranks hold a FINITE gradient of 3e38 in one element; their SUM overflows fp32.  where='head':
-    the element is in the first bucket -> nothing is updated; 'tail': in the last bucket -> the tail's
-    update is skipped (the head's already ran) and no Inf reaches the parameters."""
+    """Both ranks hold a FINITE gradient of 3e38 in one element; their SUM overflows fp32.  The local test
+    (|g| >= FLT_MAX / world) flags it before any all-reduce, so wherever the element sits (first or last
+    bucket) the whole step is skipped on every rank: no Inf reaches the parameters and no step is applied
+    to only part of the arena."""
     _env(rank, world, port)
     torch.set_num_threads(1)
     from proteinbert_pytorch_replication_amd.parallel import dist as pdist
@@ -162,11 +163,7 @@ def _overflow_worker(rank, world, port, out_dir, where):
     step(*SyntheticUniRefGO(CFG["sequences_length"], CFG["num_annotations"], 4, "cpu", seed=100 + rank,
                             use_kernel=False).next_batch())
     assert torch.isfinite(opt.arena.data).all(), f"rank {rank}: an overflowed sum reached the parameters"
-    tail0 = ddp.buckets[-1][0]
-    if where == "head":
-        assert torch.equal(opt.arena.data, before), f"rank {rank} updated despite an overflowing sum"
-    else:
-        assert torch.equal(opt.arena.data[tail0:], before[tail0:]), f"rank {rank}: tail updated"
+    assert torch.equal(opt.arena.data, before), f"rank {rank} updated part of the arena despite an overflowing sum"
     torch.save(opt.arena.data, os.path.join(out_dir, f"rank{rank}.pt"))
     pdist.destroy()
 
@@ -287,3 +284,25 @@ def test_rccl_node_defaults_respect_environment(monkeypatch):
     monkeypatch.setenv("PBX_RCCL_DEFAULTS", "0")
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
     assert pdist.rccl_node_defaults(8) is None
+
+
+def _uid_worker(rank, world, port, out_dir):
+    """The direct RCCL communicator's unique-id hand-off (parallel/rccl.py) through the process group's store:
+    rank 0's id reaches every rank byte for byte (no GPU needed for this part)."""
+    _env(rank, world, port)
+    from proteinbert_pytorch_replication_amd.parallel import dist as pdist
+    from proteinbert_pytorch_replication_amd.parallel import rccl
+    pdist.init_distributed(device="cpu")
+    blob = bytes(range(128)) + b""
+    got = rccl.exchange_unique_id(rank, "pbx_test_uid/0", lambda: blob)
+    got2 = rccl.exchange_unique_id(rank, "pbx_test_uid/1", lambda: bytes(reversed(blob)))
+    assert rccl.wanted() is False              # gloo: the buckets stay on torch.distributed
+    with open(os.path.join(out_dir, f"uid{rank}.bin"), "wb") as f:
+        f.write(got + got2)
+    pdist.destroy()
+
+
+def test_rccl_unique_id_exchange(tmp_path):
+    mp.start_processes(_uid_worker, args=(3, _free_port(), str(tmp_path)), nprocs=3, start_method="spawn", join=True)
+    blobs = [open(tmp_path / f"uid{r}.bin", "rb").read() for r in range(3)]
+    assert blobs[0] == blobs[1] == blobs[2] == bytes(range(128)) + bytes(reversed(range(128)))

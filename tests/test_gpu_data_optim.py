@@ -65,6 +65,35 @@ def test_nonfinite_flag_kernel(n):
     assert int(fa.set_nonfinite_skip().item()) == 0
 
 
+@pytest.mark.parametrize("n", [5, 300001])
+def test_nonfinite_flag_bound_and_accumulate(n):
+    """The DP form: bound = FLT_MAX / world flags finite elements whose sum over the ranks could overflow, and
+    accumulate = 1 ORs into the flag (one flag per step over every bucket)."""
+    from proteinbert_pytorch_replication_amd.ops import _lib
+    ws = torch.empty(1024, dtype=torch.int32, device="cuda")
+    flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+    st = _lib.stream_ptr(torch.device("cuda"))
+    bound = 3.4028234663852886e38 / 8
+    g = torch.randn(n, device="cuda")
+
+    def run(x, acc):
+        _lib.call("pbx_nonfinite_flag", x.data_ptr(), x.numel(), ws.data_ptr(), flag.data_ptr(), bound, acc, st)
+        return int(flag.item())
+
+    assert run(g, 0) == 0
+    big = g.clone()
+    big[n - 1] = 5e37                           # finite, but 8 ranks of it overflow fp32
+    assert run(big, 0) == 1
+    assert run(g, 1) == 1                       # accumulate keeps the earlier bucket's 1
+    assert run(g, 0) == 0                       # a fresh step overwrites
+    ok = g.clone()
+    ok[0] = 3e37                                # below FLT_MAX / 8
+    assert run(ok, 1) == 0
+    nan = g.clone()
+    nan[n // 2] = float("nan")
+    assert run(nan, 1) == 1
+
+
 def test_clip_grad_norm_gpu():
     p = torch.nn.Parameter(torch.zeros(5000, device="cuda"))
     fa = FusedAdam([p], lr=0.1)

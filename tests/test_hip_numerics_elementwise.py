@@ -96,7 +96,7 @@ def test_embedding_fold_elementwise_vs_fp32(L, B):
         nmax, p999 = elementwise(got[n][used], ref[used])
         print(f"L={L} B={B} {n}: max|err|/max|ref| {nmax:.2e}  p99.9 rel {p999:.2e}")
         # observed (round 5): max 1.0e-2 / p99.9 0.18 (the embedding: its 26 rows sum ~19 K positions each)
-        assert nmax < 2e-2 and p999 < 0.35, (n, nmax, p999)
+        assert nmax < 2e-2 and p999 < 0.25, (n, nmax, p999)
         assert torch.count_nonzero(got[n][~used]) == 0
 
 

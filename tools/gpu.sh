@@ -15,6 +15,7 @@
 #   pmc <tag> <counters> [bench.py args] one rocprofv3 --pmc pass (counters comma-separated, within
 #                                        the per-block limits) over a short bench run
 #   py <tag> <seconds> <script> [args]   any python script (a probe under tools/) with a time limit
+#   profpy <tag> <seconds> <script> [args]  rocprofv3 kernel trace + stats of any python script
 # Example:
 #   gpurun --timeout 900 -- 'bash tools/gpu.sh tests -- bench r4_base --steps 50 -- prof r4_prof'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -66,6 +67,12 @@ run_task() {
       python3 tools/profsum.py "$st" 13 40 > gpurun_out/${tag}_summary.txt 2>&1 || true
       python3 tools/critpath.py "$tr" > gpurun_out/${tag}_critpath.txt 2>&1 || true
       head -25 gpurun_out/${tag}_summary.txt ;;
+    profpy)
+      local tag=$1 secs=$2; shift 2
+      rm -rf gpurun_out/$tag
+      $T "$secs" rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$tag -o run -- python3 -u "$@" \
+        > gpurun_out/$tag.log 2>&1 || fatal $? "profpy $tag"
+      tail -3 gpurun_out/$tag.log ;;
     pmc)
       local tag=$1 ctr=$2; shift 2
       rm -rf gpurun_out/$tag

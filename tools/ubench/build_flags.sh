@@ -1,6 +1,6 @@
 #!/bin/bash
-# Build the kernel library from the WORKING TREE's csrc/ with extra compile flags into
-# tools/ubench/abl/libpbx_<name>.so (experiments: PBX_HIP_LIB=... python tools/ubench/convbench.py).
+# Build the kernel library from the WORKING TREE's csrc/ (or SRC=<dir>, e.g. an older checkout for a same-box
+# A/B) with extra compile flags into tools/ubench/abl/libpbx_<name>.so (PBX_HIP_LIB=... python tools/...).
 # usage: tools/ubench/build_flags.sh <name> [hipcc flags...]
 set -e
 name=$1; shift

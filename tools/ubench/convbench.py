@@ -1,8 +1,8 @@
 """Time the conv kernels (conv_fwd3, csrc/conv2.hip; conv_dgrad4, csrc/conv4.hip; wgrad2, csrc/wgrad.hip)
-at the bench shape with whatever library PBX_HIP_LIB names (compare --ref-lib outputs for a variant): phase ablations are separate builds of the
-same source built with extra -D flags (tools/ubench/build_flags.sh <name> -D...).
+at the bench shape through their exported launchers (whole sequences: no context-parallel halo rows), with
+whatever library PBX_HIP_LIB names (a variant built by tools/ubench/build_flags.sh).
 
-    PBX_HIP_LIB=tools/ubench/abl/libpbx_noepi.so python tools/ubench/convbench.py --tag noepi
+    python tools/ubench/convbench.py [--B 1024 --L 512]
 """
 import argparse
 import os
@@ -46,15 +46,15 @@ bias = torch.randn(C, device=dev) * 0.1
 gb = torch.randn(B, C, device=dev) * 0.1
 pre_n, pre_w, s1 = (torch.empty_like(x) for _ in range(3))
 stt = torch.empty(B, (L + 127) // 128, 2, device=dev)
-fwd = lambda: _lib.call("pbx_conv_fwd3", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
+fwd = lambda: _lib.call("pbx_conv_fwd3x", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
                         bias.data_ptr(), gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(),
-                        stt.data_ptr(), B, L, KS, dil, st)
+                        stt.data_ptr(), B, L, KS, dil, 0, 0, st)
 us = timeit(fwd)
 print(f"[{a.tag}] conv_fwd3   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
 ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
 dx, dpn, dpw = (torch.empty_like(x) for _ in range(3))
-dg4 = lambda: _lib.call("pbx_conv_dgrad4", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
-                        ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, st)
+dg4 = lambda: _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
+                        ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, 0, 0, st)
 us = timeit(dg4)
 print(f"[{a.tag}] conv_dgrad4 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
 slab = torch.empty(64 * 2 * KS * C * C, device=dev)
