@@ -67,6 +67,9 @@ def parse():
     ap.add_argument("--gelu", default=None, choices=["fitted", "exact"],
                     help="GELU core of the fused kernels (default: PBX_GELU or fitted): fitted = logistic fit "
                          "(max |err| 2.9e-4); exact = the erf form of the reference's nn.GELU()")
+    ap.add_argument("--dp-batch-softmax", action="store_true",
+                    help="reference local head: softmax over the whole DP batch (three [L, 32] all-reduces per "
+                         "step; DP=N then equals the single-process batch-N*b step)")
     ap.add_argument("--semantics", default="reference", choices=["reference", "paper"],
                     help="paper: published attention/LN/softmax (per-position LayerNorm, softmax over positions)")
     return ap.parse_args()
@@ -125,6 +128,9 @@ def main():
     ddp = BucketedAllReduce(opt.arena, bucket_mb=a.bucket_mb) if info.distributed else None
     if ddp is not None:
         ddp.broadcast_parameters(model)
+    if a.dp_batch_softmax and info.distributed:
+        from proteinbert_pytorch_replication_amd.parallel import batch_softmax
+        batch_softmax.enable()
     # bf16 activations on the GPU; the CPU rehearsal path (gloo ranks, BASELINE cfg 1) computes in fp32
     dtype = torch.float32 if (a.impl == "faithful" or dev.type != "cuda") else torch.bfloat16
     step = PretrainStep(model, opt, ddp, compute_dtype=dtype)
@@ -179,6 +185,7 @@ def main():
                "world_size": n, "backend": info.backend if n > 1 else "single",
                "rccl_env": getattr(info, "rccl_env", None),
                "dp_transport": ddp.transport if ddp is not None else "none",
+               "dp_batch_softmax": bool(a.dp_batch_softmax and n > 1),
                "gelu": _gelu_label(a.impl),
                "device": _device_label(dev), "final_loss": round(final_loss, 5),
                # the reference reduces its loss in float64 (float64 weights, utils.py:293-294); the fused

@@ -121,7 +121,8 @@ def pretrain_main(argv: Optional[List[str]] = None) -> dict:
                    grad_clip=cfg.optim.grad_clip, async_checkpoint=a.async_checkpoint, metrics_path=a.metrics,
                    tensorboard_dir=a.tensorboard,
                    resume=a.resume, profile_steps=a.profile_steps, profile_dir=a.profile_dir,
-                   zero_optimizer=a.zero, comm_dtype=cfg.dist.comm_dtype)
+                   zero_optimizer=a.zero, comm_dtype=cfg.dist.comm_dtype,
+                   dp_batch_softmax=cfg.dist.dp_batch_softmax)
     if info.is_main:
         print(json.dumps({"final_loss": res["train_loss"][-1] if res["train_loss"] else None,
                           "iterations": len(res["train_loss"]), "final_model": res.get("final_model_path")}))

@@ -75,6 +75,7 @@ class DistConfig:
     backend: str = "auto"               # auto -> nccl (RCCL) on GPU, gloo on CPU
     bucket_mb: float = 8.0              # sized for 7 xGMI links (see parallel/ddp.py)
     comm_dtype: str = "fp32"            # fp32 | bf16 gradient all-reduce
+    dp_batch_softmax: bool = False      # reference local head: softmax over the WHOLE DP batch (parallel/batch_softmax.py)
     timeout_s: int = 600
 
 

@@ -371,7 +371,11 @@ class ProteinBERT(nn.Module):
     def heads_torch(self, h: torch.Tensor, g: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
         lo = self.pretraining_local_output[0]
         logits_l = F.linear(h.float(), lo.weight, lo.bias)                      # [B,L,V]
-        probs_l = torch.softmax(logits_l, dim=0 if self.semantics == "reference" else -1)
+        if self.semantics == "reference":
+            from ..parallel.batch_softmax import softmax_over_batch
+            probs_l = softmax_over_batch(logits_l)     # this rank's batch, or the DP group's (dp_batch_softmax)
+        else:
+            probs_l = torch.softmax(logits_l, dim=-1)
         go = self.pretraining_global_output[0]
         probs_g = torch.sigmoid(F.linear(g.float(), go.weight, go.bias))
         return probs_l, probs_g

@@ -67,7 +67,7 @@ def hip_flags() -> List[str]:
     # GELU cores of the VALU-bound pool epilogue) stays packed.  +1.4 % on the step, same-box A/B
     # (tools/gpu_scalar_ab.sh, profiles/r2_v8_scalar_ab.txt).
     return ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
-            "-ffp-contract=fast", "-fno-slp-vectorize", "-Wno-unused-result", "-I", CSRC]
+            "-ffp-contract=fast-honor-pragmas", "-fno-slp-vectorize", "-Wno-unused-result", "-I", CSRC]
 
 
 def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8, variant: str = "fitted") -> str:
@@ -78,6 +78,11 @@ def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8, variant
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     objs = []
+    # a change of compiler flags rebuilds every object (mtimes alone would keep the old code)
+    stamp = os.path.join(bdir, "flags.txt")
+    flags = " ".join([hipcc, *hip_flags(), *extra])
+    if not os.path.exists(stamp) or open(stamp).read() != flags:
+        force = True
 
     def compile_one(src: str) -> str:
         obj = os.path.join(bdir, os.path.basename(src) + ".o")
@@ -91,6 +96,8 @@ def build_hip(verbose: bool = False, force: bool = False, jobs: int = 8, variant
         tmp = lib + ".tmp"
         _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp, *objs], verbose)
         os.replace(tmp, lib)
+    with open(stamp, "w") as f:
+        f.write(flags)
     return lib
 
 

@@ -218,6 +218,8 @@ __global__ void __launch_bounds__(512, 4) conv_fwd3_kernel(
     float o[8];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
+      // no FMA contraction of the GELU product into these adds: conv_fwd5 (conv5.hip) rounds the same way
+#pragma clang fp contract(off)
       const f32x2 v = (f32x2){xv[2 * e], xv[2 * e + 1]} + go[e] + go[4 + e] + gbp[e];
       o[2 * e] = v.x;
       o[2 * e + 1] = v.y;

@@ -129,7 +129,7 @@ __global__ void __launch_bounds__(256) lhead_fold_kernel(const float2* __restric
   if (ok) {
     for (int c = cg; c < nchunks; c += 4) {
       const float2 p = part[(size_t)c * L * VP + i];
-      if (mode == 0) {
+      if (mode != 1) {
         const float mn = fmaxf(m, p.x);
         sum = sum * __expf(m - mn) + p.y * __expf(p.x - mn);
         m = mn;
@@ -141,14 +141,14 @@ __global__ void __launch_bounds__(256) lhead_fold_kernel(const float2* __restric
   red[cg][il] = make_float2(m, sum);
   __syncthreads();
   if (cg != 0 || !ok) return;
-  if (mode == 0) {
+  if (mode != 1) {
     float mm = red[0][il].x;
 #pragma unroll
     for (int k = 1; k < 4; ++k) mm = fmaxf(mm, red[k][il].x);
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < 4; ++k) ss += red[k][il].y * __expf(red[k][il].x - mm);
-    out[i] = make_float2(mm, ss > 0.f ? 1.0f / ss : 0.f);
+    out[i] = make_float2(mm, mode == 2 ? ss : ss > 0.f ? 1.0f / ss : 0.f);   // mode 2: raw (M, S)
   } else {
     out[i] = make_float2(red[0][il].y + red[1][il].y + red[2][il].y + red[3][il].y, 0.f);
   }
@@ -596,33 +596,70 @@ __global__ void __launch_bounds__(512) lhead_fused_kernel(const bf16_t* __restri
 // MS/T [L * 32 * 2] each, loss_part / dbo_part [ntiles], [ntiles * V]; ntiles = ceil(B/16) ceil(L/32).
 PBX_EXPORT int pbx_local_head3_tiles(int B, int L) { return ((B + SB - 1) / SB) * ((L + PT - 1) / PT); }
 
+namespace {
+constexpr int LDS1 = VP * 256 + VP * 4 + SB * PT * (VP + 1) * 4;
+constexpr int LDS5 = 8 * PT * 256 + VP * 256 + PT * VP * 8 + PT * VP * 4 + VP * 4 + 8 * VP * 4;
+void lhead3_attrs() {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)lhead_logits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS1);
+    (void)hipFuncSetAttribute((const void*)lhead_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, LDS5);
+    attr = true;
+  }
+}
+}  // namespace
+
+// The five passes in three stages, so that a data-parallel group can share the batch axis of the softmax
+// (parallel/batch_softmax.py): stage A = passes 1-2 -- with raw = 1 the fold leaves (M, S) for the caller
+// to merge over ranks into (M, 1/S) --, stage B = passes 3-4 (T, which the caller sums over ranks),
+// stage C = pass 5.
+PBX_EXPORT int pbx_local_head3_a(const void* h, const float* wo, const float* bo, float* Z, float* part, float* MS,
+                                 int raw, int B, int L, int V, hipStream_t st) {
+  if (V > VP || V < 1 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  lhead3_attrs();
+  const int nt = pbx_local_head3_tiles(B, L);
+  const int nch = (B + SB - 1) / SB;
+  hipLaunchKernelGGL(lhead_logits_kernel, dim3(nt), dim3(512), LDS1, st, (const bf16_t*)h, wo, bo, Z, (float2*)part,
+                     B, L, V);
+  hipLaunchKernelGGL(lhead_fold_kernel, dim3((L * VP + 63) / 64), dim3(256), 0, st, (const float2*)part, nch, L,
+                     (float2*)MS, raw ? 2 : 0);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_local_head3_b(const float* Z, const float* MS, const void* y, const float* wl, float* tpart,
+                                 float* loss_part, float* T, int B, int L, int V, hipStream_t st) {
+  if (V > VP || V < 1 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  const int nt = pbx_local_head3_tiles(B, L);
+  const int nch = (B + SB - 1) / SB;
+  const float inv_bl = 1.0f / ((float)B * (float)L);
+  hipLaunchKernelGGL(lhead_ce_kernel, dim3(nt), dim3(512), 0, st, Z, (const float2*)MS, (const long long*)y, wl,
+                     (float2*)tpart, loss_part, B, L, V, inv_bl);
+  hipLaunchKernelGGL(lhead_fold_kernel, dim3((L * VP + 63) / 64), dim3(256), 0, st, (const float2*)tpart, nch, L,
+                     (float2*)T, 1);
+  return pbx_launch_status();
+}
+
+PBX_EXPORT int pbx_local_head3_c(const float* Z, const float* MS, const float* T, const void* y, const float* wl,
+                                 const float* wo, const float* bo, void* dh, void* dz, float* dbo_part, int B, int L,
+                                 int V, hipStream_t st) {
+  if (V > VP || V < 1 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
+  lhead3_attrs();
+  const int nt = pbx_local_head3_tiles(B, L);
+  const float inv_bl = 1.0f / ((float)B * (float)L);
+  hipLaunchKernelGGL(lhead_grad_kernel, dim3(nt), dim3(512), LDS5, st, Z, (const float2*)MS, (const float2*)T,
+                     (const long long*)y, wl, wo, bo, (bf16_t*)dh, (bf16_t*)dz, dbo_part, B, L, V, inv_bl);
+  return pbx_launch_status();
+}
+
 // Passes 1-5 (see header).  Outputs: dh [B][L][128] bf16, dz [B*L][32] bf16 (for dWo = dz^T h, a GEMM
 // the caller issues), dbo_part [ntiles][V], loss_part [ntiles] (each already divided by B L).
 PBX_EXPORT int pbx_local_head3(const void* h, const float* wo, const float* bo, const void* y, const float* wl,
                                void* dh, void* dz, float* dbo_part, float* loss_part, float* Z, float* part,
                                float* tpart, float* MS, float* T, int B, int L, int V, hipStream_t st) {
-  if (V > VP || V < 1 || B < 1 || L < 1) return (int)hipErrorInvalidValue;
-  const int nt = pbx_local_head3_tiles(B, L);
-  const int nch = (B + SB - 1) / SB;
-  const float inv_bl = 1.0f / ((float)B * (float)L);
-  constexpr int lds1 = VP * 256 + VP * 4 + SB * PT * (VP + 1) * 4;
-  constexpr int lds5 = 8 * PT * 256 + VP * 256 + PT * VP * 8 + PT * VP * 4 + VP * 4 + 8 * VP * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)lhead_logits_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds1);
-    (void)hipFuncSetAttribute((const void*)lhead_grad_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lds5);
-    attr = true;
-  }
-  hipLaunchKernelGGL(lhead_logits_kernel, dim3(nt), dim3(512), lds1, st, (const bf16_t*)h, wo, bo, Z, (float2*)part,
-                     B, L, V);
-  const int nf = (L * VP + 63) / 64;
-  hipLaunchKernelGGL(lhead_fold_kernel, dim3(nf), dim3(256), 0, st, (const float2*)part, nch, L, (float2*)MS, 0);
-  hipLaunchKernelGGL(lhead_ce_kernel, dim3(nt), dim3(512), 0, st, Z, (const float2*)MS, (const long long*)y, wl,
-                     (float2*)tpart, loss_part, B, L, V, inv_bl);
-  hipLaunchKernelGGL(lhead_fold_kernel, dim3(nf), dim3(256), 0, st, (const float2*)tpart, nch, L, (float2*)T, 1);
-  hipLaunchKernelGGL(lhead_grad_kernel, dim3(nt), dim3(512), lds5, st, Z, (const float2*)MS, (const float2*)T,
-                     (const long long*)y, wl, wo, bo, (bf16_t*)dh, (bf16_t*)dz, dbo_part, B, L, V, inv_bl);
-  return pbx_launch_status();
+  int rc = pbx_local_head3_a(h, wo, bo, Z, part, MS, 0, B, L, V, st);
+  if (rc == 0) rc = pbx_local_head3_b(Z, MS, y, wl, tpart, loss_part, T, B, L, V, st);
+  if (rc == 0) rc = pbx_local_head3_c(Z, MS, T, y, wl, wo, bo, dh, dz, dbo_part, B, L, V, st);
+  return rc;
 }
 
 // Positions per workgroup of pbx_local_head_fused: 2 for B <= 512, 1 for B <= 1024 (0: unsupported).

@@ -21,6 +21,7 @@ import torch
 from . import _lib, streams
 from .gemm import gemm as _gemm, gemm_batch
 from .gemm import go_head_parts
+from ..parallel import batch_softmax
 from ..train.arena import notify_grads_ready
 from ..utils.determinism import fused_deterministic
 
@@ -33,6 +34,9 @@ _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_local_head3_tiles", [_I, _I])
 _lib.register("pbx_local_head_fused", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_local_head3_a", [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_local_head3_b", [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
+_lib.register("pbx_local_head3_c", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 # local head: one launch for B <= 512 (pbx_local_head_fused: 61 vs 108 us for the five-pass form at
 # B = L = 512, profiles/r3k_*); larger per-GPU batches take the five-pass form
 LHEAD_FUSED = True
@@ -48,6 +52,8 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
     st = _s(dev)
     B, L, C = h.shape
     V = wo.shape[0]
+    if batch_softmax.active():
+        return _local_head_dp(h, wo, bo, y_l, w_l, loss_slot)
     if LHEAD_FUSED and B <= 1024:
         # one launch: a workgroup per 2 positions (B <= 512) or 1 (B <= 1024) x all samples (the batch
         # reductions stay on chip)
@@ -77,6 +83,40 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
               ms_t[0].data_ptr(), ms_t[1].data_ptr(), B, L, V, st)
     _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
     return dh, dz, dbo_part
+
+
+def _local_head_dp(h, wo, bo, y_l, w_l, loss_slot):
+    """The five-pass head with the batch axis of its softmax shared by the data-parallel group
+    (``parallel/batch_softmax.py``): stage A leaves the raw (M, S) for the cross-rank merge, stage B's
+    T = sum_b G P is summed over ranks before stage C forms dZ = P (G - T)."""
+    dev = h.device
+    st = _s(dev)
+    B, L, C = h.shape
+    V = wo.shape[0]
+    nt = _lib.lib().pbx_local_head3_tiles(B, L)
+    nch = (B + 15) // 16
+    dh = torch.empty_like(h)
+    dz = torch.empty((B * L, 32), dtype=BF16, device=dev)
+    dbo_part = torch.empty((nt, V), dtype=F32, device=dev)
+    lparts = torch.empty(nt, dtype=F32, device=dev)
+    Z = torch.empty((B * L, 32), dtype=F32, device=dev)
+    part = torch.empty((2, nch, L, 32, 2), dtype=F32, device=dev)
+    ms_t = torch.empty((2, L, 32, 2), dtype=F32, device=dev)
+    wo_c = wo.detach().contiguous()
+    y_c = y_l.contiguous()
+    w_c = w_l.float().contiguous()
+    _lib.call("pbx_local_head3_a", h.data_ptr(), wo_c.data_ptr(), bo.data_ptr(), Z.data_ptr(), part[0].data_ptr(),
+              ms_t[0].data_ptr(), 1, B, L, V, st)
+    batch_softmax.merge_head_stats(ms_t[0])
+    _lib.call("pbx_local_head3_b", Z.data_ptr(), ms_t[0].data_ptr(), y_c.data_ptr(), w_c.data_ptr(),
+              part[1].data_ptr(), lparts.data_ptr(), ms_t[1].data_ptr(), B, L, V, st)
+    batch_softmax.all_reduce_(ms_t[1], "sum")
+    _lib.call("pbx_local_head3_c", Z.data_ptr(), ms_t[0].data_ptr(), ms_t[1].data_ptr(), y_c.data_ptr(),
+              w_c.data_ptr(), wo_c.data_ptr(), bo.data_ptr(), dh.data_ptr(), dz.data_ptr(), dbo_part.data_ptr(),
+              B, L, V, st)
+    _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+    return dh, dz, dbo_part
+
 
 _lib.register("pbx_glob_bwd", [_P, _I, _I, _I, _I, _P, _P])
 _lib.register("pbx_glob3_fwd", [_P, _I, _I, _I, _I, _I, _F, _P])

@@ -19,6 +19,7 @@ Every op raises if the HIP library is missing — there is no silent eager fallb
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Dict, Optional, Tuple
 
 import torch
@@ -31,6 +32,7 @@ from .global_track import bf16_of
 _P, _I, _F, _L = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_long
 
 _lib.register("pbx_conv_fwd3x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
+_lib.register("pbx_conv_fwd5x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_conv_dgrad4x", [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_wgrad2x", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P])
 _lib.register("pbx_pack_conv_frag", [_P, _P, _P, _I, _P])
@@ -72,12 +74,18 @@ def _p(t: Optional[torch.Tensor]):
     return None if t is None else t.data_ptr()
 
 
+# the conv forward: the persistent software-pipelined kernel (csrc/conv5.hip, dilation 5) or conv_fwd3
+# (csrc/conv2.hip, any dilation; also the first block's token-gather form).  PBX_CONV_FWD=3 keeps conv_fwd3.
+CONV_FWD5 = os.environ.get("PBX_CONV_FWD", "5") == "5"
+
+
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream, xlo: int = 0,
              xhi: int = 0) -> None:
     """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward).
     ``xlo``/``xhi``: rows of the neighbouring sequence shards around each sample's L rows of ``x``
     (context parallelism, :mod:`..parallel.cp_fused`)."""
-    _lib.call("pbx_conv_fwd3x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+    name = "pbx_conv_fwd5x" if (CONV_FWD5 and KS == 9 and dil == 5) else "pbx_conv_fwd3x"
+    _lib.call(name, x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
               gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(), stats.data_ptr(), B, L, KS, dil, xlo, xhi, stream)
 
 

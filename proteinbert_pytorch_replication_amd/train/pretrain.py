@@ -71,7 +71,8 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
              async_checkpoint: bool = False, metrics_path: Optional[str] = None, resume: str = "none",
              fuse_optimizer: bool = True, final_save: bool = True, profile_steps: Optional[str] = None,
              profile_dir: Optional[str] = None, zero_optimizer: bool = False,
-             comm_dtype="fp32", tensorboard_dir: Optional[str] = None) -> Dict[str, Any]:
+             comm_dtype="fp32", tensorboard_dir: Optional[str] = None,
+             dp_batch_softmax: bool = False) -> Dict[str, Any]:
     info = pdist.init_distributed()
     if device is None:
         device = info.device
@@ -102,6 +103,11 @@ def pretrain(model: torch.nn.Module, train_dataloader, optimizer: torch.optim.Op
                 {"fp32": torch.float32, "bf16": torch.bfloat16}[comm_dtype]
             ddp = BucketedAllReduce(optimizer.arena, bucket_mb=bucket_mb, comm_dtype=cdt)
             ddp.broadcast_parameters(model)
+        if dp_batch_softmax:
+            # the reference local head normalises over the batch axis: share it over the DP ranks so DP=N
+            # with micro-batch b is the batch-N*b step (modules.py:277-284)
+            from ..parallel import batch_softmax
+            batch_softmax.enable()
 
     scheduler = WarmupThenPlateau(optimizer, warmup_duration=warmup_duration, patience=optim_scheduler_patience)
     step_fn = PretrainStep(model, optimizer, ddp, local_loss_fn, global_loss_fn, compute_dtype, grad_clip)

@@ -300,7 +300,9 @@ def test_embed_fold_matches_data_gradient_path(arena, det, semantics, L, monkeyp
         err = (g0[n] - g1[n]).norm().item()
         ref = g0[n].norm().item()
         print(f"{n:60s} |g|={ref:.3e} err={err:.3e}")
-        tol = 2e-2 if n == "local_embedding.weight" else 1e-3
+        # outside deterministic mode the block-0 broadcast-gradient column sums use fp32 atomics (order noise
+        # ~1e-10, tools/probe_conv_det.py) that can flip a bf16 rounding downstream of them
+        tol = 2e-2 if n == "local_embedding.weight" else (1e-3 if det else 1e-2)
         assert err <= tol * ref + 1e-6, (n, err, ref)
 
 
@@ -358,8 +360,18 @@ def test_conv_fwd_token_gather_matches_embedding_input(B, L):
                       B, L, 9, 5, st)
         else:
             x = E.to(torch.bfloat16)[tok].contiguous()
-            conv_fwd(x, wpn, wpw, bn, bw, gb, o[0], o[1], o[2], st1, B, L, 9, 5, st)
+            # conv_fwd3 itself (conv_fwd picks the persistent conv_fwd5 for dilation 5: same s1 / GELU'
+            # images, LayerNorm partials summed in another order -- checked below)
+            _lib.call("pbx_conv_fwd3x", x.data_ptr(), wpn.data_ptr(), wpw.data_ptr(), bn.data_ptr(), bw.data_ptr(),
+                      gb.data_ptr(), o[0].data_ptr(), o[1].data_ptr(), o[2].data_ptr(), st1.data_ptr(), B, L, 9, 5,
+                      0, 0, st)
+            o5 = [torch.empty_like(t) for t in o]
+            st5 = torch.empty_like(st1)
+            conv_fwd(x, wpn, wpw, bn, bw, gb, o5[0], o5[1], o5[2], st5, B, L, 9, 5, st)
         outs.append(o + [st1])
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+    for a, b in zip(o5, outs[0][:3]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(st5, outs[0][3], rtol=2e-5, atol=2e-5 * L * 128)

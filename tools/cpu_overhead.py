@@ -21,6 +21,8 @@ ap.add_argument("--steps", type=int, default=20)
 ap.add_argument("--dp", action="store_true",
                 help="attach the bucketed all-reduce (forced on a 1-rank RCCL group): the DP step's hooks")
 ap.add_argument("--graph", action="store_true", help="time hipGraph replays (GraphedStep) instead of eager steps")
+ap.add_argument("--batch-softmax", action="store_true",
+                help="with --dp: the local head's batch softmax shared over the (1-rank) group -- its cost")
 ap.add_argument("--dp-variant", default="full", choices=["full", "nocomm", "nooverlap"],
                 help="--dp diagnosis: nocomm = hooks and flags but no all-reduce; nooverlap = finish() + "
                      "whole-arena Adam")
@@ -39,6 +41,9 @@ if a.dp:
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:29517", rank=0, world_size=1,
                             timeout=datetime.timedelta(seconds=60), device_id=dev, pg_options=nccl_pg_options())
     ddp = BucketedAllReduce(opt.arena, force=True)
+    if a.batch_softmax:
+        from proteinbert_pytorch_replication_amd.parallel import batch_softmax
+        batch_softmax.enable(force=True)
     if a.dp_variant == "nocomm":
         class _Done:
             def wait(self):
@@ -62,7 +67,7 @@ t1 = time.perf_counter()
 torch.cuda.synchronize()
 t2 = time.perf_counter()
 mode = ("graph" if a.graph else "eager") + (f" + DP buckets ({len(ddp.buckets)}, 1-rank RCCL, {a.dp_variant})"
-                                            if ddp else "")
+                                            if ddp else "") + (" + shared batch softmax" if a.batch_softmax else "")
 print(f"B={a.batch} {mode}: issue {1000 * (t1 - t0) / a.steps:.3f} ms/step   complete {1000 * (t2 - t0) / a.steps:.3f} "
       "ms/step", flush=True)
 if os.environ.get("PBX_CPROFILE"):

@@ -10,7 +10,7 @@ mkdir -p tools/ubench/abl
 objs=""
 for f in "$src"/*.hip; do
   o="$d/$(basename "$f" .hip).o"
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=fast -fno-slp-vectorize -Wno-unused-result -I "$src" "$@" -c "$f" -o "$o" &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics -ffp-contract=fast-honor-pragmas -fno-slp-vectorize -Wno-unused-result -I "$src" "$@" -c "$f" -o "$o" &
   objs="$objs $o"
 done
 wait

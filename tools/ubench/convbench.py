@@ -51,6 +51,11 @@ fwd = lambda: _lib.call("pbx_conv_fwd3x", x.data_ptr(), fp.data_ptr(), fp.data_p
                         stt.data_ptr(), B, L, KS, dil, 0, 0, st)
 us = timeit(fwd)
 print(f"[{a.tag}] conv_fwd3   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+fwd5 = lambda: _lib.call("pbx_conv_fwd5x", x.data_ptr(), fp.data_ptr(), fp.data_ptr(), bias.data_ptr(),  # noqa: E731
+                         bias.data_ptr(), gb.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), s1.data_ptr(),
+                         stt.data_ptr(), B, L, KS, dil, 0, 0, st)
+us = timeit(fwd5)
+print(f"[{a.tag}] conv_fwd5   {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
 ds1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
 dx, dpn, dpw = (torch.empty_like(x) for _ in range(3))
 dg4 = lambda: _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(),  # noqa
