@@ -7,8 +7,6 @@
 //
 // (A persistent, software-pipelined forward -- the epilogue of tile i-1 inside the K loop of tile i --
 // lived here in rounds 3-4: equal in isolation, 3.3 % slower in the step; removed in round 5.)
-#include <stdlib.h>
-
 #include "mfma.h"
 
 using namespace pbx;
@@ -16,8 +14,10 @@ typedef unsigned short bf16_t;
 
 namespace {
 constexpr int CH = 128;
+constexpr int BM = 128;              // positions per tile
 constexpr int KS = 9;                // taps (the launcher refuses other sizes)
 constexpr int NI = KS * 8;           // K-steps per tile (taps x 16-channel blocks)
+constexpr int NPT = BM / 32;         // 32-position MFMA tiles per wave
 
 
 // ------------------------------------------------------------------------------------------------
@@ -48,15 +48,11 @@ struct FinArgs {
   float eps;
 };
 
-// BM: positions per tile (128: two workgroups per CU; 64: three, so that one workgroup's staging overlaps
-// another's MFMA loop more often)
-template <bool FIN, int BM>
-__global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
+template <bool FIN>
+__global__ void __launch_bounds__(256, 2) conv_dgrad4_kernel(
     const bf16_t* __restrict__ ds1, const bf16_t* __restrict__ gdn, const bf16_t* __restrict__ gdw,
     const bf16x8* __restrict__ ftn, const bf16x8* __restrict__ ftw, bf16_t* __restrict__ dx,
     bf16_t* __restrict__ dpre_n, bf16_t* __restrict__ dpre_w, int L, int dil, int ilo, int ihi, FinArgs fa) {
-  constexpr int NPT = BM / 32;         // 32-position MFMA tiles per wave
-  constexpr int NK = ((BM + 8) * 16 + 255) / 256;   // narrow-tile 16-B chunks per thread (FIN)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int T = (L + BM - 1) / BM;
   int tid0;
@@ -92,7 +88,7 @@ __global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
 
   // FIN: dS1 of the central rows (narrow-tile rows (tid >> 4) + 16 m - 4, channel chunk tid & 15) and
   // this thread's share of their column sums
-  uint4 keep[NK];
+  uint4 keep[9];
   float csum[8];
   float mean1 = 0.f, rstd1 = 0.f, m1 = 0.f, m2 = 0.f;
   if constexpr (FIN) {
@@ -163,11 +159,10 @@ __global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
     // registers; each thread converts its own chunks of `an` in place (dS1 -> dpre_n)
     const int nch = RN * 16;
 #pragma unroll
-    for (int mb = 0; mb < NK; mb += 3) {
+    for (int mb = 0; mb < 9; mb += 3) {
       uint4 pq[3];
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        if (mb + i >= NK) break;
         const int idx = tid + 256 * (mb + i);
         const int pos = pos0 - halo_n + (idx >> 4);
         pq[i] = *reinterpret_cast<const uint4*>(gdn + sbase + (size_t)min(max(pos, 0), L - 1) * CH + (idx & 15) * 8);
@@ -175,7 +170,6 @@ __global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const int m = mb + i;
-        if (m >= NK) break;
         const int idx = tid + 256 * m;
         const int j = idx >> 4, ch = idx & 15;
         const int pos = pos0 - halo_n + j;
@@ -310,7 +304,7 @@ __global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
     }
     // dx = dS1 (registers) + acc over the central rows
 #pragma unroll
-    for (int m = 0; m < NK; ++m) {
+    for (int m = 0; m < 9; ++m) {
       const int row = (tid >> 4) + 16 * m - halo_n, cc = tid & 15;
       if (row < 0 || row >= vrows) continue;
       float gv[8], o[8];
@@ -344,30 +338,10 @@ __global__ void __launch_bounds__(256, BM == 128 ? 2 : 3) conv_dgrad4_kernel(
 bool dgrad4_attr_set = false;
 }  // namespace
 
-// positions per data-gradient tile: 128 (two workgroups per CU) or 64 (three); PBX_DGRAD_BM selects
-static int dgrad_bm() {
-  static int bm = 0;
-  if (bm == 0) {
-    const char* e = getenv("PBX_DGRAD_BM");
-    bm = (e != nullptr && atoi(e) == 64) ? 64 : 128;
-  }
-  return bm;
-}
-
-int conv_dgrad4_lds(int dil, int BM) {
+int conv_dgrad4_lds(int dil) {
   const int a = (2 * BM + 8 * (1 + dil)) * 256;
   const int e = BM * CH * 4 + 4 * CH * 4;     // the fp32 dx tile + the FIN dgb partials
   return a > e ? a : e;
-}
-
-static void dgrad4_attrs() {
-  if (!dgrad4_attr_set) {
-    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<false, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<true, 128>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<false, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<true, 64>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
-    dgrad4_attr_set = true;
-  }
 }
 
 // KS = 9: gdn / gdw are the GELU'(pre) images the forward (pbx_conv_fwd3x / pbx_conv_fwd3t) stored.
@@ -376,15 +350,17 @@ static void dgrad4_attrs() {
 PBX_EXPORT int pbx_conv_dgrad4x(const void* ds1, const void* gdn, const void* gdw, const void* ftn, const void* ftw,
                                 void* dx, void* dpre_n, void* dpre_w, int B, int L, int KS_, int dil, int ilo, int ihi,
                                 hipStream_t st) {
-  const int BM = dgrad_bm();
-  const int lds = conv_dgrad4_lds(dil, BM);
+  const int lds = conv_dgrad4_lds(dil);
   if (KS_ != KS || dil < 1 || lds > 163840 || B < 1 || L < 1 || ilo < 0 || ihi < 0) return (int)hipErrorInvalidValue;
-  dgrad4_attrs();
+  if (!dgrad4_attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    dgrad4_attr_set = true;
+  }
   const int T = (L + BM - 1) / BM;
-  auto kern = BM == 128 ? conv_dgrad4_kernel<false, 128> : conv_dgrad4_kernel<false, 64>;
-  hipLaunchKernelGGL(kern, dim3(B * T), dim3(256),
-                     lds, st, (const bf16_t*)ds1, (const bf16_t*)gdn, (const bf16_t*)gdw, (const bf16x8*)ftn,
-                     (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, dil, ilo, ihi, FinArgs{});
+  hipLaunchKernelGGL(conv_dgrad4_kernel<false>, dim3(B * T), dim3(256), lds, st, (const bf16_t*)ds1,
+                     (const bf16_t*)gdn, (const bf16_t*)gdw, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx,
+                     (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, dil, ilo, ihi, FinArgs{});
   return pbx_launch_status();
 }
 
@@ -395,16 +371,19 @@ PBX_EXPORT int pbx_conv_dgrad4f(const void* dh1, const void* s1, const float* st
                                 int TS1, const float* g1, const void* gdn, const void* gdw, const void* ftn,
                                 const void* ftw, void* dx, void* dpre_n, void* dpre_w, float* dgb, int B, int L,
                                 int KS_, int dil, float eps, hipStream_t st) {
-  const int BM = dgrad_bm();
-  const int lds = conv_dgrad4_lds(dil, BM);
+  const int lds = conv_dgrad4_lds(dil);
   if (KS_ != KS || dil < 1 || lds > 163840 || B < 1 || L < 1 || T1 < 1 || BM1 < 1 || TS1 < 1)
     return (int)hipErrorInvalidValue;
-  dgrad4_attrs();
+  if (!dgrad4_attr_set) {
+    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    (void)hipFuncSetAttribute((const void*)conv_dgrad4_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 163840);
+    dgrad4_attr_set = true;
+  }
   const int T = (L + BM - 1) / BM;
   FinArgs fa{(const bf16_t*)dh1, (const bf16_t*)s1, st1, T1, BM1, sums1, TS1, g1, dgb, eps};
-  auto kern = BM == 128 ? conv_dgrad4_kernel<true, 128> : conv_dgrad4_kernel<true, 64>;
-  hipLaunchKernelGGL(kern, dim3(B * T), dim3(256),
-                     lds, st, nullptr, (const bf16_t*)gdn, (const bf16_t*)gdw, (const bf16x8*)ftn, (const bf16x8*)ftw,
-                     (bf16_t*)dx, (bf16_t*)dpre_n, (bf16_t*)dpre_w, L, dil, 0, 0, fa);
+  hipLaunchKernelGGL(conv_dgrad4_kernel<true>, dim3(B * T), dim3(256), lds, st, nullptr, (const bf16_t*)gdn,
+                     (const bf16_t*)gdw, (const bf16x8*)ftn, (const bf16x8*)ftw, (bf16_t*)dx, (bf16_t*)dpre_n,
+                     (bf16_t*)dpre_w, L, dil, 0, 0, fa);
   return pbx_launch_status();
 }
+
