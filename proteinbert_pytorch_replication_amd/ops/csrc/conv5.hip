@@ -29,8 +29,10 @@
 //   LDS: two x-tile buffers (168 rows x 256 B, swz256), the previous tile's pre-activations (2 x 32 KB row
 //   images), gb, biases: 151 KB.
 //
-// Outputs equal conv_fwd3's up to FMA-contraction ulps of s1 (tests/test_hip_conv_fwd5.py: the GELU' images
-// bitwise); the LayerNorm (mean, M2) tile partials come from the same stored values in another order.
+// s1 and the GELU' images equal conv_fwd3's bitwise (both keep the GELU product out of FMA contraction;
+// tests/test_hip_conv_fwd5.py); the LayerNorm (mean, M2) tile partials sum the same stored values in another
+// order.  The inline-asm loads' registers are checked against compiler copies by tools/asm_hazards.py
+// (tests/test_asm_hazards.py).
 #include "mfma.h"
 
 using namespace pbx;

@@ -79,6 +79,16 @@ def _p(t: Optional[torch.Tensor]):
 CONV_FWD5 = os.environ.get("PBX_CONV_FWD", "5") == "5"
 
 
+def conv_dgrad_fin(dh1, s1, st1, T1, BM1, sums1, TS1, g1, gdn, gdw, wtn, wtw, dx, dpn, dpw, dgb, B, L, KS, dil,
+                   stream):
+    """Conv data gradient with the LayerNorm-1 backward finalize fused in (whole sequences, conv_dgrad4<FIN>):
+    dx, both convs' dpre (for the weight gradient) and dgb += the column sums of dS1.  (A persistent form with
+    the staging pipelined into the K loop measured no better in the step: profiles/r6/conv_dgrad5_attempts.txt.)"""
+    _lib.call("pbx_conv_dgrad4f", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
+              TS1, g1.data_ptr(), gdn.data_ptr(), gdw.data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
+              dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), dgb.data_ptr(), B, L, KS, dil, LN_EPS, stream)
+
+
 def conv_fwd(x, wpn, wpw, bn, bw, gb, pre_n, pre_w, s1, stats, B, L, KS, dil, stream, xlo: int = 0,
              xhi: int = 0) -> None:
     """``pre_n``/``pre_w``: GELU'(pre-activation) outputs for the backward, or None (no backward).
@@ -419,9 +429,8 @@ class LocalBlockFn(torch.autograd.Function):
             dgb_ready()
         demb = None
         if fin:
-            _lib.call("pbx_conv_dgrad4f", dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, BM1, sums1.data_ptr(),
-                      TS1, g1.data_ptr(), pre_n.data_ptr(), pre_w.data_ptr(), wtn.data_ptr(), wtw.data_ptr(),
-                      dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), dgb.data_ptr(), B, L, KS, dil, LN_EPS, stream)
+            conv_dgrad_fin(dh1, s1, st1, T1, BM1, sums1, TS1, g1, pre_n, pre_w, wtn, wtw, dx, dpn, dpw, dgb, B, L,
+                           KS, dil, stream)
             dgb_ready()
         elif ctx.emb_grad:
             # first block, folded: no conv data gradient (the conv part of dE comes with the weight gradient)

@@ -1,4 +1,5 @@
-"""Time the conv kernels (conv_fwd3, csrc/conv2.hip; conv_dgrad4, csrc/conv4.hip; wgrad2, csrc/wgrad.hip)
+"""Time the conv kernels (conv_fwd3 / conv_fwd5, csrc/conv2.hip / conv5.hip; conv_dgrad4,
+csrc/conv4.hip; wgrad2, csrc/wgrad.hip)
 at the bench shape through their exported launchers (whole sequences: no context-parallel halo rows), with
 whatever library PBX_HIP_LIB names (a variant built by tools/ubench/build_flags.sh).
 
@@ -62,6 +63,18 @@ dg4 = lambda: _lib.call("pbx_conv_dgrad4x", ds1.data_ptr(), pre_n.data_ptr(), pr
                         ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(), dpw.data_ptr(), B, L, KS, dil, 0, 0, st)
 us = timeit(dg4)
 print(f"[{a.tag}] conv_dgrad4 {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
+# the FIN form (LN1 backward finalize fused in)
+dh1 = (torch.randn(B, L, C, device=dev) * 0.1).to(bf)
+g1 = torch.randn(L, C, device=dev) * 0.1 + 1.0
+T1 = (L + 127) // 128
+st1 = torch.stack([torch.zeros(B, T1, device=dev), torch.full((B, T1), 128.0 * C * 0.25, device=dev)], -1)
+sums1 = torch.randn(B, 4, 2, device=dev)
+dgb = torch.zeros(B, C, device=dev)
+fin_args = lambda: [dh1.data_ptr(), s1.data_ptr(), st1.data_ptr(), T1, 128, sums1.data_ptr(), 4, g1.data_ptr(),  # noqa
+                    pre_n.data_ptr(), pre_w.data_ptr(), ft.data_ptr(), ft.data_ptr(), dx.data_ptr(), dpn.data_ptr(),
+                    dpw.data_ptr(), dgb.data_ptr()]
+us = timeit(lambda: _lib.call("pbx_conv_dgrad4f", *fin_args(), B, L, KS, dil, 1e-5, st))
+print(f"[{a.tag}] conv_dgrad4<FIN> {us:8.1f} us  {flops / us / 1e6:7.1f} TFLOP/s", flush=True)
 slab = torch.empty(64 * 2 * KS * C * C, device=dev)
 bslab = torch.empty(64 * 2 * C, device=dev)
 dwn, dww = torch.zeros(C, C, KS, device=dev), torch.zeros(C, C, KS, device=dev)
