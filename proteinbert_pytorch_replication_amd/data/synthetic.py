@@ -123,7 +123,11 @@ class SyntheticUniRefGO:
             from ..ops import corrupt as corrupt_op
             out = corrupt_op.corrupt_batch(tokens, ann, self.corruption, seed=self.seed, step=1,
                                            step_dev=self.step_dev)
-            self.step_dev.add_(1)
+            if self.step_dev.is_cuda:
+                from ..ops import _lib
+                _lib.call("pbx_add_i64", self.step_dev.data_ptr(), 1, _lib.stream_ptr(self.step_dev.device))
+            else:
+                self.step_dev.add_(1)
             return out
         return corrupt_batch_torch(tokens, ann, self.corruption, self.generator)
 

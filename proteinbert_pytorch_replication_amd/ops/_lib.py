@@ -60,6 +60,10 @@ _SIGS = {
     "pbx_sumsq_flat": [_P, _I64, _P, _P, _P],
     "pbx_clip_scale_flat": [_P, _I64, _P, _F32, _P],
     "pbx_nonfinite_flag": [_P, _I64, _P, _P, _F32, _I32, _P],
+    "pbx_fill_flat": [_P, _I64, _F32, _P],
+    "pbx_add_scalar": [_P, _F32, _P],
+    "pbx_add_i64": [_P, _I64, _P],
+    "pbx_colsum_set": [_P, _I32, _I32, _P, _P, _P],
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -228,6 +228,7 @@ PBX_EXPORT int pbx_bias_gelu_bwd(const float* dout, const float* u, const float*
 // dst[c] += scale * sum_r src[r][c]   (scale: optional device scalar).  A block covers 32 columns with
 // 8 row-lanes (row r -> lane r % 8), the 8 partials are combined in LDS in fixed order
 // (deterministic); used to fold per-position partial gradients into the arena.
+template <bool SET>
 __global__ void __launch_bounds__(256) colsum_add_kernel(const float* __restrict__ src, int rows, int cols, int ld,
                                                          float* __restrict__ dst, const float* __restrict__ scale) {
   __shared__ float part[8][33];
@@ -248,13 +249,24 @@ __global__ void __launch_bounds__(256) colsum_add_kernel(const float* __restrict
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) s += part[k][cl];
-    dst[c] += scale != nullptr ? s * scale[0] : s;
+    const float v = scale != nullptr ? s * scale[0] : s;
+    if constexpr (SET) dst[c] = v;
+    else dst[c] += v;
   }
 }
 
 PBX_EXPORT int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st) {
   if (cols <= 0 || rows <= 0) return 0;
-  hipLaunchKernelGGL(colsum_add_kernel, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, cols, dst, scale);
+  hipLaunchKernelGGL(colsum_add_kernel<false>, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, cols, dst,
+                     scale);
+  return pbx_launch_status();
+}
+
+// dst[c] = scale * sum_r src[r][c] (no zero-fill of dst needed: the loss slots of the fused heads)
+PBX_EXPORT int pbx_colsum_set(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st) {
+  if (cols <= 0 || rows <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(colsum_add_kernel<true>, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, cols, dst,
+                     scale);
   return pbx_launch_status();
 }
 
@@ -302,6 +314,6 @@ PBX_EXPORT int pbx_colsum_add2(const float* src0, int cols0, float* dst0, const 
 PBX_EXPORT int pbx_colsum_add_ld(const float* src, int rows, int cols, int ld, float* dst, const float* scale,
                                  hipStream_t st) {
   if (cols <= 0 || rows <= 0 || ld < cols) return cols <= 0 || rows <= 0 ? 0 : (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(colsum_add_kernel, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, ld, dst, scale);
+  hipLaunchKernelGGL(colsum_add_kernel<false>, dim3((cols + 31) / 32), dim3(256), 0, st, src, rows, cols, ld, dst, scale);
   return pbx_launch_status();
 }

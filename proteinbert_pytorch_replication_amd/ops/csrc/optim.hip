@@ -187,3 +187,43 @@ PBX_EXPORT int pbx_clip_scale_flat(float* x, int64_t n, const float* sumsq, floa
   hipLaunchKernelGGL(clip_scale_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, sumsq, max_norm);
   return pbx_launch_status();
 }
+
+// x[0 .. n) = v (the gradient arena's per-step zero fill: 16-B stores, grid-stride)
+__global__ void __launch_bounds__(256) fill_flat_kernel(float* __restrict__ x, int64_t n, float v) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride)
+    reinterpret_cast<float4*>(x)[i] = make_float4(v, v, v, v);
+  const int64_t t = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n && blockIdx.x * blockDim.x + threadIdx.x < 4) x[t] = v;
+}
+
+PBX_EXPORT int pbx_fill_flat(float* x, int64_t n, float v, hipStream_t stream) {
+  if (n <= 0) return 0;
+  if (((uintptr_t)x & 15) != 0) return (int)hipErrorInvalidValue;
+  int64_t blocks = (n / 4 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(fill_flat_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, x, n, v);
+  return pbx_launch_status();
+}
+
+// *x += v on the device (the optimizer's step counter; one lane, a vector store)
+__global__ void __launch_bounds__(64) add_scalar_kernel(float* __restrict__ x, float v) {
+  if (threadIdx.x == 0) x[0] = x[0] + v;
+}
+
+PBX_EXPORT int pbx_add_scalar(float* x, float v, hipStream_t stream) {
+  hipLaunchKernelGGL(add_scalar_kernel, dim3(1), dim3(64), 0, stream, x, v);
+  return pbx_launch_status();
+}
+
+// *x += v for an int64 device counter (the synthetic-data step counter)
+__global__ void __launch_bounds__(64) add_i64_kernel(long long* __restrict__ x, long long v) {
+  if (threadIdx.x == 0) x[0] = x[0] + v;
+}
+
+PBX_EXPORT int pbx_add_i64(long long* x, long long v, hipStream_t stream) {
+  hipLaunchKernelGGL(add_i64_kernel, dim3(1), dim3(64), 0, stream, x, v);
+  return pbx_launch_status();
+}

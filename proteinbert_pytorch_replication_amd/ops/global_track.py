@@ -31,6 +31,7 @@ _lib.register("pbx_row_ln_bwd", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P,
 _lib.register("pbx_bias_gelu", [_P, _P, _P, _P, _I, _I, _P])
 _lib.register("pbx_bias_gelu_bwd", [_P, _P, _P, _P, _P, _I, _I, _P, _P])
 _lib.register("pbx_colsum_add", [_P, _I, _I, _P, _P, _P])
+_lib.register("pbx_colsum_set", [_P, _I, _I, _P, _P, _P])
 _lib.register("pbx_local_head3", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
 _lib.register("pbx_local_head3_tiles", [_I, _I])
 _lib.register("pbx_local_head_fused", [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P])
@@ -45,7 +46,7 @@ LHEAD_FUSED = True
 def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l: torch.Tensor, w_l: torch.Tensor,
                        loss_slot: torch.Tensor):
     """Local head + its CE term, reference semantics (softmax over the batch axis; ``csrc/lhead.hip``):
-    five coalesced passes over 16-sample x 32-position row tiles.  Adds the mean loss into ``loss_slot``
+    five coalesced passes over 16-sample x 32-position row tiles.  Writes the mean loss into ``loss_slot``
     and returns (dh [B, L, 128] bf16, dz [B*L, 32] bf16 -- dL/dlogits for the dWo GEMM -- and the
     per-tile bias-gradient partials [tiles, V])."""
     dev = h.device
@@ -66,7 +67,7 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
         _lib.call("pbx_local_head_fused", h.data_ptr(), wo.detach().contiguous().data_ptr(), bo.data_ptr(),
                   y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dz.data_ptr(),
                   dbo_part.data_ptr(), lparts.data_ptr(), B, L, V, st)
-        _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+        _lib.call("pbx_colsum_set", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
         return dh, dz, dbo_part
     nt = _lib.lib().pbx_local_head3_tiles(B, L)          # the kernel's tile grid (16 samples x 32 positions)
     nch = (B + 15) // 16
@@ -81,7 +82,7 @@ def local_head_forward(h: torch.Tensor, wo: torch.Tensor, bo: torch.Tensor, y_l:
               y_l.contiguous().data_ptr(), w_l.float().contiguous().data_ptr(), dh.data_ptr(), dz.data_ptr(),
               dbo_part.data_ptr(), lparts.data_ptr(), Z.data_ptr(), part[0].data_ptr(), part[1].data_ptr(),
               ms_t[0].data_ptr(), ms_t[1].data_ptr(), B, L, V, st)
-    _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+    _lib.call("pbx_colsum_set", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
     return dh, dz, dbo_part
 
 
@@ -114,7 +115,7 @@ def _local_head_dp(h, wo, bo, y_l, w_l, loss_slot):
     _lib.call("pbx_local_head3_c", Z.data_ptr(), ms_t[0].data_ptr(), ms_t[1].data_ptr(), y_c.data_ptr(),
               w_c.data_ptr(), wo_c.data_ptr(), bo.data_ptr(), dh.data_ptr(), dz.data_ptr(), dbo_part.data_ptr(),
               B, L, V, st)
-    _lib.call("pbx_colsum_add", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
+    _lib.call("pbx_colsum_set", lparts.data_ptr(), nt, 1, loss_slot.data_ptr(), None, st)
     return dh, dz, dbo_part
 
 
@@ -633,7 +634,7 @@ class HeadsLossFn(torch.autograd.Function):
         B, L, C = h.shape
         V = wo.shape[0]
         A = wa.shape[0]
-        loss = torch.zeros(2, dtype=F32, device=dev)
+        loss = torch.empty(2, dtype=F32, device=dev)        # each head writes its slot (pbx_colsum_set)
         if streams.ENABLED and dev.type == "cuda":
             # the GO head (GEMM + VALU-heavy BCE epilogue) on its own stream beside the memory-bound
             # local head; the loss sum waits for both
@@ -653,7 +654,7 @@ class HeadsLossFn(torch.autograd.Function):
         ctx.save_for_backward(dh, dzl, dbo_part, h, dz, dba, gx)
         ctx.params = (wo, bo, wa, ba)
         ctx.V = V
-        total = loss.sum()
+        total = loss_total(loss)
         ctx.mark_non_differentiable(loss)
         ctx.set_materialize_grads(False)
         return total, loss
@@ -702,7 +703,7 @@ def go_head_forward(g2_bf: torch.Tensor, wa: torch.Tensor, ba: torch.Tensor, y_g
                     w_g: torch.Tensor, loss_slot: torch.Tensor):
     """GO head + its BCE term (reference ``modules.py:286-293``, ``utils.py:294``) as ONE launch:
     z = g2 Wa^T + ba, sigmoid, BCE with the log clamp, weight, dz = dL/dz (bf16) and the bias-gradient
-    partials (``pbx_go_head_fused``); the mean loss is added into ``loss_slot`` (device scalar).
+    partials (``pbx_go_head_fused``); the mean loss is written into ``loss_slot`` (device scalar).
     Returns (dz [B, A] view of a column-padded buffer, bias-gradient partials [ceil(B/128), A], g2)."""
     dev = g2_bf.device
     st = _s(dev)
@@ -722,7 +723,7 @@ def go_head_forward(g2_bf: torch.Tensor, wa: torch.Tensor, ba: torch.Tensor, y_g
     _lib.call("pbx_go_head_fused", gx.data_ptr(), gx.stride(0), wab.data_ptr(), wab.stride(0), ba.data_ptr(),
               y.data_ptr(), A, _lib.ptr(wrow), _lib.ptr(wfull), dz.data_ptr(), dz_pad.stride(0), dba.data_ptr(),
               lparts.data_ptr(), B, A, gx.shape[1], st)
-    _lib.call("pbx_colsum_add", lparts.data_ptr(), lparts.numel(), 1, loss_slot.data_ptr(), None, st)
+    _lib.call("pbx_colsum_set", lparts.data_ptr(), lparts.numel(), 1, loss_slot.data_ptr(), None, st)
     return dz, dba, gx
 
 
@@ -759,6 +760,28 @@ def go_head_backward(dz, dba, g2_bf, wa, dwa_dst, dba_dst, scale=None) -> torch.
 
 
 _UNIT_LOSS_GRAD = [False]
+
+
+def loss_total(loss: torch.Tensor) -> torch.Tensor:
+    """loss[0] + loss[1] as a 0-d device tensor (one in-tree launch: the fixed-order column sum)."""
+    if loss.is_cuda:
+        total = torch.empty((), dtype=F32, device=loss.device)
+        _lib.call("pbx_colsum_set", loss.data_ptr(), loss.numel(), 1, total.data_ptr(), None, _s(loss.device))
+        return total
+    return loss.sum()
+
+
+_ONES = {}
+
+
+def unit_seed(t: torch.Tensor) -> torch.Tensor:
+    """A cached device 1.0 of ``t``'s shape / dtype: ``torch.autograd.backward(loss, unit_seed(loss))`` starts
+    the backward without the fill kernel autograd's implicit seed launches every step."""
+    key = (t.device, t.dtype, tuple(t.shape))
+    v = _ONES.get(key)
+    if v is None:
+        v = _ONES[key] = torch.ones(t.shape, dtype=t.dtype, device=t.device)
+    return v
 
 
 class unit_loss_grad:

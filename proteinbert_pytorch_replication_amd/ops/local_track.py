@@ -304,7 +304,7 @@ class LocalBlockFn(torch.autograd.Function):
         gb = gb.detach().float().contiguous()
         if x is None:
             x_ext, hlo = None, 0
-            emb_b = emb.detach().to(torch.bfloat16).contiguous()
+            emb_b = bf16_of(emb)                  # the optimizer-maintained bf16 mirror: no cast launch
             _lib.call("pbx_conv_fwd3t", tok.data_ptr(), emb_b.data_ptr(), wpn.data_ptr(), wpw.data_ptr(),
                       bn.data_ptr(), bw.data_ptr(), gb.data_ptr(), _p(pre_n), _p(pre_w), s1.data_ptr(),
                       st1.data_ptr(), B, L, KS, dil, stream)

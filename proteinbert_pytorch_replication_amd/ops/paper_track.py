@@ -25,8 +25,8 @@ import torch
 from . import _lib, streams
 from ..train.arena import notify_grads_ready
 from .gemm import gemm as _gemm
-from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward, mm32,
-                           addmm_into)
+from .global_track import (BF16, F32, _Grads, _UNIT_LOSS_GRAD, bf16_of, go_head_backward, go_head_forward,
+                           loss_total, mm32, addmm_into)
 from .local_track import (CH, conv_dgrad, conv_fwd, conv_tile, dwl_slab, pack_conv, _grad_dst, _wgrad,
                           _wgrad_tok, embed_fold_bwd, wgrad_tok_ok)
 
@@ -345,7 +345,7 @@ class PaperHeadsLossFn(torch.autograd.Function):
         B, L, C = h.shape
         V = wo.shape[0]
         A = wa.shape[0]
-        loss = torch.zeros(2, dtype=F32, device=dev)
+        loss = torch.empty(2, dtype=F32, device=dev)        # each head writes its slot (pbx_colsum_set)
         R = B * L
         hb = h.reshape(R, C)
         # one launch (csrc/phead.hip): logits, row softmax over V, weighted NLL, dZ, dh = dZ Wo, bias-gradient
@@ -360,7 +360,7 @@ class PaperHeadsLossFn(torch.autograd.Function):
         _lib.call("pbx_paper_head", hb.data_ptr(), wo.detach().float().contiguous().data_ptr(),
                   bo.detach().float().contiguous().data_ptr(), y.data_ptr(), wl.data_ptr(), dh.data_ptr(),
                   dzl.data_ptr(), dbo_part.data_ptr(), loss_part.data_ptr(), R, V, 1.0 / float(R), st)
-        _lib.call("pbx_colsum_add", loss_part.data_ptr(), parts, 1, loss.data_ptr(), None, st)
+        _lib.call("pbx_colsum_set", loss_part.data_ptr(), parts, 1, loss.data_ptr(), None, st)
         dbo = torch.zeros(V, dtype=F32, device=dev)
         _lib.call("pbx_colsum_add", dbo_part.data_ptr(), parts, V, dbo.data_ptr(), None, st)
         dwo32 = torch.empty((32, C), dtype=F32, device=dev)
@@ -371,7 +371,7 @@ class PaperHeadsLossFn(torch.autograd.Function):
         ctx.params = (wo, bo, wa, ba)
         ctx.mark_non_differentiable(loss)
         ctx.set_materialize_grads(False)
-        return loss.sum(), loss
+        return loss_total(loss), loss
 
     @staticmethod
     def backward(ctx, dtotal, _dparts):

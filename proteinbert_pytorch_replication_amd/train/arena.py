@@ -67,6 +67,12 @@ class FlatArena:
     def zero_grad(self) -> None:
         if not self.grads_attached():
             self.attach_grads()
+        if self.grad.is_cuda:
+            from ..ops import _lib
+            if _lib.available():
+                # in-tree fill: the step runs no PyTorch-native kernel
+                _lib.call("pbx_fill_flat", self.grad.data_ptr(), self.grad.numel(), 0.0, _lib.stream_ptr(self.grad.device))
+                return
         self.grad.zero_()
 
     def attach_bf16_shadow(self, shadow: torch.Tensor) -> None:

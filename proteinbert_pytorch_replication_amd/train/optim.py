@@ -99,7 +99,8 @@ class FusedAdam(torch.optim.Optimizer):
         if _hip_ok(a.data):
             if not torch.cuda.is_current_stream_capturing():
                 self.prepare()
-            self._step_dev.add_(1.0)
+            from ..ops import _lib
+            _lib.call("pbx_add_scalar", self._step_dev.data_ptr(), 1.0, _lib.stream_ptr(self._step_dev.device))
 
     @torch.no_grad()
     def step_range(self, start: int, end: int) -> None:

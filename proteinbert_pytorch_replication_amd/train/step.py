@@ -73,10 +73,10 @@ class PretrainStep:
         # device scalars (no host sync): the per-head losses of the last step, for the metrics
         self.last_parts = (l_local.detach(), l_global.detach())
         if self.model.resolved_backend(self.device) == "hip":
-            from ..ops.global_track import unit_loss_grad
+            from ..ops.global_track import unit_loss_grad, unit_seed
             from ..ops import streams
             with unit_loss_grad():
-                loss.backward()
+                torch.autograd.backward(loss, unit_seed(loss))
             streams.join()                      # conv weight gradients ran on the aux stream
         else:
             loss.backward()
