@@ -476,6 +476,7 @@ bool wgrad_tok_attr_set = false;
 }  // namespace
 
 extern "C" int pbx_colsum_add(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st);
+extern "C" int pbx_colsum_set(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st);
 
 // Rows of the per-workgroup slab pbx_wgrad_tok needs ([R][2][9][V][128] fp32).
 PBX_EXPORT int pbx_wgrad_tok_rows(int B, int L) {
@@ -504,8 +505,7 @@ PBX_EXPORT int pbx_wgrad_tok(const void* tok, const void* dy0, const void* dy1, 
   hipLaunchKernelGGL(wgrad_tok_kernel, dim3(R), dim3(512), 2 * buf, st, (const long long*)tok, (const bf16_t*)dy0,
                      (const bf16_t*)dy1, slab, B, L, dil1, R, V, buf);
   const int cols = 2 * KS * V * CH;
-  (void)hipMemsetAsync(S, 0, (size_t)cols * sizeof(float), st);
-  int rc = pbx_colsum_add(slab, R, cols, S, nullptr, st);
+  int rc = pbx_colsum_set(slab, R, cols, S, nullptr, st);
   if (rc != 0) return rc;
   hipLaunchKernelGGL(wgrad_tok_finish_kernel, dim3(2 * CH), dim3(128), 0, st, S, E, dw0, dw1, db0, db1, V, W0, W1,
                      dEslab);
