@@ -258,38 +258,42 @@ __global__ void __launch_bounds__(256) colsum_add_kernel(const float* __restrict
 // The same fold over 4 adjacent columns per thread (16-B loads, 128 columns per workgroup) with 8 rows in
 // flight per thread; per column the additions are exactly colsum_add_kernel's (a0: rows rl + 16 i, a1: rows
 // rl + 8 + 16 i, then the 8 row-lane partials in order), so the two give bitwise-equal results.
+__device__ __forceinline__ void add4(float4& a, const float4& v) { a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w; }
+
+// this thread's partial (row lane rl of 8) of column quad c, in colsum_add_kernel's order
+__device__ __forceinline__ float4 fold4_partial(const float4* __restrict__ src, int rows, int cols4, int c, int rl) {
+  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
+  int r = rl;
+  for (; r + 56 < rows; r += 64) {
+    float4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(r + 8 * u) * cols4 + c];
+#pragma unroll
+    for (int u = 0; u < 8; u += 2) {
+      add4(a0, v[u]);
+      add4(a1, v[u + 1]);
+    }
+  }
+  for (; r + 8 < rows; r += 16) {
+    add4(a0, src[(size_t)r * cols4 + c]);
+    add4(a1, src[(size_t)(r + 8) * cols4 + c]);
+  }
+  for (; r < rows; r += 8) add4(a0, src[(size_t)r * cols4 + c]);
+  return make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+}
+
 template <bool SET>
 __global__ void __launch_bounds__(256) colsum_add4_kernel(const float4* __restrict__ src, int rows, int cols4,
                                                           float4* __restrict__ dst, const float* __restrict__ scale) {
   __shared__ float4 part[8][32];
   const int cl = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int c = blockIdx.x * 32 + cl;
-  float4 a0 = make_float4(0.f, 0.f, 0.f, 0.f), a1 = a0;
-  auto add = [](float4& a, const float4& v) { a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w; };
-  if (c < cols4) {
-    int r = rl;
-    for (; r + 56 < rows; r += 64) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(r + 8 * u) * cols4 + c];
-#pragma unroll
-      for (int u = 0; u < 8; u += 2) {
-        add(a0, v[u]);
-        add(a1, v[u + 1]);
-      }
-    }
-    for (; r + 8 < rows; r += 16) {
-      add(a0, src[(size_t)r * cols4 + c]);
-      add(a1, src[(size_t)(r + 8) * cols4 + c]);
-    }
-    for (; r < rows; r += 8) add(a0, src[(size_t)r * cols4 + c]);
-  }
-  part[rl][cl] = make_float4(a0.x + a1.x, a0.y + a1.y, a0.z + a1.z, a0.w + a1.w);
+  part[rl][cl] = c < cols4 ? fold4_partial(src, rows, cols4, c, rl) : make_float4(0.f, 0.f, 0.f, 0.f);
   __syncthreads();
   if (rl == 0 && c < cols4) {
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) add(s, part[k][cl]);
+    for (int k = 0; k < 8; ++k) add4(s, part[k][cl]);
     if (scale != nullptr) {
       const float f = scale[0];
       s = make_float4(s.x * f, s.y * f, s.z * f, s.w * f);
@@ -298,7 +302,7 @@ __global__ void __launch_bounds__(256) colsum_add4_kernel(const float4* __restri
       dst[c] = s;
     } else {
       float4 d = dst[c];
-      add(d, s);
+      add4(d, s);
       dst[c] = d;
     }
   }
@@ -326,6 +330,27 @@ PBX_EXPORT int pbx_colsum_add(const float* src, int rows, int cols, float* dst, 
 PBX_EXPORT int pbx_colsum_set(const float* src, int rows, int cols, float* dst, const float* scale, hipStream_t st) {
   if (cols <= 0 || rows <= 0) return (int)hipErrorInvalidValue;
   return colsum_launch<true>(src, rows, cols, dst, scale, st);
+}
+
+// dst[g][c] = sum_r src[g][r][c] over r = 0 .. R-1 in order (one thread per (g, c); loads coalesced over c):
+// the per-group partial folds of paper semantics (dgb over position tiles, dq over split-L chunks)
+__global__ void __launch_bounds__(256) group_colsum_kernel(const float* __restrict__ src, int G, int R, int C,
+                                                           float* __restrict__ dst) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)G * C) return;
+  const long g = i / C;
+  const int c = (int)(i - g * C);
+  const float* p = src + (size_t)g * R * C + c;
+  float a = 0.f;
+  for (int r = 0; r < R; ++r) a += p[(size_t)r * C];
+  dst[i] = a;
+}
+
+PBX_EXPORT int pbx_group_colsum(const float* src, int G, int R, int C, float* dst, hipStream_t st) {
+  if (G < 1 || R < 1 || C < 1) return (int)hipErrorInvalidValue;
+  const long n = (long)G * C;
+  hipLaunchKernelGGL(group_colsum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, src, G, R, C, dst);
+  return pbx_launch_status();
 }
 
 // two folds with the same row count in one launch (a weight slab and its bias slab): blocks < ceil(cols0 / 32)

@@ -14,7 +14,7 @@ flat-arena ``.grad`` views.
 from __future__ import annotations
 
 import ctypes
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -219,6 +219,11 @@ class _Grads:
             if g is not None and g.is_contiguous() and g.dtype == F32:
                 self.dst.append(g)
                 self.direct.append(True)
+            elif p is not None and not p.requires_grad:
+                # a constant (paper semantics' unit attention weight): the kernels' writes go to scratch
+                # nobody reads -- no zero-fill, no gradient returned
+                self.dst.append(_scratch_like(p))
+                self.direct.append(False)
             else:
                 self.dst.append(None if p is None else torch.zeros(p.shape, dtype=F32, device=p.device))
                 self.direct.append(False)
@@ -227,7 +232,20 @@ class _Grads:
         direct = [p for p, d in zip(self.params, self.direct) if d and p is not None]
         if direct:
             notify_grads_ready(direct)
-        return [None if (d or p is None) else g for p, g, d in zip(self.params, self.dst, self.direct)]
+        return [None if (d or p is None or not p.requires_grad) else g
+                for p, g, d in zip(self.params, self.dst, self.direct)]
+
+
+_SCRATCH: Dict[Tuple, torch.Tensor] = {}
+
+
+def _scratch_like(p: torch.Tensor) -> torch.Tensor:
+    key = (tuple(p.shape), str(p.device))
+    t = _SCRATCH.get(key)
+    if t is None:
+        t = torch.empty(p.shape, dtype=F32, device=p.device)
+        _SCRATCH[key] = t
+    return t
 
 
 _lib.register("pbx_ann_supported", [_I, _I, _I])

@@ -44,6 +44,18 @@ _lib.register("pbx_sg_query_dg", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_sg_query_dwq", [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P])
 _lib.register("pbx_sg_query_ws", [_I, _I, _I, _I])
 _lib.register("pbx_pa_wimg", [_P, _P, _P, _I, _I, _I, _I, _P])
+_lib.register("pbx_group_colsum", [_P, _I, _I, _I, _P, _P])
+
+
+def group_colsum(t: torch.Tensor) -> torch.Tensor:
+    """``[G, R, C]`` fp32 -> ``[G, C]``, summed over R in order (``csrc/glob.hip``)."""
+    G, R, C = t.shape
+    if t.device.type != "cuda":
+        return t.sum(dim=1)
+    t = t.contiguous()
+    out = torch.empty((G, C), dtype=F32, device=t.device)
+    _lib.call("pbx_group_colsum", t.data_ptr(), G, R, C, out.data_ptr(), _lib.stream_ptr(t.device))
+    return out
 _lib.register("pbx_pa_dwkv_add", [_P, _P, _P, _I, _I, _I, _I, _P])
 
 
@@ -199,7 +211,7 @@ class PaperBlockFn(torch.autograd.Function):
                           o.data_ptr(), dO.data_ptr(), dpre.data_ptr(), dq_part.data_ptr(), B, L, H, K, VD, ns,
                           stream)
                 dh2_att = [mm32(dpre, wsave.t()).to(BF16), None]                          # [R, C] bf16
-            dqs = dq_part.sum(dim=1).view(B, H, K)
+            dqs = group_colsum(dq_part).view(B, H, K)
             if cp is not None:
                 cp.all_reduce_(dqs)             # q is replicated: its gradient sums every shard's positions
             G = gf32.shape[1]
@@ -239,7 +251,7 @@ class PaperBlockFn(torch.autograd.Function):
                   g1.data_ptr(), be1.data_ptr(), wl_b.data_ptr(), bl.data_ptr(), g2.data_ptr(), ds1.data_ptr(),
                   dgbp.data_ptr(), dg2.data_ptr(), dbe2.data_ptr(), dg1.data_ptr(), dbe1.data_ptr(), dwl.data_ptr(),
                   dbl.data_ptr(), *dwl_slab(dev), B, L, stream)
-        dgb = dgbp.sum(dim=1)
+        dgb = group_colsum(dgbp)
         if cp is not None:
             cp.all_reduce_(dgb)                 # gb is replicated: its gradient sums every shard's positions
         dpn, dpw = torch.empty_like(x), torch.empty_like(x)

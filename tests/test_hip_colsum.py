@@ -30,3 +30,18 @@ def test_colsum_vector_path_bitwise(rows, cols, fn):
     if fn == "pbx_colsum_add":
         ref = ref + init.double()
     assert torch.allclose(dst_v.double(), ref, rtol=1e-5, atol=1e-4 * (rows ** 0.5))
+
+
+
+@pytest.mark.parametrize("G,R,C", [(1024, 16, 128), (4096, 2, 64), (3, 1, 5)])
+def test_group_colsum_in_order(G, R, C):
+    from proteinbert_pytorch_replication_amd.ops.paper_track import group_colsum
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(G + R + C)
+    src = torch.randn(G, R, C, device=dev, generator=g)
+    out = group_colsum(src)
+    ref = torch.zeros(G, C, device=dev)
+    for r in range(R):                   # the kernel's order: r = 0 .. R-1, fp32
+        ref = ref + src[:, r]
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
