@@ -373,8 +373,8 @@ class PaperHeadsLossFn(torch.autograd.Function):
                   bo.detach().float().contiguous().data_ptr(), y.data_ptr(), wl.data_ptr(), dh.data_ptr(),
                   dzl.data_ptr(), dbo_part.data_ptr(), loss_part.data_ptr(), R, V, 1.0 / float(R), st)
         _lib.call("pbx_colsum_set", loss_part.data_ptr(), parts, 1, loss.data_ptr(), None, st)
-        dbo = torch.zeros(V, dtype=F32, device=dev)
-        _lib.call("pbx_colsum_add", dbo_part.data_ptr(), parts, V, dbo.data_ptr(), None, st)
+        dbo = torch.empty(V, dtype=F32, device=dev)
+        _lib.call("pbx_colsum_set", dbo_part.data_ptr(), parts, V, dbo.data_ptr(), None, st)
         dwo32 = torch.empty((32, C), dtype=F32, device=dev)
         _gemm(dzl, hb, dwo32, ta=True, tb=False)                                            # K = B*L: split-K
         dwo = dwo32[:V]
@@ -399,7 +399,9 @@ class PaperHeadsLossFn(torch.autograd.Function):
         else:
             s = dtotal.reshape(1).to(F32).contiguous()
             dh_s = (dh.float() * s.reshape(())).to(dh.dtype)
-        dwo_d.add_(dwo if s is None else dwo * s)
-        dbo_d.add_(dbo if s is None else dbo * s)
+        # dst += s * src as one-row folds (in-tree, csrc/glob.hip)
+        st = _lib.stream_ptr(dh.device)
+        _lib.call("pbx_colsum_add", dwo.data_ptr(), 1, dwo.numel(), dwo_d.data_ptr(), _lib.ptr(s), st)
+        _lib.call("pbx_colsum_add", dbo.data_ptr(), 1, dbo.numel(), dbo_d.data_ptr(), _lib.ptr(s), st)
         dg2 = go_head_backward(dz, dba, g2_bf, wa, dwa_d, dba_d, s)
         return (dh_s, dg2, None, *gr.finish(), None, None, None, None)
