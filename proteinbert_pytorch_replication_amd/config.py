@@ -125,13 +125,14 @@ PRESETS: Dict[str, RunConfig] = {
                           num_heads=4, num_blocks=2),
         kernel=KernelConfig(backend="torch", dtype="fp32"),
         train=TrainConfig(batch_size=4)),
-    # Per-GPU batches are sized for throughput on a 288 GB MI355X (5.9 GiB peak at 1024 in round 5): at 256
-    # sequences many fused kernels still run only 1-2 work items per wave (latency-bound); 512 fills the chip,
-    # and 1024 amortises the step's fixed part (weight-gradient reductions, the optimizer, launch tails).
-    # Round-5 same-box sweep: B=1024 102.4k, 1536 103.8k, 2048 104.4k seq/s (profiles/r5/batch_sweep.txt).
+    # Per-GPU batches are sized for throughput on a 288 GB MI355X: at 256 sequences many fused kernels still
+    # run only 1-2 work items per wave (latency-bound); 512 fills the chip, and larger batches amortise the
+    # step's fixed part (weight-gradient folds, the optimizer, the first block's tail, launch latency).
+    # Round-6 same-box sweep (profiles/r6/batch_sweep.txt): B=1024 98.2k / 98.9k, 1536 100.4k, 2048 101.7k /
+    # 101.7k seq/s (+3.2 %) at 11.4 GiB peak -- 4 % of the HBM; round 5: +2 % (profiles/r5/batch_sweep.txt).
     "cfg2_paper_l512": RunConfig(
         name="cfg2_paper_l512", model=_paper_model(512),
-        train=TrainConfig(batch_size=1024)),
+        train=TrainConfig(batch_size=2048)),
     "cfg3_paper_l1024_dp8": RunConfig(
         name="cfg3_paper_l1024_dp8", model=_paper_model(1024),
         train=TrainConfig(batch_size=256)),
