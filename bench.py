@@ -51,7 +51,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: preset)")
     ap.add_argument("--seq-len", type=int, default=None)
-    ap.add_argument("--preset", default=None, help="config preset (default: cfg2_paper_l512, or "
+    ap.add_argument("--preset", default=None, help="config preset (default: cfg2_paper_l512; "
+                    "cfg3_paper_l1024_dp8 / cfg4_long_l4096_dp8 with --seq-len 1024 / 4096; "
                     "cfg5_finetune_ss_l512_dp8 with --mode finetune)")
     ap.add_argument("--mode", default="pretrain", choices=["pretrain", "finetune"],
                     help="pretrain: the headline step; finetune: BASELINE cfg 5, frozen encoder + per-residue "
@@ -110,7 +111,12 @@ def main():
         hiplib.set_gelu(a.gelu)
     info = pdist.init_distributed()
     dev = info.device
-    cfg = get_preset(a.preset or ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else "cfg2_paper_l512"))
+    preset = a.preset
+    if preset is None:
+        # the BASELINE preset of this mode / sequence length (its per-GPU batch), cfg 2 otherwise
+        preset = ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else
+                  {1024: "cfg3_paper_l1024_dp8", 4096: "cfg4_long_l4096_dp8"}.get(a.seq_len, "cfg2_paper_l512"))
+    cfg = get_preset(preset)
     mcfg = cfg.model
     L = a.seq_len or mcfg.sequences_length
     B = a.batch or cfg.train.batch_size

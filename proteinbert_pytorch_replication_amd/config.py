@@ -133,15 +133,18 @@ PRESETS: Dict[str, RunConfig] = {
     "cfg2_paper_l512": RunConfig(
         name="cfg2_paper_l512", model=_paper_model(512),
         train=TrainConfig(batch_size=2048)),
+    # The other GPU configs get the same ~1M tokens per GPU and step (11.2 GiB peak); round-6 one-box sweeps
+    # (profiles/r6/batch_sweep.txt): L=1024 B=256 46.8k -> 1024 53.7k seq/s, L=4096 B=64 11.0k -> 256 13.1k,
+    # fine-tune B=512 250k -> 2048 297k.
     "cfg3_paper_l1024_dp8": RunConfig(
         name="cfg3_paper_l1024_dp8", model=_paper_model(1024),
-        train=TrainConfig(batch_size=256)),
+        train=TrainConfig(batch_size=1024)),
     "cfg4_long_l4096_dp8": RunConfig(
         name="cfg4_long_l4096_dp8", model=_paper_model(4096),
-        train=TrainConfig(batch_size=64)),
+        train=TrainConfig(batch_size=256)),
     "cfg5_finetune_ss_l512_dp8": RunConfig(
         name="cfg5_finetune_ss_l512_dp8", model=_paper_model(512),
-        train=TrainConfig(batch_size=512)),
+        train=TrainConfig(batch_size=2048)),
     # the reference's own smoke driver (dummy_tests.py:102-118)
     "dummy_tests": RunConfig(
         name="dummy_tests", model=_paper_model(256),
