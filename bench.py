@@ -76,6 +76,13 @@ def parse():
     return ap.parse_args()
 
 
+def default_preset(mode: str, seq_len) -> str:
+    """The BASELINE preset (and so the per-GPU batch) of this mode / sequence length; cfg 2 otherwise."""
+    if mode == "finetune":
+        return "cfg5_finetune_ss_l512_dp8"
+    return {1024: "cfg3_paper_l1024_dp8", 4096: "cfg4_long_l4096_dp8"}.get(seq_len, "cfg2_paper_l512")
+
+
 def _free_port() -> int:
     import socket
     with socket.socket() as s:
@@ -111,12 +118,7 @@ def main():
         hiplib.set_gelu(a.gelu)
     info = pdist.init_distributed()
     dev = info.device
-    preset = a.preset
-    if preset is None:
-        # the BASELINE preset of this mode / sequence length (its per-GPU batch), cfg 2 otherwise
-        preset = ("cfg5_finetune_ss_l512_dp8" if a.mode == "finetune" else
-                  {1024: "cfg3_paper_l1024_dp8", 4096: "cfg4_long_l4096_dp8"}.get(a.seq_len, "cfg2_paper_l512"))
-    cfg = get_preset(preset)
+    cfg = get_preset(a.preset or default_preset(a.mode, a.seq_len))
     mcfg = cfg.model
     L = a.seq_len or mcfg.sequences_length
     B = a.batch or cfg.train.batch_size

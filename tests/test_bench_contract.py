@@ -64,3 +64,21 @@ def test_bench_rejects_world_size_mismatch():
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
     assert r.returncode == 2 and "WORLD_SIZE" in r.stderr
     assert not _json_lines(r.stdout)
+
+
+def test_default_presets_size_batches_per_length():
+    """Without --preset the bench takes the BASELINE preset of the mode / sequence length: ~1M tokens per
+    GPU and step (cfg 2: 2048 x 512, cfg 3: 1024 x 1024, cfg 4: 256 x 4096, cfg 5 fine-tune: 2048 x 512)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from proteinbert_pytorch_replication_amd.config import get_preset
+    got = {k: get_preset(bench.default_preset(*k)) for k in [("pretrain", None), ("pretrain", 512),
+                                                             ("pretrain", 1024), ("pretrain", 4096),
+                                                             ("finetune", None)]}
+    assert got[("pretrain", None)].name == got[("pretrain", 512)].name == "cfg2_paper_l512"
+    assert got[("pretrain", 1024)].name == "cfg3_paper_l1024_dp8"
+    assert got[("pretrain", 4096)].name == "cfg4_long_l4096_dp8"
+    assert got[("finetune", None)].name == "cfg5_finetune_ss_l512_dp8"
+    for (mode, L), cfg in got.items():
+        tokens = cfg.train.batch_size * (L or cfg.model.sequences_length)
+        assert tokens == 2 ** 20, (mode, L, tokens)
